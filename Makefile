@@ -1,0 +1,40 @@
+# Top-level build: libcmsbwt.so (HIP, gfx950), the cmsbwt CLI, and the oracle
+# (test infrastructure).  Outputs stay in-tree so they travel to the GPU box.
+HIPCC ?= /opt/rocm/bin/hipcc
+ARCH ?= gfx950
+SRC := cms-bwt_amd/csrc
+OUT := cms-bwt_amd/build
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-function
+HOSTFLAGS := -O3 -std=c++17 -fPIC -Wall
+
+OBJS := $(OUT)/engine.o $(OUT)/ms_walk.o $(OUT)/merge.o $(OUT)/synth.o $(OUT)/host_index.o $(OUT)/host_reader.o
+HDRS := $(wildcard $(SRC)/*.h) include/cmsbwt.h
+
+all: lib cli oracle
+
+lib: $(OUT)/libcmsbwt.so
+cli: $(OUT)/cmsbwt
+
+$(OUT):
+	mkdir -p $(OUT)
+
+$(OUT)/%.o: $(SRC)/%.hip $(HDRS) | $(OUT)
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(OUT)/host_%.o: $(SRC)/host_%.cpp $(HDRS) | $(OUT)
+	g++ $(HOSTFLAGS) -c -o $@ $<
+
+$(OUT)/libcmsbwt.so: $(OBJS)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJS)
+
+$(OUT)/cmsbwt: $(SRC)/cli_main.cpp $(OUT)/libcmsbwt.so include/cmsbwt.h
+	g++ $(HOSTFLAGS) -o $@ $< -L$(OUT) -lcmsbwt -Wl,-rpath,'$$ORIGIN'
+
+oracle:
+	$(MAKE) -C oracle
+
+clean:
+	rm -rf $(OUT)
+	$(MAKE) -C oracle clean
+
+.PHONY: all lib cli oracle clean

@@ -1,0 +1,269 @@
+"""cmsbwt — Python mirror of the CMS-BWT operator surface over libcmsbwt.so.
+
+The reference (fmasillo/CMS-BWT) exposes one entry point,
+``computeBWT(Args, ref, coll)`` (CMS-BWT.h:69, CMS-BWT-functions.cpp:1788),
+plus the ``cmsbwt`` CLI (main.cpp).  This module binds the C ABI declared in
+``include/cmsbwt.h`` with ctypes and keeps the reference's names:
+
+* :class:`Args`                  — utils.h:8-14 (filename/outname/format/buffer/prefixLength)
+* :func:`computeBWT`             — CMS-BWT-functions.cpp:1788, raises instead of ``exit()``
+* :class:`Engine`                — stage-level access (initialize_reference, ms_walk,
+                                    merge, write) on one HIP device
+
+The HIP library is mandatory: importing works without a GPU, but every
+compute call goes through ``libcmsbwt.so`` and fails loudly if the library or
+a device is missing.  There is no CPU fallback in this package.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from dataclasses import dataclass, field
+from typing import Optional
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "libcmsbwt.so")
+
+CMSBWT_OK = 0
+CMSBWT_EIO = 1
+CMSBWT_EARG = 2
+CMSBWT_EINPUT = 3
+CMSBWT_EDEVICE = 4
+CMSBWT_ELIMIT = 5
+CMSBWT_EORDER = 6
+UINT64_MAX = (1 << 64) - 1
+
+ARRAYS = {  # name -> numpy dtype, as dumped by the oracle
+    "h_start": "u4", "h_pos": "u4", "h_len": "u4", "h_smaller": "u1", "h_lchar": "u1",
+    "h_isa": "u4", "h_tonext": "u4", "h_nexthead": "u2", "bucket": "i8",
+    "rank2head": "i4", "head2rank": "i4", "bwtheads": "u1", "counters": "u8",
+}
+
+
+class CmsBwtError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"cmsbwt error {code}: {msg}")
+        self.code = code
+
+
+class _Args(ctypes.Structure):
+    _fields_ = [("prefix", ctypes.c_uint64), ("buffer_gb", ctypes.c_uint32), ("rle", ctypes.c_int32),
+                ("outname", ctypes.c_char_p), ("device", ctypes.c_int32), ("verbose", ctypes.c_int32)]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint64) for k in (
+        "n", "sn", "ndocs", "chars", "heads", "positions", "keys", "rank", "current_sum",
+        "counter_bad", "counter_good", "counter_nothing", "runs", "symbols", "order_violations")] + \
+        [(k, ctypes.c_double) for k in (
+            "t_index_s", "t_upload_s", "t_ms_walk_s", "t_merge_s", "t_write_s", "ms_walk_kernel_ms")]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def library_path() -> str:
+    return _LIB_PATH
+
+
+def load_library() -> ctypes.CDLL:
+    """Load libcmsbwt.so (built by ``make lib``); raises if it is missing."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise CmsBwtError(CMSBWT_EDEVICE, f"{_LIB_PATH} not built (run `make lib` or __graft_entry__.build())")
+    lib = ctypes.CDLL(_LIB_PATH)
+    P, U64, I32, VP = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p
+    sig = {
+        "cmsbwt_run": (I32, [ctypes.POINTER(_Args), ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Stats)]),
+        "cmsbwt_ctx_create": (I32, [I32, ctypes.POINTER(P)]),
+        "cmsbwt_ctx_destroy": (None, [P]),
+        "cmsbwt_last_error": (ctypes.c_char_p, [P]),
+        "cmsbwt_load_reference_file": (I32, [P, ctypes.c_char_p]),
+        "cmsbwt_load_reference": (I32, [P, VP, U64]),
+        "cmsbwt_load_collection_file": (I32, [P, ctypes.c_char_p, U64]),
+        "cmsbwt_load_collection": (I32, [P, VP, VP, U64]),
+        "cmsbwt_load_collection_synth": (I32, [P, U64, U64, U64, ctypes.c_double, I32]),
+        "cmsbwt_ms_walk": (I32, [P]),
+        "cmsbwt_merge": (I32, [P, I32]),
+        "cmsbwt_step": (I32, [P, I32]),
+        "cmsbwt_get_stats": (I32, [P, ctypes.POINTER(Stats)]),
+        "cmsbwt_num_runs": (U64, [P]),
+        "cmsbwt_copy_runs": (I32, [P, VP, U64]),
+        "cmsbwt_write_output": (I32, [P, ctypes.c_char_p, I32]),
+        "cmsbwt_copy_array": (I32, [P, ctypes.c_char_p, VP, ctypes.POINTER(U64)]),
+        "cmsbwt_host_read_collection": (I32, [ctypes.c_char_p, U64, VP, U64, ctypes.POINTER(U64), VP, U64,
+                                              ctypes.POINTER(U64), ctypes.POINTER(U64)]),
+        "cmsbwt_host_suffix_array": (I32, [VP, U64, VP]),
+    }
+    for name, (res, args) in sig.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+EXPORTED = [
+    "cmsbwt_run", "cmsbwt_ctx_create", "cmsbwt_ctx_destroy", "cmsbwt_last_error",
+    "cmsbwt_load_reference_file", "cmsbwt_load_reference", "cmsbwt_load_collection_file",
+    "cmsbwt_load_collection", "cmsbwt_load_collection_synth", "cmsbwt_ms_walk", "cmsbwt_merge",
+    "cmsbwt_step", "cmsbwt_get_stats", "cmsbwt_num_runs", "cmsbwt_copy_runs", "cmsbwt_write_output",
+    "cmsbwt_copy_array", "cmsbwt_host_read_collection", "cmsbwt_host_suffix_array",
+]
+
+
+@dataclass
+class Args:
+    """utils.h:8-14."""
+    filename: str = ""
+    outname: str = ""
+    format: bool = False          # -r : run-length encoded output
+    buffer: int = 2               # -b
+    prefixLength: int = UINT64_MAX  # -p
+    device: int = 0
+    verbose: bool = False
+
+
+def computeBWT(arg: Args, refFileName: str, collFileName: str) -> Stats:
+    """CMS-BWT-functions.cpp:1788-1797 — writes <outname>.rl_bwt|.bwt and .log.
+
+    Raises :class:`CmsBwtError` where the reference would ``exit()``."""
+    lib = load_library()
+    out = arg.outname or arg.filename
+    a = _Args(arg.prefixLength, arg.buffer, 1 if arg.format else 0, out.encode(), arg.device,
+              1 if arg.verbose else 0)
+    st = Stats()
+    rc = lib.cmsbwt_run(ctypes.byref(a), refFileName.encode(), collFileName.encode(), ctypes.byref(st))
+    if rc != CMSBWT_OK:
+        raise CmsBwtError(rc, f"computeBWT failed, see {out}.log")
+    return st
+
+
+class Engine:
+    """One HIP device context; stages of the hot path callable one by one."""
+
+    def __init__(self, device: int = 0):
+        self._lib = load_library()
+        p = ctypes.c_void_p()
+        rc = self._lib.cmsbwt_ctx_create(device, ctypes.byref(p))
+        if rc != CMSBWT_OK:
+            raise CmsBwtError(rc, f"no usable HIP device {device}")
+        self._ctx = p
+
+    def close(self):
+        if self._ctx:
+            self._lib.cmsbwt_ctx_destroy(self._ctx)
+            self._ctx = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _chk(self, rc: int):
+        if rc != CMSBWT_OK:
+            raise CmsBwtError(rc, self._lib.cmsbwt_last_error(self._ctx).decode(errors="replace"))
+
+    # initialize_reference (FN:151-310)
+    def initialize_reference(self, path: str):
+        self._chk(self._lib.cmsbwt_load_reference_file(self._ctx, path.encode()))
+
+    def load_reference_bytes(self, ref: bytes):
+        buf = ctypes.create_string_buffer(ref, len(ref))
+        self._chk(self._lib.cmsbwt_load_reference(self._ctx, buf, len(ref)))
+
+    def load_collection_file(self, path: str, prefix: int = UINT64_MAX):
+        self._chk(self._lib.cmsbwt_load_collection_file(self._ctx, path.encode(), prefix))
+
+    def load_collection(self, docs):
+        import numpy as np
+        text = b"".join(docs)
+        off = np.zeros(len(docs) + 1, dtype=np.uint64)
+        off[1:] = np.cumsum([len(d) for d in docs])
+        buf = ctypes.create_string_buffer(text, max(1, len(text)))
+        self._chk(self._lib.cmsbwt_load_collection(self._ctx, buf, off.ctypes.data, len(docs)))
+
+    def load_synth(self, seed: int, copy_begin: int, ncopies: int, p: float, leading_empty_doc: bool = True):
+        self._chk(self._lib.cmsbwt_load_collection_synth(self._ctx, seed, copy_begin, ncopies, p,
+                                                         1 if leading_empty_doc else 0))
+
+    def ms_walk(self):
+        self._chk(self._lib.cmsbwt_ms_walk(self._ctx))
+
+    def merge(self, rle: bool = True):
+        self._chk(self._lib.cmsbwt_merge(self._ctx, 1 if rle else 0))
+
+    def step(self, rle: bool = True):
+        self._chk(self._lib.cmsbwt_step(self._ctx, 1 if rle else 0))
+
+    def stats(self) -> Stats:
+        st = Stats()
+        self._chk(self._lib.cmsbwt_get_stats(self._ctx, ctypes.byref(st)))
+        return st
+
+    def runs_bytes(self) -> bytes:
+        nr = self._lib.cmsbwt_num_runs(self._ctx)
+        buf = ctypes.create_string_buffer(max(1, nr * 9))
+        self._chk(self._lib.cmsbwt_copy_runs(self._ctx, buf, nr * 9))
+        return buf.raw[: nr * 9]
+
+    def write_output(self, outname: str, rle: bool = True):
+        self._chk(self._lib.cmsbwt_write_output(self._ctx, outname.encode(), 1 if rle else 0))
+
+    def array(self, name: str):
+        import numpy as np
+        nb = ctypes.c_uint64()
+        self._chk(self._lib.cmsbwt_copy_array(self._ctx, name.encode(), None, ctypes.byref(nb)))
+        out = np.empty(nb.value // np.dtype(ARRAYS[name]).itemsize, dtype=ARRAYS[name])
+        self._chk(self._lib.cmsbwt_copy_array(self._ctx, name.encode(), out.ctypes.data if out.size else None,
+                                              ctypes.byref(nb)))
+        return out
+
+
+def host_read_collection(path: str, prefix: int = UINT64_MAX):
+    """Reader only (no GPU): returns (list of document bytes, sn)."""
+    import numpy as np
+    lib = load_library()
+    tl, nd, sn = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    rc = lib.cmsbwt_host_read_collection(path.encode(), prefix, None, 0, ctypes.byref(tl), None, 0,
+                                         ctypes.byref(nd), ctypes.byref(sn))
+    if rc:
+        raise CmsBwtError(rc, f"cannot read {path}")
+    text = ctypes.create_string_buffer(max(1, tl.value))
+    off = np.zeros(nd.value + 1, dtype=np.uint64)
+    rc = lib.cmsbwt_host_read_collection(path.encode(), prefix, text, tl.value, ctypes.byref(tl),
+                                         off.ctypes.data, nd.value + 1, ctypes.byref(nd), ctypes.byref(sn))
+    if rc:
+        raise CmsBwtError(rc, f"cannot read {path}")
+    raw = text.raw
+    return [raw[int(off[k]):int(off[k + 1])] for k in range(nd.value)], sn.value
+
+
+def host_suffix_array(s: bytes):
+    import numpy as np
+    lib = load_library()
+    out = np.empty(len(s), dtype=np.int32)
+    buf = ctypes.create_string_buffer(s, max(1, len(s)))
+    rc = lib.cmsbwt_host_suffix_array(buf, len(s), out.ctypes.data if len(s) else None)
+    if rc:
+        raise CmsBwtError(rc, "suffix array failed")
+    return out
+
+
+def decode_rl(raw: bytes):
+    """(lengths uint64, chars uint8) of a .rl_bwt byte string (FN:1708-1709 records)."""
+    import numpy as np
+    a = np.frombuffer(raw, dtype=np.uint8).reshape(-1, 9)
+    return a[:, :8].copy().view("<u8").ravel(), a[:, 8].copy()

@@ -1,0 +1,52 @@
+// device_common.h — shared device-side definitions for the CMS-BWT engine.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cmsbwt {
+
+constexpr int kMaxLevels = 6;   // block-minima levels over LCP (64^6 > 2^32)
+constexpr uint32_t kPoolB = 16; // head records per pool block
+constexpr uint8_t kSep = 2;     // CMS-BWT.h:28
+
+// Reference index staged in HBM; int32/uint32 arrays,
+// x as bytes with 64 bytes of padding so the LCE loop can read 16 B past n.
+struct DevRef {
+  const uint8_t* x;
+  const int32_t* sa;
+  const uint32_t* isa;
+  const int32_t* lcp;     // n+1 entries
+  const int32_t* plcp;    // max-neighbour PLCP (FN:272-274)
+  const uint8_t* bwt;
+  const int32_t* lvl[kMaxLevels];  // lvl[0][b] = min lcp[64b..64b+63], lvl[k] = min of 64 lvl[k-1]
+  uint32_t lvlLen[kMaxLevels];
+  int nlvl;
+  uint32_t n;
+};
+
+// One restart chunk of the MS walk: positions [a, b) of document `doc`.
+struct Chunk {
+  uint32_t doc;
+  uint32_t a;
+  uint32_t b;
+  uint32_t last;  // 1 if this is the last chunk of its document
+};
+
+// 16-byte head record as written by the MS walk (MatchInVectorBigger, match.h:5-16,
+// minus toNext/idx which are assigned later).
+struct HeadRec {
+  uint32_t start;   // doc-local position
+  uint32_t pos;     // reference position of the match
+  uint32_t len;     // match length
+  uint32_t flags;   // bit 0 smaller, bits 8..15 char before the head (listOfChars)
+};
+
+struct Pool {
+  HeadRec* rec;
+  uint32_t* blkChunk;
+  uint32_t* blkSeq;
+  uint32_t* used;      // atomic block counter
+  uint32_t capBlocks;
+};
+
+}  // namespace cmsbwt

@@ -1,0 +1,976 @@
+// engine.hip — host orchestration of the CMS-BWT hot path on one MI355X, and
+// the C ABI of include/cmsbwt.h.
+//
+// Stage map (reference = CMS-BWT-functions.cpp, "FN"):
+//   load_reference ... FN:151-310  (host SA-IS + LCP, staged into HBM)
+//   load_collection .. FN:1138-1275 (reader) -> text + doc offsets in HBM
+//   ms_walk .......... FN:1151-1212 walk (k_ms_walk), FN:1359-1385 j-scan
+//   merge ............ FN:1387-1416 grouping (radix sorts), FN:1432-1494 ranks
+//                      + suffix sort of the head string (prefix doubling),
+//                      FN:1504-1603 counters, FN:1618-1777 inversion + runs
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+#include <cstring>
+
+#include <hip/hip_runtime.h>
+#include <rocprim/rocprim.hpp>
+
+#include <algorithm>
+#include <chrono>
+#include <fstream>
+#include <string>
+#include <vector>
+
+#include "../../include/cmsbwt.h"
+#include "device_common.h"
+#include "host_index.h"
+#include "host_reader.h"
+#include "kernels.h"
+#include "merge_kernels.h"
+#include "synth.h"
+
+namespace cmsbwt {
+
+struct WidenU64 {
+  __host__ __device__ uint64_t operator()(uint32_t v) const { return (uint64_t)v; }
+};
+
+struct HipError {
+  std::string msg;
+};
+
+#define HIPCHK(x)                                                                              \
+  do {                                                                                         \
+    hipError_t e_ = (x);                                                                       \
+    if (e_ != hipSuccess)                                                                      \
+      throw HipError{std::string(#x) + " -> " + hipGetErrorString(e_) + " @" + std::to_string(__LINE__)}; \
+  } while (0)
+
+struct InputError {
+  int code;
+  std::string msg;
+};
+
+template <class T>
+struct DBuf {
+  T* p = nullptr;
+  uint64_t n = 0;
+  DBuf() = default;
+  DBuf(const DBuf&) = delete;
+  DBuf& operator=(const DBuf&) = delete;
+  ~DBuf() { release(); }
+  void alloc(uint64_t k) {
+    release();
+    n = k;
+    if (k) HIPCHK(hipMalloc((void**)&p, std::max<uint64_t>(k * sizeof(T), 64)));
+  }
+  void zero(hipStream_t st) { if (n) HIPCHK(hipMemsetAsync(p, 0, n * sizeof(T), st)); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    n = 0;
+  }
+  uint64_t bytes() const { return n * sizeof(T); }
+};
+
+static int bits_for(uint64_t v) {  // bits to represent values in [0, v]
+  int b = 1;
+  while (b < 64 && (v >> b)) b++;
+  return b;
+}
+
+struct Engine {
+  int device = 0;
+  hipStream_t st = nullptr;
+  std::string err;
+  cmsbwt_stats stats{};
+
+  // ---- reference
+  bool refLoaded = false;
+  HostIndex hix;
+  DBuf<uint8_t> dx, dbwt;
+  DBuf<int32_t> dsa, dlcp, dplcp;
+  DBuf<uint32_t> disa;
+  DBuf<int32_t> dlvl[kMaxLevels];
+  DevRef R{};
+
+  // ---- collection
+  bool collLoaded = false;
+  DBuf<uint8_t> dtext;
+  DBuf<uint64_t> ddoc;
+  std::vector<uint64_t> hdoc;  // doc offsets (ndocs+1), doc k = [hdoc[k], hdoc[k+1]-1)
+  uint64_t ndocs = 0, chars = 0, sn = 0;
+
+  // ---- walk outputs
+  bool walked = false;
+  uint32_t H = 0;
+  DBuf<uint32_t> hStart, hPos, hLen, hIsa, hTonext;
+  DBuf<uint8_t> hSmall, hChar;
+  DBuf<uint16_t> hNext;
+  DBuf<int32_t> diff;
+  DBuf<uint8_t> hasHead;
+
+  // ---- merge outputs (kept for parity copies)
+  bool merged = false;
+  uint32_t K = 0;
+  DBuf<int32_t> T;
+  DBuf<uint32_t> saT;
+  DBuf<uint8_t> bwtHeads;
+  DBuf<unsigned long long> counter;
+  DBuf<int64_t> bucket;
+  DBuf<uint8_t> runs;
+  uint64_t nruns = 0;
+  int lastRle = 1;
+  DBuf<uint8_t> tmp;  // rocPRIM scratch
+
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+
+  explicit Engine(int dev) : device(dev) {
+    HIPCHK(hipSetDevice(dev));
+    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+    HIPCHK(hipEventCreate(&ev0));
+    HIPCHK(hipEventCreate(&ev1));
+  }
+  ~Engine() {
+    if (ev0) (void)hipEventDestroy(ev0);
+    if (ev1) (void)hipEventDestroy(ev1);
+    if (st) (void)hipStreamDestroy(st);
+  }
+
+  void* scratch(size_t bytes) {
+    if (tmp.n < bytes) tmp.alloc(bytes + (bytes >> 3) + 256);
+    return tmp.p;
+  }
+  void sync() { HIPCHK(hipStreamSynchronize(st)); }
+
+  template <class T_>
+  T_ read1(const T_* d) {
+    T_ v;
+    HIPCHK(hipMemcpyAsync(&v, d, sizeof(T_), hipMemcpyDeviceToHost, st));
+    sync();
+    return v;
+  }
+
+  // ---- rocPRIM helpers
+  template <class In, class Out, class Init>
+  void exscan(In in, Out out, Init init, uint64_t n) {
+    if (!n) return;
+    size_t b = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, b, in, out, init, (size_t)n, rocprim::plus<Init>(), st));
+    HIPCHK(rocprim::exclusive_scan(scratch(b), b, in, out, init, (size_t)n, rocprim::plus<Init>(), st));
+  }
+  template <class In, class Out, class Op>
+  void inscan(In in, Out out, uint64_t n, Op op) {
+    if (!n) return;
+    size_t b = 0;
+    HIPCHK(rocprim::inclusive_scan(nullptr, b, in, out, (size_t)n, op, st));
+    HIPCHK(rocprim::inclusive_scan(scratch(b), b, in, out, (size_t)n, op, st));
+  }
+  template <class Kt, class Vt>
+  void sort_pairs(const Kt* kin, Kt* kout, const Vt* vin, Vt* vout, uint64_t n, int bits) {
+    if (!n) return;
+    size_t b = 0;
+    HIPCHK(rocprim::radix_sort_pairs(nullptr, b, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, st));
+    HIPCHK(rocprim::radix_sort_pairs(scratch(b), b, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, st));
+  }
+  template <class Kt>
+  void sort_keys(const Kt* kin, Kt* kout, uint64_t n, int bits) {
+    if (!n) return;
+    size_t b = 0;
+    HIPCHK(rocprim::radix_sort_keys(nullptr, b, kin, kout, (size_t)n, 0u, (unsigned)bits, st));
+    HIPCHK(rocprim::radix_sort_keys(scratch(b), b, kin, kout, (size_t)n, 0u, (unsigned)bits, st));
+  }
+  uint32_t select_flagged(const uint32_t* in, const uint32_t* flags, uint32_t* out, uint32_t n) {
+    if (!n) return 0;
+    DBuf<uint32_t> cnt;
+    cnt.alloc(1);
+    size_t b = 0;
+    HIPCHK(rocprim::select(nullptr, b, in, flags, out, cnt.p, (size_t)n, st));
+    HIPCHK(rocprim::select(scratch(b), b, in, flags, out, cnt.p, (size_t)n, st));
+    return read1(cnt.p);
+  }
+
+  // =====================================================================
+  // reference (FN:151-310)
+  void load_reference_bytes(const std::string& trimmed) {
+    auto t0 = std::chrono::steady_clock::now();
+    for (unsigned char c : trimmed)
+      if (c == 2) throw InputError{CMSBWT_EINPUT, "reference contains byte 0x02 (the document separator)"};
+    if (trimmed.size() + 130 >= (1ull << 31)) throw InputError{CMSBWT_ELIMIT, "reference longer than 2^31 (int32 SA)"};
+    build_index(trimmed, hix);
+    const uint32_t n = hix.n;
+    // Skip-search precondition: PLCP[q] + q non-decreasing.
+    for (uint32_t q = 0; q + 1 < n; q++)
+      if ((int64_t)hix.plcp[q + 1] + 1 < (int64_t)hix.plcp[q])
+        throw InputError{CMSBWT_EINPUT, "internal: PLCP monotonicity violated"};
+    dx.alloc((uint64_t)n + 64);
+    HIPCHK(hipMemsetAsync(dx.p, 0, n + 64, st));
+    HIPCHK(hipMemcpyAsync(dx.p, hix.x.data(), n, hipMemcpyHostToDevice, st));
+    dsa.alloc(n);
+    HIPCHK(hipMemcpyAsync(dsa.p, hix.sa.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    disa.alloc(n);
+    HIPCHK(hipMemcpyAsync(disa.p, hix.isa.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    dlcp.alloc((uint64_t)n + 1);
+    HIPCHK(hipMemcpyAsync(dlcp.p, hix.lcp.data(), ((size_t)n + 1) * 4, hipMemcpyHostToDevice, st));
+    dplcp.alloc((uint64_t)n + 1);
+    HIPCHK(hipMemcpyAsync(dplcp.p, hix.plcp.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
+    dbwt.alloc(n);
+    HIPCHK(hipMemcpyAsync(dbwt.p, hix.bwt.data(), n, hipMemcpyHostToDevice, st));
+    // block minima levels over lcp[0..n)
+    std::vector<int32_t> prev(hix.lcp.begin(), hix.lcp.begin() + n), cur;
+    int L = 0;
+    memset(&R, 0, sizeof(R));
+    do {
+      cur.assign((prev.size() + 63) / 64, INT32_MAX);
+      for (size_t i = 0; i < prev.size(); i++) cur[i / 64] = std::min(cur[i / 64], prev[i]);
+      dlvl[L].alloc(cur.size());
+      HIPCHK(hipMemcpyAsync(dlvl[L].p, cur.data(), cur.size() * 4, hipMemcpyHostToDevice, st));
+      R.lvl[L] = dlvl[L].p;
+      R.lvlLen[L] = (uint32_t)cur.size();
+      L++;
+      prev.swap(cur);
+    } while (prev.size() > 64 && L < kMaxLevels);
+    R.nlvl = L;
+    R.x = dx.p;
+    R.sa = dsa.p;
+    R.isa = disa.p;
+    R.lcp = dlcp.p;
+    R.plcp = dplcp.p;
+    R.bwt = dbwt.p;
+    R.n = n;
+    sync();
+    refLoaded = true;
+    stats.n = n;
+    stats.t_index_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+
+  // =====================================================================
+  // collection
+  void check_bytes(const uint8_t* p, uint64_t len) {
+    for (uint64_t i = 0; i < len; i++)
+      if (!hix.present[p[i]])
+        throw InputError{CMSBWT_EINPUT, "collection byte " + std::to_string((int)p[i]) +
+                                            " does not occur in the reference (reference behaviour undefined)"};
+  }
+  void reset_collection() {
+    collLoaded = walked = merged = false;
+    H = K = 0;
+  }
+  void upload_collection(const Collection& c) {
+    if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
+    auto t0 = std::chrono::steady_clock::now();
+    reset_collection();
+    for (uint64_t d = 0; d < c.ndocs(); d++) {
+      uint64_t len = c.off[d + 1] - c.off[d] - 1;
+      if (len >= (1ull << 32) - 1) throw InputError{CMSBWT_ELIMIT, "document longer than 2^32 (uint32 positions)"};
+      check_bytes(c.text.data() + c.off[d], len);
+    }
+    dtext.alloc(c.text.size() + 64);
+    HIPCHK(hipMemsetAsync(dtext.p + c.text.size(), kSep, 64, st));
+    if (!c.text.empty()) HIPCHK(hipMemcpyAsync(dtext.p, c.text.data(), c.text.size(), hipMemcpyHostToDevice, st));
+    hdoc = c.off;
+    ddoc.alloc(hdoc.size());
+    HIPCHK(hipMemcpyAsync(ddoc.p, hdoc.data(), hdoc.size() * 8, hipMemcpyHostToDevice, st));
+    sync();
+    ndocs = c.ndocs();
+    chars = c.chars;
+    sn = c.sn;
+    collLoaded = true;
+    stats.t_upload_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  void load_synth(uint64_t seed, uint64_t copy_begin, uint64_t ncopies, double p, int leadingEmpty) {
+    if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
+    reset_collection();
+    // the reference must be the synthetic reference of the same seed: its
+    // trimmed length is n - (augmentation) ; recover L from the stored x.
+    const uint64_t L = hix.ref_len;
+    for (uint64_t k = 0; k < std::min<uint64_t>(L, 4096); k++)
+      if ((uint8_t)hix.x[k] != (uint8_t)synth_acgt(synth_base_code(seed, k)))
+        throw InputError{CMSBWT_EARG, "loaded reference is not the synthetic reference of this seed"};
+    uint64_t base = leadingEmpty ? 1 : 0;
+    uint64_t total = base + ncopies * (L + 1);
+    dtext.alloc(total + 64);
+    HIPCHK(hipMemsetAsync(dtext.p, kSep, total + 64, st));
+    launch_synth_collection(dtext.p, L, seed, copy_begin, ncopies, synth_threshold(p), base, st);
+    HIPCHK(hipGetLastError());
+    hdoc.clear();
+    hdoc.push_back(0);
+    if (leadingEmpty) hdoc.push_back(1);
+    for (uint64_t d = 0; d < ncopies; d++) hdoc.push_back(base + (d + 1) * (L + 1));
+    ddoc.alloc(hdoc.size());
+    HIPCHK(hipMemcpyAsync(ddoc.p, hdoc.data(), hdoc.size() * 8, hipMemcpyHostToDevice, st));
+    sync();
+    ndocs = hdoc.size() - 1;
+    chars = ncopies * L;
+    sn = total;
+    collLoaded = true;
+  }
+
+  // =====================================================================
+  // MS walk + head finalisation
+  uint32_t chunk_size() const {
+    if (const char* e = getenv("CMSBWT_CHUNK")) return (uint32_t)std::max(64L, atol(e));
+    uint64_t c = chars / (256ull * 64 * 8);
+    c = std::max<uint64_t>(2048, std::min<uint64_t>(32768, c));
+    return (uint32_t)c;
+  }
+
+  void ms_walk() {
+    if (!collLoaded) throw InputError{CMSBWT_EARG, "load a collection first"};
+    auto t0 = std::chrono::steady_clock::now();
+    walked = merged = false;
+    const uint32_t C = chunk_size();
+    std::vector<Chunk> chunks;
+    std::vector<uint32_t> lastChunk(ndocs);
+    for (uint64_t d = 0; d < ndocs; d++) {
+      uint64_t L = hdoc[d + 1] - hdoc[d] - 1;
+      uint64_t nc = std::max<uint64_t>(1, (L + C - 1) / C);
+      for (uint64_t k = 0; k < nc; k++) {
+        Chunk ch;
+        ch.doc = (uint32_t)d;
+        ch.a = (uint32_t)(k * C);
+        ch.b = (uint32_t)std::min<uint64_t>(L, (k + 1) * C);
+        ch.last = k + 1 == nc;
+        chunks.push_back(ch);
+      }
+      lastChunk[d] = (uint32_t)chunks.size() - 1;
+    }
+    const uint32_t nch = (uint32_t)chunks.size();
+    DBuf<Chunk> dch;
+    dch.alloc(nch);
+    HIPCHK(hipMemcpyAsync(dch.p, chunks.data(), nch * sizeof(Chunk), hipMemcpyHostToDevice, st));
+    DBuf<uint32_t> chunkCount, used;
+    chunkCount.alloc(nch);
+    used.alloc(1);
+    // pool sized for ~3% heads + one partial block per chunk; grown on overflow
+    uint64_t cap = (uint64_t)nch + chars / 32 / kPoolB + 1024;
+    DBuf<HeadRec> rec;
+    DBuf<uint32_t> blkChunk, blkSeq;
+    uint32_t usedBlocks = 0;
+    while (true) {
+      if (cap > 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "head pool exceeds 2^32 blocks"};
+      rec.alloc(cap * kPoolB);
+      blkChunk.alloc(cap);
+      blkSeq.alloc(cap);
+      used.zero(st);
+      Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
+      HIPCHK(hipEventRecord(ev0, st));
+      launch_ms_walk(R, dtext.p, ddoc.p, dch.p, nch, pool, chunkCount.p, st);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(ev1, st));
+      usedBlocks = read1(used.p);
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, ev0, ev1));
+      stats.ms_walk_kernel_ms = ms;
+      if (usedBlocks <= cap) break;
+      cap = (uint64_t)usedBlocks + (uint64_t)nch + 1024;
+    }
+    // chunk bases (end phrase counted in the last chunk of each document)
+    DBuf<uint32_t> withEnd, chunkBase;
+    withEnd.alloc(nch);
+    chunkBase.alloc(nch);
+    {
+      std::vector<uint32_t> cc(nch);
+      HIPCHK(hipMemcpyAsync(cc.data(), chunkCount.p, nch * 4, hipMemcpyDeviceToHost, st));
+      sync();
+      uint64_t tot = 0;
+      for (uint32_t c = 0; c < nch; c++) { cc[c] += chunks[c].last; tot += cc[c]; }
+      if (tot >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^31-1 heads (int32 ranks, FN:1436)"};
+      H = (uint32_t)tot;
+      HIPCHK(hipMemcpyAsync(withEnd.p, cc.data(), nch * 4, hipMemcpyHostToDevice, st));
+    }
+    exscan(withEnd.p, chunkBase.p, 0u, nch);
+    hStart.alloc(H); hPos.alloc(H); hLen.alloc(H); hIsa.alloc(H); hTonext.alloc(H);
+    hSmall.alloc(H); hChar.alloc(H); hNext.alloc(H);
+    HeadsSoA h = heads();
+    Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
+    launch_scatter_heads(pool, usedBlocks, chunkCount.p, chunkBase.p, h, st);
+    DBuf<uint32_t> dLast, docEnd;
+    dLast.alloc(ndocs);
+    HIPCHK(hipMemcpyAsync(dLast.p, lastChunk.data(), ndocs * 4, hipMemcpyHostToDevice, st));
+    docEnd.alloc(ndocs);
+    launch_end_phrases(dtext.p, ddoc.p, (uint32_t)ndocs, dLast.p, chunkCount.p, chunkBase.p, R.n, h, docEnd.p, st);
+    diff.alloc((uint64_t)R.n + 1);
+    diff.zero(st);
+    hasHead.alloc(R.n);
+    hasHead.zero(st);
+    DBuf<uint32_t> errf;
+    errf.alloc(1);
+    errf.zero(st);
+    launch_finalize(R, h, H, docEnd.p, (uint32_t)ndocs, diff.p, hasHead.p, errf.p, st);
+    HIPCHK(hipGetLastError());
+    uint32_t ef = read1(errf.p);
+    if (ef & 1) throw InputError{CMSBWT_EINPUT, "internal: match ends not monotone inside a document"};
+    if (ef & 6) throw InputError{CMSBWT_EINPUT, "isaNext/run index outside the reference (reference UB)"};
+    walked = true;
+    stats.heads = H;
+    stats.ndocs = ndocs;
+    stats.chars = chars;
+    stats.sn = sn;
+    stats.t_ms_walk_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+
+  HeadsSoA heads() {
+    return HeadsSoA{hStart.p, hPos.p, hLen.p, hSmall.p, hChar.p, hIsa.p, hTonext.p, hNext.p};
+  }
+
+  // =====================================================================
+  // merge
+  void merge(int rle) {
+    if (!walked) throw InputError{CMSBWT_EARG, "run ms_walk first"};
+    auto t0 = std::chrono::steady_clock::now();
+    const uint32_t n = R.n;
+    const uint32_t E = (uint32_t)ndocs;
+    const int bN = bits_for(n);
+    HeadsSoA h = heads();
+
+    // ---- grouping: perm sorted by (pos, len, isaNext, idx)   FN:1387-1416
+    DBuf<uint32_t> perm, perm2, key, key2;
+    perm.alloc(H); perm2.alloc(H); key.alloc(H); key2.alloc(H);
+    mk_iota(perm.p, H, st);
+    mk_gather(hIsa.p, perm.p, key.p, H, st);
+    sort_pairs(key.p, key2.p, perm.p, perm2.p, H, bN);
+    mk_gather(hLen.p, perm2.p, key.p, H, st);
+    sort_pairs(key.p, key2.p, perm2.p, perm.p, H, 32);
+    mk_gather(hPos.p, perm.p, key.p, H, st);
+    sort_pairs(key.p, key2.p, perm.p, perm2.p, H, bN);
+    perm.release();
+    DBuf<uint32_t>& P = perm2;  // sorted members
+    // items
+    mk_item_flags(P.p, h, key.p, H, st);
+    inscan(key.p, key2.p, H, rocprim::plus<uint32_t>());
+    K = read1(key2.p + (H - 1));
+    DBuf<uint32_t> aPos, aLen, aIsa, aUntil, aCount, aFirst, aSlot;
+    DBuf<uint8_t> aSmall;
+    aPos.alloc(K); aLen.alloc(K); aIsa.alloc(K); aUntil.alloc(K); aCount.alloc(K); aFirst.alloc(K);
+    aSmall.alloc(K);
+    ItemsSoA A0{aPos.p, aLen.p, aIsa.p, aSmall.p, aUntil.p, aCount.p, aFirst.p, nullptr, nullptr};
+    mk_item_fill(P.p, key.p, key2.p, h, H, A0, st);
+    mk_item_count(aFirst.p, aCount.p, K, H, st);
+    key.release();
+    key2.release();
+    // map order inside each position (match.h:27-33): stable sort by class/len, then by pos
+    DBuf<uint32_t> io, io2, ik, ik2;
+    io.alloc(K); io2.alloc(K); ik.alloc(K); ik2.alloc(K);
+    mk_iota(io.p, K, st);
+    mk_item_key(aLen.p, aSmall.p, io.p, ik.p, K, st);
+    sort_pairs(ik.p, ik2.p, io.p, io2.p, K, 32);
+    mk_gather(aPos.p, io2.p, ik.p, K, st);
+    sort_pairs(ik.p, ik2.p, io2.p, io.p, K, bN);
+    ik.release(); ik2.release(); io2.release();
+    DBuf<uint32_t> sPos, sLen, sIsa, sUntil, sCount, sFirst, sSlot;
+    DBuf<uint8_t> sSmall;
+    sPos.alloc(K); sLen.alloc(K); sIsa.alloc(K); sUntil.alloc(K); sCount.alloc(K); sFirst.alloc(K);
+    sSlot.alloc((uint64_t)K + 1); sSmall.alloc(K);
+    ItemsSoA S{sPos.p, sLen.p, sIsa.p, sSmall.p, sUntil.p, sCount.p, sFirst.p, sSlot.p, nullptr};
+    mk_item_permute(A0, io.p, S, K, st);
+    io.release();
+    aPos.release(); aLen.release(); aIsa.release(); aUntil.release(); aCount.release(); aFirst.release();
+    aSmall.release();
+    // slots = prefixSumForPositions (FN:1504-1515)
+    exscan(sCount.p, sSlot.p, 0u, K);
+    {
+      uint32_t hh = H;
+      HIPCHK(hipMemcpyAsync(sSlot.p + K, &hh, 4, hipMemcpyHostToDevice, st));
+    }
+    DBuf<uint32_t> posBegin, posF;
+    posBegin.alloc((uint64_t)n + 1);
+    posF.alloc(n);
+    mk_pos_begin(sPos.p, K, n, posBegin.p, st);
+    mk_pos_f(sPos.p, sSmall.p, posBegin.p, K, n, posF.p, st);
+    DBuf<unsigned long long> cstats;
+    cstats.alloc(8);
+    cstats.zero(st);
+    mk_check_items(S, posBegin.p, posF.p, K, cstats.p + 3, st);
+
+    // ---- ranks (FN:1432-1453)
+    DBuf<uint32_t> itemsSA, headsSA, itemRankBase, headBase;
+    itemsSA.alloc(n); headsSA.alloc(n); itemRankBase.alloc(n); headBase.alloc(n);
+    mk_sa_counts(dsa.p, posBegin.p, sSlot.p, n, E, itemsSA.p, headsSA.p, st);
+    exscan(itemsSA.p, itemRankBase.p, 0u, n);
+    exscan(headsSA.p, headBase.p, 0u, n);
+    itemsSA.release(); headsSA.release();
+    T.alloc((uint64_t)H + 1);
+    saT.alloc((uint64_t)H + 1);
+    DBuf<uint32_t> grp;
+    grp.alloc((uint64_t)H + 1);
+    {
+      int32_t z = 0;
+      uint32_t hh = H, zz = 0;
+      HIPCHK(hipMemcpyAsync(T.p + H, &z, 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(saT.p, &hh, 4, hipMemcpyHostToDevice, st));
+      HIPCHK(hipMemcpyAsync(grp.p + H, &zz, 4, hipMemcpyHostToDevice, st));
+    }
+    mk_ranks(S, K, P.p, posBegin.p, disa.p, itemRankBase.p, headBase.p, n, E, T.p, saT.p, grp.p, st);
+    itemRankBase.release();
+    stats.rank = (uint64_t)E + 2 + (uint64_t)(K - 1);
+    sync();
+
+    // ---- suffix sort of the head string (libsais_int, FN:1455-1459)
+    {
+      DBuf<uint32_t> ac, acOff;
+      ac.alloc(K);
+      acOff.alloc(K);
+      mk_active_count(S, K, n, ac.p, st);
+      exscan(ac.p, acOff.p, 0u, K);
+      uint32_t U = 0;
+      {
+        uint32_t lastOff = read1(acOff.p + (K - 1)), lastC = read1(ac.p + (K - 1));
+        U = lastOff + lastC;
+      }
+      DBuf<uint32_t> act, act2, val, val2, lab, labMax, keep;
+      DBuf<uint64_t> k64, k64b;
+      act.alloc(U); act2.alloc(U); val.alloc(U); val2.alloc(U); lab.alloc(U); labMax.alloc(U); keep.alloc(U);
+      k64.alloc(U); k64b.alloc(U);
+      mk_active_init(S, K, n, disa.p, posBegin.p, headBase.p, acOff.p, act.p, st);
+      const int bH = bits_for(H);
+      // groups must be visited in suffix-array order (k_dbl_apply writes the
+      // u-th smallest key to the u-th smallest active sa position)
+      sort_keys(act.p, act2.p, U, bH);
+      std::swap(act.p, act2.p);
+      for (uint64_t hstep = 1; U > 0; hstep <<= 1) {
+        if (hstep > H) throw InputError{CMSBWT_EINPUT, "internal: head-string suffix sort did not converge"};
+        mk_dbl_keys(act.p, saT.p, grp.p, (uint32_t)hstep, U, k64.p, val.p, st);
+        sort_pairs(k64.p, k64b.p, val.p, val2.p, U, 32 + bH);
+        mk_dbl_apply(act.p, k64b.p, val2.p, U, saT.p, lab.p, st);
+        inscan(lab.p, labMax.p, U, rocprim::maximum<uint32_t>());
+        mk_dbl_groups(act.p, k64b.p, val2.p, labMax.p, U, grp.p, keep.p, st);
+        U = select_flagged(act.p, keep.p, act2.p, U);
+        std::swap(act.p, act2.p);
+      }
+    }
+    grp.release();
+    DBuf<uint32_t> headRank;
+    headRank.alloc(H);
+    bwtHeads.alloc(H);
+    mk_head_ranks(saT.p, hChar.p, H, headRank.p, bwtHeads.p, st);
+
+    // ---- next-head ranks, sorted per item (FN:1480-1494)
+    DBuf<uint32_t> nhr;
+    nhr.alloc(H);
+    {
+      DBuf<uint64_t> nk, nk2;
+      nk.alloc(H); nk2.alloc(H);
+      mk_nhr_keys(S, K, P.p, headRank.p, hNext.p, nk.p, st);
+      sort_keys(nk.p, nk2.p, H, 32 + bits_for(K));
+      mk_low32(nk2.p, nhr.p, H, st);
+    }
+    headRank.release();
+
+    // ---- counterSmallerThanHead (FN:1523-1603)
+    counter.alloc((uint64_t)H + 1);
+    counter.zero(st);
+    uint64_t W = 0;
+    {
+      DBuf<uint64_t> wp;
+      wp.alloc((uint64_t)K + 1);
+      auto u64in = rocprim::make_transform_iterator(sUntil.p, WidenU64());
+      exscan(u64in, wp.p, (uint64_t)0, K);
+      uint64_t lastWp = read1(wp.p + (K - 1));
+      uint32_t lastU = read1(sUntil.p + (K - 1));
+      W = lastWp + lastU;
+      HIPCHK(hipMemcpyAsync(wp.p + K, &W, 8, hipMemcpyHostToDevice, st));
+      auto te = std::chrono::steady_clock::now();
+      HIPCHK(hipEventRecord(ev0, st));
+      mk_counter(S, K, wp.p, W, hasHead.p, posBegin.p, posF.p, nhr.p, counter.p, cstats.p, n, st);
+      HIPCHK(hipGetLastError());
+      HIPCHK(hipEventRecord(ev1, st));
+      sync();
+      float ms = 0;
+      HIPCHK(hipEventElapsedTime(&ms, ev0, ev1));
+      counter_kernel_ms = ms;
+      (void)te;
+    }
+    unsigned long long cs[8];
+    HIPCHK(hipMemcpyAsync(cs, cstats.p, sizeof(cs), hipMemcpyDeviceToHost, st));
+    sync();
+    stats.counter_bad = cs[0];
+    stats.counter_good = cs[1];
+    stats.counter_nothing = cs[2];
+    stats.order_violations = cs[3];
+    if (cs[4]) throw InputError{CMSBWT_EINPUT, "counter target beyond the reference (reference UB)"};
+    if (cs[3]) throw InputError{CMSBWT_EORDER,
+                                "MatchInSet comparator is not a strict weak order on this input (" +
+                                    std::to_string(cs[3]) + " ambiguous comparisons); std::map layout would "
+                                    "depend on insertion history"};
+    W_work = W;
+
+    // ---- buckets (FN:1162-1171) and inversion (FN:1618-1628, done as a gather)
+    bucket.alloc(n);
+    {
+      DBuf<int32_t> cnt;
+      cnt.alloc(n);
+      inscan(diff.p, cnt.p, n, rocprim::plus<int32_t>());
+      mk_bucket(cnt.p, hasHead.p, n, bucket.p, st);
+    }
+
+    // ---- writer (FN:1631-1777) as segments + run-length merge
+    WriterIn wi{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, sCount.p, headBase.p, bwtHeads.p, counter.p,
+                n, E, rle};
+    DBuf<unsigned long long> segN, segOff;
+    segN.alloc(n);
+    segOff.alloc(n);
+    mk_seg_count(wi, segN.p, st);
+    exscan(segN.p, segOff.p, 0ull, n);
+    uint64_t S_ = (uint64_t)E + read1(segOff.p + (n - 1)) + read1(segN.p + (n - 1));
+    segN.release();
+    DBuf<uint8_t> sc;
+    DBuf<unsigned long long> sn_, flag, runId, cum;
+    sc.alloc(S_); sn_.alloc(S_);
+    mk_seg_emit(wi, segOff.p, sc.p, sn_.p, st);
+    segOff.release();
+    flag.alloc(S_); runId.alloc(S_); cum.alloc(S_);
+    mk_run_flags(sc.p, S_, flag.p, st);
+    inscan(flag.p, runId.p, S_, rocprim::plus<unsigned long long>());
+    inscan(sn_.p, cum.p, S_, rocprim::plus<unsigned long long>());
+    uint64_t Rn = read1(runId.p + (S_ - 1));
+    uint64_t symbols = read1(cum.p + (S_ - 1));
+    flag.release();
+    DBuf<unsigned long long> runEnd;
+    DBuf<uint8_t> runChar;
+    runEnd.alloc(Rn); runChar.alloc(Rn);
+    mk_run_pack(sc.p, runId.p, cum.p, S_, runEnd.p, runChar.p, st);
+    runs.alloc(Rn * 9);
+    mk_run_records(runEnd.p, runChar.p, Rn, runs.p, st);
+    HIPCHK(hipGetLastError());
+    sync();
+    nruns = Rn;
+    lastRle = rle;
+    merged = true;
+    stats.keys = K;
+    stats.current_sum = H;
+    stats.runs = Rn;
+    stats.symbols = symbols;
+    stats.positions = count_positions(posBegin);
+    stats.t_merge_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+  float counter_kernel_ms = 0;
+  uint64_t W_work = 0;
+
+  uint64_t count_positions(DBuf<uint32_t>& posBegin) {
+    // phrasesSet.size(): positions holding heads (n-1 always present)
+    std::vector<uint32_t> pb(R.n + 1);
+    HIPCHK(hipMemcpyAsync(pb.data(), posBegin.p, pb.size() * 4, hipMemcpyDeviceToHost, st));
+    sync();
+    uint64_t c = 0;
+    for (uint32_t p = 0; p < R.n; p++) c += pb[p + 1] > pb[p];
+    return c;
+  }
+
+  // =====================================================================
+  void copy_runs(uint8_t* out, uint64_t cap) {
+    if (!merged) throw InputError{CMSBWT_EARG, "run merge first"};
+    if (cap < nruns * 9) throw InputError{CMSBWT_EARG, "output buffer too small"};
+    if (nruns) HIPCHK(hipMemcpyAsync(out, runs.p, nruns * 9, hipMemcpyDeviceToHost, st));
+    sync();
+  }
+
+  void write_output(const std::string& outname, int rle) {
+    if (!merged) throw InputError{CMSBWT_EARG, "run merge first"};
+    if (rle != lastRle) throw InputError{CMSBWT_EARG, "merge was run with a different output format"};
+    auto t0 = std::chrono::steady_clock::now();
+    std::vector<uint8_t> host(nruns * 9);
+    copy_runs(host.data(), host.size());
+    if (rle) {
+      FILE* f = fopen((outname + ".rl_bwt").c_str(), "wb");
+      if (!f) throw InputError{CMSBWT_EIO, "cannot open " + outname + ".rl_bwt"};
+      fwrite(host.data(), 1, host.size(), f);
+      fclose(f);
+    } else {
+      FILE* f = fopen((outname + ".bwt").c_str(), "wb");
+      if (!f) throw InputError{CMSBWT_EIO, "cannot open " + outname + ".bwt"};
+      std::vector<uint8_t> buf(1 << 20);
+      size_t fill = 0;
+      for (uint64_t j = 0; j < nruns; j++) {
+        uint64_t len;
+        memcpy(&len, host.data() + 9 * j, 8);
+        uint8_t c = host[9 * j + 8];
+        while (len) {
+          uint64_t k = std::min<uint64_t>(len, buf.size() - fill);
+          memset(buf.data() + fill, c, k);
+          fill += k;
+          len -= k;
+          if (fill == buf.size()) { fwrite(buf.data(), 1, fill, f); fill = 0; }
+        }
+      }
+      if (fill) fwrite(buf.data(), 1, fill, f);
+      fclose(f);
+    }
+    if (R.n < 1000000) {  // FN:919-924 small-reference side output
+      std::vector<unsigned long long> c((uint64_t)H + 1);
+      HIPCHK(hipMemcpyAsync(c.data(), counter.p, c.size() * 8, hipMemcpyDeviceToHost, st));
+      sync();
+      FILE* f = fopen((outname + ".counterSmallerThanHead_true").c_str(), "wb");
+      if (!f) throw InputError{CMSBWT_EIO, "cannot open counter file"};
+      fwrite(c.data(), 8, c.size(), f);
+      fclose(f);
+    }
+    stats.t_write_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+
+  // parity copies
+  uint64_t copy_array(const std::string& name, void* out) {
+    auto cp = [&](const void* d, uint64_t bytes) -> uint64_t {
+      if (out && bytes) {
+        HIPCHK(hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, st));
+        sync();
+      }
+      return bytes;
+    };
+    if (name.rfind("h_", 0) == 0 && !walked) throw InputError{CMSBWT_EARG, "run ms_walk first"};
+    if (name == "h_start") return cp(hStart.p, (uint64_t)H * 4);
+    if (name == "h_pos") return cp(hPos.p, (uint64_t)H * 4);
+    if (name == "h_len") return cp(hLen.p, (uint64_t)H * 4);
+    if (name == "h_smaller") return cp(hSmall.p, H);
+    if (name == "h_lchar") return cp(hChar.p, H);
+    if (name == "h_isa") return cp(hIsa.p, (uint64_t)H * 4);
+    if (name == "h_tonext") return cp(hTonext.p, (uint64_t)H * 4);
+    if (name == "h_nexthead") return cp(hNext.p, (uint64_t)H * 2);
+    if (!merged) throw InputError{CMSBWT_EARG, "run merge first"};
+    if (name == "bucket") return cp(bucket.p, (uint64_t)R.n * 8);
+    if (name == "rank2head") return cp(T.p, ((uint64_t)H + 1) * 4);
+    if (name == "head2rank") return cp(saT.p, ((uint64_t)H + 1) * 4);
+    if (name == "bwtheads") return cp(bwtHeads.p, H);
+    if (name == "counters") return cp(counter.p, ((uint64_t)H + 1) * 8);
+    throw InputError{CMSBWT_EARG, "unknown array " + name};
+  }
+};
+
+}  // namespace cmsbwt
+
+// =========================================================================
+// C ABI
+using cmsbwt::Engine;
+
+struct cmsbwt_ctx {
+  Engine* e = nullptr;
+  std::string err;
+};
+
+template <class F>
+static int guard(cmsbwt_ctx* c, F&& f) {
+  try {
+    f();
+    return CMSBWT_OK;
+  } catch (const cmsbwt::InputError& ie) {
+    if (c) c->err = ie.msg;
+    return ie.code;
+  } catch (const cmsbwt::HipError& he) {
+    if (c) c->err = he.msg;
+    return CMSBWT_EDEVICE;
+  } catch (const std::bad_alloc&) {
+    if (c) c->err = "host out of memory";
+    return CMSBWT_ELIMIT;
+  }
+}
+
+extern "C" {
+
+int cmsbwt_ctx_create(int device, cmsbwt_ctx** out) {
+  if (!out) return CMSBWT_EARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) return CMSBWT_EDEVICE;
+  cmsbwt_ctx* c = new cmsbwt_ctx();
+  int rc = guard(c, [&] { c->e = new Engine(device); });
+  if (rc) { delete c; return rc; }
+  *out = c;
+  return CMSBWT_OK;
+}
+
+void cmsbwt_ctx_destroy(cmsbwt_ctx* ctx) {
+  if (!ctx) return;
+  delete ctx->e;
+  delete ctx;
+}
+
+const char* cmsbwt_last_error(const cmsbwt_ctx* ctx) { return ctx ? ctx->err.c_str() : "null context"; }
+
+int cmsbwt_load_reference_file(cmsbwt_ctx* ctx, const char* path) {
+  if (!ctx || !path) return CMSBWT_EARG;
+  return guard(ctx, [&] {
+    std::string x, err;
+    if (!cmsbwt::read_reference(path, x, err)) throw cmsbwt::InputError{CMSBWT_EIO, err};
+    ctx->e->load_reference_bytes(x);
+  });
+}
+
+int cmsbwt_load_reference(cmsbwt_ctx* ctx, const uint8_t* ref, uint64_t len) {
+  if (!ctx || (!ref && len)) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->load_reference_bytes(std::string((const char*)ref, len)); });
+}
+
+int cmsbwt_load_collection_file(cmsbwt_ctx* ctx, const char* path, uint64_t prefix) {
+  if (!ctx || !path) return CMSBWT_EARG;
+  return guard(ctx, [&] {
+    cmsbwt::Collection c;
+    std::string err;
+    if (!cmsbwt::read_collection(path, prefix, c, err)) throw cmsbwt::InputError{CMSBWT_EIO, err};
+    ctx->e->upload_collection(c);
+  });
+}
+
+int cmsbwt_load_collection(cmsbwt_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint64_t ndocs) {
+  if (!ctx || !doc_off) return CMSBWT_EARG;
+  return guard(ctx, [&] {
+    cmsbwt::Collection c;
+    c.off.assign(1, 0);
+    for (uint64_t d = 0; d < ndocs; d++) {
+      if (doc_off[d + 1] < doc_off[d]) throw cmsbwt::InputError{CMSBWT_EARG, "doc offsets not ascending"};
+      c.text.insert(c.text.end(), text + doc_off[d], text + doc_off[d + 1]);
+      c.text.push_back(2);
+      c.off.push_back(c.text.size());
+    }
+    c.chars = c.text.size() - ndocs;
+    c.sn = c.text.size();
+    ctx->e->upload_collection(c);
+  });
+}
+
+int cmsbwt_load_collection_synth(cmsbwt_ctx* ctx, uint64_t seed, uint64_t copy_begin, uint64_t ncopies, double p,
+                                 int leading_empty_doc) {
+  if (!ctx) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->load_synth(seed, copy_begin, ncopies, p, leading_empty_doc); });
+}
+
+int cmsbwt_ms_walk(cmsbwt_ctx* ctx) {
+  if (!ctx) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->ms_walk(); });
+}
+
+int cmsbwt_merge(cmsbwt_ctx* ctx, int rle) {
+  if (!ctx) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->merge(rle); });
+}
+
+int cmsbwt_step(cmsbwt_ctx* ctx, int rle) {
+  if (!ctx) return CMSBWT_EARG;
+  return guard(ctx, [&] {
+    ctx->e->ms_walk();
+    ctx->e->merge(rle);
+  });
+}
+
+int cmsbwt_get_stats(const cmsbwt_ctx* ctx, cmsbwt_stats* out) {
+  if (!ctx || !out) return CMSBWT_EARG;
+  *out = ctx->e->stats;
+  return CMSBWT_OK;
+}
+
+uint64_t cmsbwt_num_runs(const cmsbwt_ctx* ctx) { return ctx && ctx->e->merged ? ctx->e->nruns : 0; }
+
+int cmsbwt_copy_runs(cmsbwt_ctx* ctx, uint8_t* out, uint64_t cap) {
+  if (!ctx || !out) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->copy_runs(out, cap); });
+}
+
+int cmsbwt_write_output(cmsbwt_ctx* ctx, const char* outname, int rle) {
+  if (!ctx || !outname) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->write_output(outname, rle); });
+}
+
+int cmsbwt_copy_array(cmsbwt_ctx* ctx, const char* name, void* out, uint64_t* bytes) {
+  if (!ctx || !name) return CMSBWT_EARG;
+  return guard(ctx, [&] {
+    uint64_t b = ctx->e->copy_array(name, out);
+    if (bytes) *bytes = b;
+  });
+}
+
+int cmsbwt_host_read_collection(const char* path, uint64_t prefix, uint8_t* text, uint64_t text_cap,
+                                uint64_t* text_len, uint64_t* doc_off, uint64_t doc_cap, uint64_t* ndocs,
+                                uint64_t* sn) {
+  if (!path) return CMSBWT_EARG;
+  cmsbwt::Collection c;
+  std::string err;
+  if (!cmsbwt::read_collection(path, prefix, c, err)) return CMSBWT_EIO;
+  const uint64_t nd = c.ndocs();
+  if (text_len) *text_len = c.chars;
+  if (ndocs) *ndocs = nd;
+  if (sn) *sn = c.sn;
+  if (text && text_cap < c.chars) return CMSBWT_EARG;
+  if (doc_off && doc_cap < nd + 1) return CMSBWT_EARG;
+  uint64_t o = 0;
+  for (uint64_t d = 0; d < nd; d++) {
+    uint64_t len = c.off[d + 1] - c.off[d] - 1;
+    if (doc_off) doc_off[d] = o;
+    if (text) memcpy(text + o, c.text.data() + c.off[d], len);
+    o += len;
+  }
+  if (doc_off) doc_off[nd] = o;
+  return CMSBWT_OK;
+}
+
+int cmsbwt_host_suffix_array(const uint8_t* s, uint64_t n, int32_t* sa_out) {
+  if ((!s || !sa_out) && n) return CMSBWT_EARG;
+  if (n >= (1ull << 31) - 2) return CMSBWT_ELIMIT;
+  std::vector<int32_t> v(n);
+  for (uint64_t i = 0; i < n; i++) v[i] = s[i];
+  cmsbwt::suffix_array_sais(v.data(), sa_out, (int64_t)n, 256);
+  return CMSBWT_OK;
+}
+
+// Whole run with the reference's log (FN keys).
+int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path, cmsbwt_stats* stats_out) {
+  if (!a || !ref_path || !coll_path || !a->outname) return CMSBWT_EARG;
+  std::string out = a->outname;
+  std::ofstream log(out + ".log");
+  cmsbwt_ctx* ctx = nullptr;
+  int rc = cmsbwt_ctx_create(a->device, &ctx);
+  if (rc) {
+    log << "HIP device " << a->device << " unavailable\n";
+    return rc;
+  }
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
+    return (long long)std::chrono::duration_cast<std::chrono::milliseconds>(y - x).count();
+  };
+  auto t0 = now();
+  log << "About to read ref\n";
+  rc = cmsbwt_load_reference_file(ctx, ref_path);
+  if (rc) { log << ctx->err << "\n"; cmsbwt_ctx_destroy(ctx); return rc; }
+  Engine& e = *ctx->e;
+  log << "Reference (size = " << e.hix.x.size() << "):\n\t";
+  log << "Computing SA done in " << (long long)(e.hix.t_sa * 1000) << " ms\n";
+  log << "Computing LCP and PLCP done in " << (long long)(e.hix.t_lcp * 1000) << " ms\n";
+  log << "Preprocessing done in " << ms(t0, now()) << " ms\n";
+  auto t1 = now();
+  rc = cmsbwt_load_collection_file(ctx, coll_path, a->prefix);
+  if (rc) { log << ctx->err << "\n"; cmsbwt_ctx_destroy(ctx); return rc; }
+  log << "File is in memory\n";
+  log << "_x.len: " << e.R.n << '\n';
+  log << "_sx.len: " << e.sn << '\n';
+  rc = cmsbwt_ms_walk(ctx);
+  if (rc) { log << ctx->err << "\n"; cmsbwt_ctx_destroy(ctx); return rc; }
+  log << "Finished parsing file of length: " << e.sn << "\n";
+  rc = cmsbwt_merge(ctx, a->rle ? 1 : 0);
+  if (rc) { log << ctx->err << "\n"; cmsbwt_ctx_destroy(ctx); return rc; }
+  const cmsbwt_stats& s = e.stats;
+  log << "phrasesSet.size(): " << s.positions << "\n";
+  log << "headNumber: " << s.heads << "\n";
+  if (e.R.n < 1000000) log << "uniqueHeadNumber: " << s.keys << "\n";
+  log << "ndoc: " << s.ndocs + 1 << "\n";
+  log << "docBoundaries.size(): " << s.ndocs + 1 << "\n";
+  log << "Time to compute matching statistics: " << (long long)(s.t_ms_walk_s * 1000) << " milliseconds\n";
+  log << "Rank: " << s.rank << "\n";
+  log << "currentSum: " << s.current_sum << "\n";
+  log << "counterBad: " << s.counter_bad << "\n";
+  log << "counterGood: " << s.counter_good << "\n";
+  log << "counterDoNothing: " << s.counter_nothing << "\n";
+  log << "Done computing counterSmallerThanHead for positions in " << (long long)(s.t_merge_s * 1000)
+      << " milliseconds\n";
+  log << "Inverted data in bucketsForExpandedBWT\n";
+  rc = cmsbwt_write_output(ctx, out.c_str(), a->rle ? 1 : 0);
+  if (rc) { log << ctx->err << "\n"; cmsbwt_ctx_destroy(ctx); return rc; }
+  log << "MS-walk kernel: " << s.ms_walk_kernel_ms << " ms; collection pass: " << ms(t1, now()) << " ms\n";
+  if (stats_out) *stats_out = e.stats;
+  if (a->verbose)
+    fprintf(stderr, "index %.3fs upload %.3fs walk %.3fs (kernel %.2fms) merge %.3fs write %.3fs runs %llu\n",
+            s.t_index_s, s.t_upload_s, s.t_ms_walk_s, s.ms_walk_kernel_ms, s.t_merge_s, s.t_write_s,
+            (unsigned long long)s.runs);
+  cmsbwt_ctx_destroy(ctx);
+  return CMSBWT_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,31 @@
+// host_index.h — reference index built on the host.
+#pragma once
+#include <stdint.h>
+#include <string>
+#include <vector>
+
+namespace cmsbwt {
+
+struct HostIndex {
+  std::string x;               // augmented reference, FN:231-237
+  uint32_t n = 0;              // _n
+  uint64_t ref_len = 0;        // trimmed reference length before augmentation
+  std::vector<int32_t> sa;     // _SA
+  std::vector<uint32_t> isa;   // _ISA
+  std::vector<int32_t> lcp;    // _LCP, n+1 entries, lcp[0]=0, lcp[n]=-1
+  std::vector<int32_t> plcp;   // _PLCP after the max-neighbour redefinition (FN:272-274)
+  std::vector<uint8_t> bwt;    // _BWT
+  bool present[256];           // bytes occurring in x[0..n-3] (collection check)
+  double t_sa = 0, t_lcp = 0;
+};
+
+// Suffix array of s[0..n) over alphabet [0, k) with the "end of string is
+// smallest" convention (same as libsais).  Induced sorting (SA-IS).
+void suffix_array_sais(const int32_t* s, int32_t* sa, int64_t n, int64_t k);
+
+// FN:155-213: read FASTA (first byte '>') or raw reference, trim.
+bool read_reference(const std::string& path, std::string& x, std::string& err);
+// FN:231-297 on an already-read+trimmed sequence.
+void build_index(const std::string& trimmed, HostIndex& ix);
+
+}  // namespace cmsbwt

@@ -1,0 +1,50 @@
+// kernels.h — host-side launchers of the engine's HIP kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "device_common.h"
+
+namespace cmsbwt {
+
+// Heads in document (idx) order, SoA.
+struct HeadsSoA {
+  uint32_t* start;
+  uint32_t* pos;
+  uint32_t* len;
+  uint8_t* smaller;
+  uint8_t* lchar;
+  uint32_t* isa;       // isaNext after k_finalize
+  uint32_t* tonext;
+  uint16_t* nexthead;
+};
+
+// Items (distinct (pos, len, isaNext) keys) in map order: pos ascending, then
+// the MatchInSet order of match.h:27-33 — the order of the reference's slots.
+struct ItemsSoA {
+  uint32_t* pos;
+  uint32_t* len;
+  uint32_t* isa;
+  uint8_t* smaller;
+  uint32_t* until;     // untilNext of the first-inserted head
+  uint32_t* count;     // heads in the item
+  uint32_t* first;     // offset of its members in `perm`
+  uint32_t* slot;      // exclusive prefix of count (prefixSumForPositions)
+  uint32_t* fbegin;    // per item: first F-class item of its position (class split)
+};
+
+// ms_walk.hip
+void launch_ms_walk(const DevRef& R, const uint8_t* text, const uint64_t* docOff, const Chunk* chunks,
+                    uint32_t nchunks, const Pool& pool, uint32_t* chunkCount, hipStream_t st);
+void launch_scatter_heads(const Pool& pool, uint32_t blocksUsed, const uint32_t* chunkCount,
+                          const uint32_t* chunkBase, const HeadsSoA& h, hipStream_t st);
+void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t ndocs,
+                        const uint32_t* docLastChunk, const uint32_t* chunkCount, const uint32_t* chunkBase,
+                        uint32_t n, const HeadsSoA& h, uint32_t* docEndIdx, hipStream_t st);
+void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint32_t* docEndIdx,
+                     uint32_t ndocs, int32_t* diff, uint8_t* hasHead, uint32_t* errFlags, hipStream_t st);
+
+// synth.hip
+void launch_synth_collection(uint8_t* text, uint64_t L, uint64_t seed, uint64_t copy_begin, uint64_t ncopies,
+                             uint64_t pthr, uint64_t base, hipStream_t st);
+
+}  // namespace cmsbwt

@@ -1,0 +1,614 @@
+// merge.hip — MS-factor -> BWT-run merge kernels (FN:1387-1777).
+//
+// Every kernel here is integer/byte work; the heavy lifting between them is
+// done by rocPRIM radix sorts and scans driven from engine.hip.
+#include <hip/hip_runtime.h>
+#include "device_common.h"
+#include "kernels.h"
+#include "merge_kernels.h"
+
+namespace cmsbwt {
+
+__global__ void k_iota(uint32_t* p, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] = (uint32_t)i;
+}
+
+__global__ void k_gather_u32(const uint32_t* __restrict__ src, const uint32_t* __restrict__ perm,
+                             uint32_t* __restrict__ dst, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) dst[i] = src[perm[i]];
+}
+
+// key for the MatchInSet order (match.h:27-33) on consistent data:
+// smaller=true first by len ascending, then smaller=false by len descending.
+__global__ void k_item_key(const uint32_t* __restrict__ len, const uint8_t* __restrict__ sm,
+                           const uint32_t* __restrict__ perm, uint32_t* __restrict__ key, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint32_t q = perm[i];
+  uint32_t L = len[q];
+  key[i] = sm[q] ? L : (0x80000000u | (0x7fffffffu - L));
+}
+
+// item boundaries over perm sorted by (pos, len, isaNext, idx)
+__global__ void k_item_flags(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ pos,
+                             const uint32_t* __restrict__ len, const uint32_t* __restrict__ isa,
+                             uint32_t* __restrict__ flag, uint64_t H) {
+  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= H) return;
+  if (k == 0) { flag[k] = 1; return; }
+  uint32_t a = perm[k], b = perm[k - 1];
+  flag[k] = (pos[a] != pos[b] || len[a] != len[b] || isa[a] != isa[b]) ? 1u : 0u;
+}
+
+// One item per flagged position; the first member (smallest idx) supplies
+// untilNext and smaller, as the first std::map insertion does (FN:1406-1413).
+__global__ void k_item_fill(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flag,
+                            const uint32_t* __restrict__ itemIncl, HeadsSoA h, uint64_t H,
+                            ItemsSoA it) {
+  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= H || !flag[k]) return;
+  uint32_t q = itemIncl[k] - 1;
+  uint32_t a = perm[k];
+  it.pos[q] = h.pos[a];
+  it.len[q] = h.len[a];
+  it.isa[q] = h.isa[a];
+  it.smaller[q] = h.smaller[a];
+  it.until[q] = h.tonext[a];
+  it.first[q] = (uint32_t)k;
+}
+
+__global__ void k_item_count(const uint32_t* __restrict__ first, uint32_t* __restrict__ count, uint32_t K,
+                             uint32_t H) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= K) return;
+  uint32_t e = q + 1 < K ? first[q + 1] : H;
+  count[q] = e - first[q];
+}
+
+// gather item attributes into map order
+__global__ void k_item_permute(ItemsSoA in, const uint32_t* __restrict__ order, ItemsSoA out, uint32_t K) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= K) return;
+  uint32_t s = order[q];
+  out.pos[q] = in.pos[s];
+  out.len[q] = in.len[s];
+  out.isa[q] = in.isa[s];
+  out.smaller[q] = in.smaller[s];
+  out.until[q] = in.until[s];
+  out.count[q] = in.count[s];
+  out.first[q] = in.first[s];
+}
+
+// posBegin[p] = first item (map order) with pos >= p, p in [0, n]
+__global__ void k_pos_begin(const uint32_t* __restrict__ ipos, uint32_t K, uint32_t n,
+                            uint32_t* __restrict__ posBegin) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q > K) return;
+  uint32_t lo = q == 0 ? 0 : ipos[q - 1] + 1;
+  uint32_t hi = q == K ? n : ipos[q];
+  for (uint32_t p = lo; p <= hi; p++) posBegin[p] = q;
+}
+
+// posF[p] = first smaller=false item of position p (= posBegin[p+1] if none)
+__global__ void k_pos_f(const uint32_t* __restrict__ ipos, const uint8_t* __restrict__ ism,
+                        const uint32_t* __restrict__ posBegin, uint32_t K, uint32_t n,
+                        uint32_t* __restrict__ posF) {
+  uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  uint32_t b = posBegin[p], e = posBegin[p + 1];
+  uint32_t lo = b, hi = e;  // first item in [b, e) with smaller == 0 (T items come first)
+  while (lo < hi) {
+    uint32_t m = (lo + hi) >> 1;
+    if (ism[m]) lo = m + 1; else hi = m;
+  }
+  posF[p] = lo;
+}
+
+// Map-order consistency: for every position, every smaller=true item of
+// length L must have isaNext below every smaller=false item of length L,
+// otherwise match.h's comparator is not a strict weak order there and
+// std::map's layout depends on insertion history.
+__global__ void k_check_items(const ItemsSoA it, const uint32_t* __restrict__ posBegin,
+                              const uint32_t* __restrict__ posF, uint32_t K,
+                              unsigned long long* __restrict__ violations) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= K || !it.smaller[q]) return;
+  uint32_t p = it.pos[q], L = it.len[q];
+  uint32_t f = posF[p], e = posBegin[p + 1];
+  if (q + 1 < f && it.len[q + 1] == L) return;  // only the last T item of this length
+  // F part sorted by len descending: first item with len <= L
+  uint32_t lo = f, hi = e;
+  while (lo < hi) {
+    uint32_t m = (lo + hi) >> 1;
+    if (it.len[m] > L) lo = m + 1; else hi = m;
+  }
+  if (lo < e && it.len[lo] == L && it.isa[lo] <= it.isa[q]) atomicAdd(violations, 1ull);
+}
+
+// per SA rank: items and heads of position SA[r] (r = 0 -> position n-1 is
+// accounted separately: its heads are the end phrases)
+__global__ void k_sa_counts(const int32_t* __restrict__ sa, const uint32_t* __restrict__ posBegin,
+                            const uint32_t* __restrict__ slot, uint32_t n, uint32_t E,
+                            uint32_t* __restrict__ itemsSA, uint32_t* __restrict__ headsSA) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  if (r == 0) { itemsSA[0] = 0; headsSA[0] = E; return; }
+  uint32_t p = (uint32_t)sa[r];
+  uint32_t b = posBegin[p], e = posBegin[p + 1];
+  itemsSA[r] = e - b;
+  headsSA[r] = slot[e] - slot[b];
+}
+
+// Ranks of FN:1432-1453 and the initial (first-symbol) order of the head
+// string for the suffix sort (FN:1455-1459).
+__global__ void k_ranks(const ItemsSoA it, uint32_t K, const uint32_t* __restrict__ perm,
+                        const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ isaRef,
+                        const uint32_t* __restrict__ itemRankBase, const uint32_t* __restrict__ headBase,
+                        uint32_t n, uint32_t E, int32_t* __restrict__ T, uint32_t* __restrict__ sa,
+                        uint32_t* __restrict__ grp) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= K) return;
+  uint32_t p = it.pos[q];
+  uint32_t cnt = it.count[q], f = it.first[q];
+  if (p == n - 1) {  // end phrases: one rank each, in document order
+    for (uint32_t m = 0; m < cnt; m++) {
+      uint32_t idx = perm[f + m];
+      T[idx] = (int32_t)(1 + m);
+      sa[1 + m] = idx;
+      grp[idx] = 1 + m;
+    }
+    return;
+  }
+  uint32_t r = isaRef[p];
+  uint32_t b = posBegin[p];
+  int32_t rank = (int32_t)(E + 2 + itemRankBase[r] + (q - b));
+  uint32_t g = 1 + headBase[r] + (it.slot[q] - it.slot[b]);
+  for (uint32_t m = 0; m < cnt; m++) {
+    uint32_t idx = perm[f + m];
+    T[idx] = rank;
+    sa[g + m] = idx;
+    grp[idx] = g;
+  }
+}
+
+// unresolved members: sa positions of items with >= 2 heads (not end phrases)
+__global__ void k_active_init(const ItemsSoA it, uint32_t K, uint32_t n, const uint32_t* __restrict__ isaRef,
+                              const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ headBase,
+                              const uint32_t* __restrict__ actOff, uint32_t* __restrict__ act) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= K) return;
+  uint32_t p = it.pos[q], cnt = it.count[q];
+  if (p == n - 1 || cnt < 2) return;
+  uint32_t b = posBegin[p];
+  uint32_t g = 1 + headBase[isaRef[p]] + (it.slot[q] - it.slot[b]);
+  uint32_t o = actOff[q];
+  for (uint32_t m = 0; m < cnt; m++) act[o + m] = g + m;
+}
+
+__global__ void k_active_count(const ItemsSoA it, uint32_t K, uint32_t n, uint32_t* __restrict__ c) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= K) return;
+  c[q] = (it.pos[q] == n - 1 || it.count[q] < 2) ? 0 : it.count[q];
+}
+
+// prefix doubling: key = (group of suffix, group of suffix + h)
+__global__ void k_dbl_keys(const uint32_t* __restrict__ act, const uint32_t* __restrict__ sa,
+                           const uint32_t* __restrict__ grp, uint32_t h, uint32_t U,
+                           uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+  uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  uint32_t idx = sa[act[u]];
+  key[u] = ((uint64_t)grp[idx] << 32) | grp[idx + h];
+  val[u] = idx;
+}
+
+// write the sorted members back and compute the new group starts
+__global__ void k_dbl_apply(const uint32_t* __restrict__ act, const uint64_t* __restrict__ key,
+                            const uint32_t* __restrict__ val, uint32_t U, uint32_t* __restrict__ sa,
+                            uint32_t* __restrict__ lab) {
+  uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  sa[act[u]] = val[u];
+  lab[u] = (u == 0 || key[u] != key[u - 1]) ? act[u] : 0u;
+}
+
+// grp update + which members stay unresolved (their new group has >= 2 members)
+__global__ void k_dbl_groups(const uint32_t* __restrict__ act, const uint64_t* __restrict__ key,
+                             const uint32_t* __restrict__ val, const uint32_t* __restrict__ labMax,
+                             uint32_t U, uint32_t* __restrict__ grp, uint32_t* __restrict__ keep) {
+  uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  grp[val[u]] = labMax[u];
+  bool startHere = (u == 0 || key[u] != key[u - 1]);
+  bool endHere = (u + 1 == U || key[u + 1] != key[u]);
+  keep[u] = (startHere && endHere) ? 0u : 1u;
+}
+
+// FN:1468-1472: rank of each head and BWTheads (listOfChars in rank order)
+__global__ void k_head_ranks(const uint32_t* __restrict__ sa, const uint8_t* __restrict__ lchar, uint32_t H,
+                             uint32_t* __restrict__ headRank, uint8_t* __restrict__ bwtHeads) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= H) return;
+  uint32_t idx = sa[r + 1];
+  headRank[idx] = r;
+  bwtHeads[r] = lchar[idx];
+}
+
+// FN:1480-1494: next-head rank per member, keyed by item for the per-item sort
+__global__ void k_nhr_keys(const ItemsSoA it, uint32_t K, const uint32_t* __restrict__ perm,
+                           const uint32_t* __restrict__ headRank, const uint16_t* __restrict__ nexthead,
+                           uint64_t* __restrict__ key) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= K) return;
+  uint32_t cnt = it.count[q], f = it.first[q], s = it.slot[q];
+  for (uint32_t m = 0; m < cnt; m++) {
+    uint32_t idx = perm[f + m];
+    key[s + m] = ((uint64_t)q << 32) | headRank[idx + nexthead[idx]];
+  }
+}
+
+__global__ void k_low32(const uint64_t* __restrict__ key, uint32_t* __restrict__ out, uint64_t n) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) out[i] = (uint32_t)key[i];
+}
+
+// ------------------------------------------------------------ counterSmallerThanHead
+// FN:1523-1603.  Work unit (item q, offset k < untilNext): the non-head
+// suffix k+1 positions after the item's heads is placed among the items of
+// position t = pos+1+k by std::map::lower_bound semantics.
+struct CounterArgs {
+  ItemsSoA it;
+  uint32_t K;
+  const uint64_t* wp;        // exclusive prefix of untilNext (K+1)
+  uint64_t W;
+  const uint8_t* hasHead;    // bucket < 0
+  const uint32_t* posBegin;
+  const uint32_t* posF;
+  const uint32_t* nhr;       // sorted next-head ranks, slot order
+  unsigned long long* counter;
+  unsigned long long* stats; // bad, good, nothing, violations, errors
+  uint32_t n;
+  uint32_t perBlock;         // work units per block
+};
+
+__device__ __forceinline__ uint32_t d_upper_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t v) {
+  while (lo < hi) {
+    uint32_t m = (lo + hi) >> 1;
+    if (a[m] <= v) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(256) k_counter(CounterArgs A) {
+  const ItemsSoA& it = A.it;
+  uint64_t base = (uint64_t)blockIdx.x * A.perBlock;
+  uint64_t w = base + threadIdx.x;
+  uint64_t wend = min(base + A.perBlock, A.W);
+  unsigned long long bad = 0, good = 0, nothing = 0, viol = 0, errs = 0;
+  if (w < wend) {
+    // item containing w: last q with wp[q] <= w
+    uint32_t lo = 0, hi = A.K;
+    while (hi - lo > 1) {
+      uint32_t m = (lo + hi) >> 1;
+      if (A.wp[m] <= w) lo = m; else hi = m;
+    }
+    uint32_t q = lo;
+    for (; w < wend; w += blockDim.x) {
+      while (A.wp[q + 1] <= w) q++;
+      const uint32_t k = (uint32_t)(w - A.wp[q]);
+      const uint32_t p = it.pos[q];
+      const uint64_t t64 = (uint64_t)p + 1 + k;
+      if (t64 >= A.n) { errs++; continue; }
+      const uint32_t t = (uint32_t)t64;
+      if (!A.hasHead[t]) { nothing++; continue; }
+      const uint32_t L = it.len[q] - 1 - k;
+      const uint32_t I = it.isa[q];
+      const bool S = it.smaller[q] != 0;
+      const uint32_t b0 = A.posBegin[t], b1 = A.posBegin[t + 1], f = A.posF[t];
+      uint32_t ans;
+      if (S) {
+        // T part: (len < L) || (len == L && isa < I)
+        uint32_t l2 = b0, h2 = f;
+        while (l2 < h2) {
+          uint32_t m = (l2 + h2) >> 1;
+          uint32_t lm = it.len[m];
+          bool pr = lm < L || (lm == L && it.isa[m] < I);
+          if (pr) l2 = m + 1; else h2 = m;
+        }
+        ans = l2;
+        // violation: an F item with len == L and isa < I
+        uint32_t l3 = f, h3 = b1;
+        while (l3 < h3) {
+          uint32_t m = (l3 + h3) >> 1;
+          if (it.len[m] > L) l3 = m + 1; else h3 = m;
+        }
+        if (l3 < b1 && it.len[l3] == L && it.isa[l3] < I) viol++;
+      } else {
+        // violation: a T item with len == L and isa >= I (last T item of len L)
+        uint32_t l3 = b0, h3 = f;
+        while (l3 < h3) {
+          uint32_t m = (l3 + h3) >> 1;
+          if (it.len[m] <= L) l3 = m + 1; else h3 = m;
+        }
+        if (l3 > b0 && it.len[l3 - 1] == L && it.isa[l3 - 1] >= I) viol++;
+        // F part: (len > L) || (len == L && isa < I)
+        uint32_t l2 = f, h2 = b1;
+        while (l2 < h2) {
+          uint32_t m = (l2 + h2) >> 1;
+          uint32_t lm = it.len[m];
+          bool pr = lm > L || (lm == L && it.isa[m] < I);
+          if (pr) l2 = m + 1; else h2 = m;
+        }
+        ans = l2;
+      }
+      if (ans >= b1) continue;  // lower_bound == end(): FN:1535-1536
+      const uint32_t cq = it.count[q];
+      const uint32_t sa_ = it.slot[ans];
+      if (it.len[ans] == L && it.isa[ans] == I) {  // same key: FN:1537-1589
+        const uint32_t co = it.count[ans];
+        const bool hasNext = ans + 1 < b1;
+        const uint32_t* me = A.nhr + it.slot[q];
+        const uint32_t* ot = A.nhr + sa_;
+        if (me[cq - 1] < ot[0]) {
+          atomicAdd(&A.counter[sa_], (unsigned long long)cq);
+          good++;
+        } else if (me[0] > ot[co - 1]) {
+          if (hasNext) atomicAdd(&A.counter[sa_ + co], (unsigned long long)cq);
+          good++;
+        } else {
+          bad++;
+          uint32_t rest = 0;
+          for (uint32_t a = 0; a < cq; a++) {
+            uint32_t bpos = d_upper_u32(ot, 0, co, me[a]);
+            if (bpos < co) atomicAdd(&A.counter[sa_ + bpos], 1ull);
+            else rest++;
+          }
+          if (rest && hasNext) atomicAdd(&A.counter[sa_ + co], (unsigned long long)rest);
+        }
+      } else {
+        atomicAdd(&A.counter[sa_], (unsigned long long)cq);
+        good++;
+      }
+    }
+  }
+  // block reduction of the statistics
+  __shared__ unsigned long long red[5];
+  if (threadIdx.x < 5) red[threadIdx.x] = 0;
+  __syncthreads();
+  if (bad) atomicAdd(&red[0], bad);
+  if (good) atomicAdd(&red[1], good);
+  if (nothing) atomicAdd(&red[2], nothing);
+  if (viol) atomicAdd(&red[3], viol);
+  if (errs) atomicAdd(&red[4], errs);
+  __syncthreads();
+  if (threadIdx.x < 5 && red[threadIdx.x]) atomicAdd(&A.stats[threadIdx.x], red[threadIdx.x]);
+}
+
+// ------------------------------------------------------------ buckets (FN:1162-1171, 1618-1628)
+__global__ void k_bucket(const int32_t* __restrict__ countIncl, const uint8_t* __restrict__ hasHead, uint32_t n,
+                         int64_t* __restrict__ bucket) {
+  uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  int64_t c = countIncl[p];
+  bucket[p] = hasHead[p] ? -c : c;
+}
+
+// ------------------------------------------------------------ writer (FN:1631-1777)
+struct WriterArgs {
+  const int32_t* sa;
+  const uint8_t* bwt;
+  const int64_t* bucket;     // pos-indexed (the inversion is this gather)
+  const uint32_t* posBegin;
+  const uint32_t* slot;      // K+1
+  const uint32_t* count;
+  const uint32_t* headBase;  // per SA rank
+  const uint8_t* bwtHeads;
+  const unsigned long long* counter;
+  uint32_t n;
+  uint32_t E;
+  int rle;                   // 1: .rl_bwt remainder quirk (FN:1761-1770); 0: .bwt (FN:1678-1686)
+};
+
+template <bool EMIT>
+__device__ __forceinline__ uint64_t d_segments(const WriterArgs& A, uint32_t r, uint8_t* oc,
+                                               unsigned long long* on) {
+  const uint32_t p = (uint32_t)A.sa[r];
+  const uint8_t c = A.bwt[r];
+  const int64_t b = A.bucket[p];
+  uint64_t ns = 0;
+  if (b > 0) {
+    if (EMIT) { oc[0] = c; on[0] = (unsigned long long)b; }
+    return 1;
+  }
+  if (b == 0) return 0;
+  int64_t acc = b;
+  const uint32_t i0 = A.posBegin[p], i1 = A.posBegin[p + 1];
+  const uint32_t s0 = A.slot[i0];
+  const uint32_t hb = A.headBase[r];
+  for (uint32_t q = i0; q < i1; q++) {
+    const uint32_t sb = A.slot[q], se = sb + A.count[q];
+    for (uint32_t s = sb; s < se; s++) {
+      const unsigned long long cs = A.counter[s];
+      if (cs) {
+        if (EMIT) { oc[ns] = c; on[ns] = cs; }
+        ns++;
+        acc += (int64_t)cs;
+      }
+      if (EMIT) { oc[ns] = A.bwtHeads[hb + (s - s0)]; on[ns] = 1; }
+      ns++;
+      acc++;
+    }
+    if (A.rle && acc != 0) {
+      if (EMIT) { oc[ns] = c; on[ns] = (unsigned long long)(-acc); }
+      ns++;
+    }
+  }
+  if (!A.rle && acc < 0) {
+    if (EMIT) { oc[ns] = c; on[ns] = (unsigned long long)(-acc); }
+    ns++;
+  }
+  return ns;
+}
+
+__global__ void k_seg_count(WriterArgs A, unsigned long long* __restrict__ segN) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= A.n) return;
+  segN[r] = r == 0 ? 0 : d_segments<false>(A, r, nullptr, nullptr);
+}
+
+__global__ void k_seg_emit(WriterArgs A, const unsigned long long* __restrict__ segOff, uint8_t* __restrict__ sc,
+                           unsigned long long* __restrict__ sn) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= A.n) return;
+  if (r == 0) {
+    for (uint32_t d = 0; d < A.E; d++) { sc[d] = A.bwtHeads[d]; sn[d] = 1; }
+    return;
+  }
+  uint64_t o = A.E + segOff[r];
+  d_segments<true>(A, r, sc + o, sn + o);
+}
+
+__global__ void k_run_flags(const uint8_t* __restrict__ sc, uint64_t S, unsigned long long* __restrict__ flag) {
+  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= S) return;
+  flag[k] = (k == 0 || sc[k] != sc[k - 1]) ? 1ull : 0ull;
+}
+
+// runId = inclusive scan of flags (1-based); cum = inclusive scan of counts.
+__global__ void k_run_pack(const uint8_t* __restrict__ sc, const unsigned long long* __restrict__ runId,
+                           const unsigned long long* __restrict__ cum, uint64_t S,
+                           unsigned long long* __restrict__ runEnd, uint8_t* __restrict__ runChar) {
+  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= S) return;
+  if (k + 1 == S || runId[k + 1] != runId[k]) {
+    uint64_t j = runId[k] - 1;
+    runEnd[j] = cum[k];
+    runChar[j] = sc[k];
+  }
+}
+
+__global__ void k_run_records(const unsigned long long* __restrict__ runEnd, const uint8_t* __restrict__ runChar,
+                              uint64_t R, uint8_t* __restrict__ out) {
+  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= R) return;
+  uint64_t len = runEnd[j] - (j ? runEnd[j - 1] : 0ull);
+  uint8_t* o = out + 9 * j;
+#pragma unroll
+  for (int b = 0; b < 8; b++) o[b] = (uint8_t)(len >> (8 * b));
+  o[8] = runChar[j];
+}
+
+// ------------------------------------------------------------ launchers
+static inline dim3 g1(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+void mk_iota(uint32_t* p, uint64_t n, hipStream_t st) { if (n) hipLaunchKernelGGL(k_iota, g1(n), dim3(256), 0, st, p, n); }
+void mk_gather(const uint32_t* src, const uint32_t* perm, uint32_t* dst, uint64_t n, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_gather_u32, g1(n), dim3(256), 0, st, src, perm, dst, n);
+}
+void mk_item_key(const uint32_t* len, const uint8_t* sm, const uint32_t* perm, uint32_t* key, uint64_t n,
+                 hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_item_key, g1(n), dim3(256), 0, st, len, sm, perm, key, n);
+}
+void mk_item_flags(const uint32_t* perm, const HeadsSoA& h, uint32_t* flag, uint64_t H, hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_item_flags, g1(H), dim3(256), 0, st, perm, h.pos, h.len, h.isa, flag, H);
+}
+void mk_item_fill(const uint32_t* perm, const uint32_t* flag, const uint32_t* incl, const HeadsSoA& h,
+                  uint64_t H, const ItemsSoA& it, hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_item_fill, g1(H), dim3(256), 0, st, perm, flag, incl, h, H, it);
+}
+void mk_item_count(const uint32_t* first, uint32_t* count, uint32_t K, uint32_t H, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_item_count, g1(K), dim3(256), 0, st, first, count, K, H);
+}
+void mk_item_permute(const ItemsSoA& in, const uint32_t* order, const ItemsSoA& out, uint32_t K, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_item_permute, g1(K), dim3(256), 0, st, in, order, out, K);
+}
+void mk_pos_begin(const uint32_t* ipos, uint32_t K, uint32_t n, uint32_t* posBegin, hipStream_t st) {
+  hipLaunchKernelGGL(k_pos_begin, g1((uint64_t)K + 1), dim3(256), 0, st, ipos, K, n, posBegin);
+}
+void mk_pos_f(const uint32_t* ipos, const uint8_t* ism, const uint32_t* posBegin, uint32_t K, uint32_t n,
+              uint32_t* posF, hipStream_t st) {
+  hipLaunchKernelGGL(k_pos_f, g1(n), dim3(256), 0, st, ipos, ism, posBegin, K, n, posF);
+}
+void mk_check_items(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, uint32_t K,
+                    unsigned long long* viol, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_check_items, g1(K), dim3(256), 0, st, it, posBegin, posF, K, viol);
+}
+void mk_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t E,
+                  uint32_t* itemsSA, uint32_t* headsSA, hipStream_t st) {
+  hipLaunchKernelGGL(k_sa_counts, g1(n), dim3(256), 0, st, sa, posBegin, slot, n, E, itemsSA, headsSA);
+}
+void mk_ranks(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uint32_t* posBegin,
+              const uint32_t* isaRef, const uint32_t* itemRankBase, const uint32_t* headBase, uint32_t n,
+              uint32_t E, int32_t* T, uint32_t* sa, uint32_t* grp, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_ranks, g1(K), dim3(256), 0, st, it, K, perm, posBegin, isaRef, itemRankBase,
+                            headBase, n, E, T, sa, grp);
+}
+void mk_active_count(const ItemsSoA& it, uint32_t K, uint32_t n, uint32_t* c, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_active_count, g1(K), dim3(256), 0, st, it, K, n, c);
+}
+void mk_active_init(const ItemsSoA& it, uint32_t K, uint32_t n, const uint32_t* isaRef,
+                    const uint32_t* posBegin, const uint32_t* headBase, const uint32_t* actOff,
+                    uint32_t* act, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_active_init, g1(K), dim3(256), 0, st, it, K, n, isaRef, posBegin, headBase,
+                            actOff, act);
+}
+void mk_dbl_keys(const uint32_t* act, const uint32_t* sa, const uint32_t* grp, uint32_t h, uint32_t U,
+                 uint64_t* key, uint32_t* val, hipStream_t st) {
+  if (U) hipLaunchKernelGGL(k_dbl_keys, g1(U), dim3(256), 0, st, act, sa, grp, h, U, key, val);
+}
+void mk_dbl_apply(const uint32_t* act, const uint64_t* key, const uint32_t* val, uint32_t U, uint32_t* sa,
+                  uint32_t* lab, hipStream_t st) {
+  if (U) hipLaunchKernelGGL(k_dbl_apply, g1(U), dim3(256), 0, st, act, key, val, U, sa, lab);
+}
+void mk_dbl_groups(const uint32_t* act, const uint64_t* key, const uint32_t* val, const uint32_t* labMax,
+                   uint32_t U, uint32_t* grp, uint32_t* keep, hipStream_t st) {
+  if (U) hipLaunchKernelGGL(k_dbl_groups, g1(U), dim3(256), 0, st, act, key, val, labMax, U, grp, keep);
+}
+void mk_head_ranks(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint32_t* headRank, uint8_t* bwtHeads,
+                   hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_head_ranks, g1(H), dim3(256), 0, st, sa, lchar, H, headRank, bwtHeads);
+}
+void mk_nhr_keys(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uint32_t* headRank,
+                 const uint16_t* nexthead, uint64_t* key, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_nhr_keys, g1(K), dim3(256), 0, st, it, K, perm, headRank, nexthead, key);
+}
+void mk_low32(const uint64_t* key, uint32_t* out, uint64_t n, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_low32, g1(n), dim3(256), 0, st, key, out, n);
+}
+void mk_counter(const ItemsSoA& it, uint32_t K, const uint64_t* wp, uint64_t W, const uint8_t* hasHead,
+                const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
+                unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st) {
+  if (!W) return;
+  CounterArgs A{it, K, wp, W, hasHead, posBegin, posF, nhr, counter, stats, n, 256 * 16};
+  uint64_t blocks = (W + A.perBlock - 1) / A.perBlock;
+  hipLaunchKernelGGL(k_counter, dim3((unsigned)blocks), dim3(256), 0, st, A);
+}
+void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st) {
+  hipLaunchKernelGGL(k_bucket, g1(n), dim3(256), 0, st, countIncl, hasHead, n, bucket);
+}
+void mk_seg_count(const WriterIn& w, unsigned long long* segN, hipStream_t st) {
+  WriterArgs A{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.count, w.headBase, w.bwtHeads, w.counter,
+               w.n, w.E, w.rle};
+  hipLaunchKernelGGL(k_seg_count, g1(w.n), dim3(256), 0, st, A, segN);
+}
+void mk_seg_emit(const WriterIn& w, const unsigned long long* segOff, uint8_t* sc, unsigned long long* sn,
+                 hipStream_t st) {
+  WriterArgs A{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.count, w.headBase, w.bwtHeads, w.counter,
+               w.n, w.E, w.rle};
+  hipLaunchKernelGGL(k_seg_emit, g1(w.n), dim3(256), 0, st, A, segOff, sc, sn);
+}
+void mk_run_flags(const uint8_t* sc, uint64_t S, unsigned long long* flag, hipStream_t st) {
+  if (S) hipLaunchKernelGGL(k_run_flags, g1(S), dim3(256), 0, st, sc, S, flag);
+}
+void mk_run_pack(const uint8_t* sc, const unsigned long long* runId, const unsigned long long* cum, uint64_t S,
+                 unsigned long long* runEnd, uint8_t* runChar, hipStream_t st) {
+  if (S) hipLaunchKernelGGL(k_run_pack, g1(S), dim3(256), 0, st, sc, runId, cum, S, runEnd, runChar);
+}
+void mk_run_records(const unsigned long long* runEnd, const uint8_t* runChar, uint64_t R, uint8_t* out,
+                    hipStream_t st) {
+  if (R) hipLaunchKernelGGL(k_run_records, g1(R), dim3(256), 0, st, runEnd, runChar, R, out);
+}
+
+}  // namespace cmsbwt

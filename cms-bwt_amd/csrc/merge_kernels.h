@@ -1,0 +1,71 @@
+// merge_kernels.h — launchers for merge.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "kernels.h"
+
+namespace cmsbwt {
+
+struct WriterIn {
+  const int32_t* sa;
+  const uint8_t* bwt;
+  const int64_t* bucket;
+  const uint32_t* posBegin;
+  const uint32_t* slot;
+  const uint32_t* count;
+  const uint32_t* headBase;
+  const uint8_t* bwtHeads;
+  const unsigned long long* counter;
+  uint32_t n;
+  uint32_t E;
+  int rle;
+};
+
+void mk_iota(uint32_t* p, uint64_t n, hipStream_t st);
+void mk_gather(const uint32_t* src, const uint32_t* perm, uint32_t* dst, uint64_t n, hipStream_t st);
+void mk_item_key(const uint32_t* len, const uint8_t* sm, const uint32_t* perm, uint32_t* key, uint64_t n,
+                 hipStream_t st);
+void mk_item_flags(const uint32_t* perm, const HeadsSoA& h, uint32_t* flag, uint64_t H, hipStream_t st);
+void mk_item_fill(const uint32_t* perm, const uint32_t* flag, const uint32_t* incl, const HeadsSoA& h,
+                  uint64_t H, const ItemsSoA& it, hipStream_t st);
+void mk_item_count(const uint32_t* first, uint32_t* count, uint32_t K, uint32_t H, hipStream_t st);
+void mk_item_permute(const ItemsSoA& in, const uint32_t* order, const ItemsSoA& out, uint32_t K, hipStream_t st);
+void mk_pos_begin(const uint32_t* ipos, uint32_t K, uint32_t n, uint32_t* posBegin, hipStream_t st);
+void mk_pos_f(const uint32_t* ipos, const uint8_t* ism, const uint32_t* posBegin, uint32_t K, uint32_t n,
+              uint32_t* posF, hipStream_t st);
+void mk_check_items(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, uint32_t K,
+                    unsigned long long* viol, hipStream_t st);
+void mk_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t E,
+                  uint32_t* itemsSA, uint32_t* headsSA, hipStream_t st);
+void mk_ranks(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uint32_t* posBegin,
+              const uint32_t* isaRef, const uint32_t* itemRankBase, const uint32_t* headBase, uint32_t n,
+              uint32_t E, int32_t* T, uint32_t* sa, uint32_t* grp, hipStream_t st);
+void mk_active_count(const ItemsSoA& it, uint32_t K, uint32_t n, uint32_t* c, hipStream_t st);
+void mk_active_init(const ItemsSoA& it, uint32_t K, uint32_t n, const uint32_t* isaRef,
+                    const uint32_t* posBegin, const uint32_t* headBase, const uint32_t* actOff,
+                    uint32_t* act, hipStream_t st);
+void mk_dbl_keys(const uint32_t* act, const uint32_t* sa, const uint32_t* grp, uint32_t h, uint32_t U,
+                 uint64_t* key, uint32_t* val, hipStream_t st);
+void mk_dbl_apply(const uint32_t* act, const uint64_t* key, const uint32_t* val, uint32_t U, uint32_t* sa,
+                  uint32_t* lab, hipStream_t st);
+void mk_dbl_groups(const uint32_t* act, const uint64_t* key, const uint32_t* val, const uint32_t* labMax,
+                   uint32_t U, uint32_t* grp, uint32_t* keep, hipStream_t st);
+void mk_head_ranks(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint32_t* headRank, uint8_t* bwtHeads,
+                   hipStream_t st);
+void mk_nhr_keys(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uint32_t* headRank,
+                 const uint16_t* nexthead, uint64_t* key, hipStream_t st);
+void mk_low32(const uint64_t* key, uint32_t* out, uint64_t n, hipStream_t st);
+void mk_counter(const ItemsSoA& it, uint32_t K, const uint64_t* wp, uint64_t W, const uint8_t* hasHead,
+                const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
+                unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st);
+void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st);
+void mk_seg_count(const WriterIn& w, unsigned long long* segN, hipStream_t st);
+void mk_seg_emit(const WriterIn& w, const unsigned long long* segOff, uint8_t* sc, unsigned long long* sn,
+                 hipStream_t st);
+void mk_run_flags(const uint8_t* sc, uint64_t S, unsigned long long* flag, hipStream_t st);
+void mk_run_pack(const uint8_t* sc, const unsigned long long* runId, const unsigned long long* cum, uint64_t S,
+                 unsigned long long* runEnd, uint8_t* runChar, hipStream_t st);
+void mk_run_records(const unsigned long long* runEnd, const uint8_t* runChar, uint64_t R, uint8_t* out,
+                    hipStream_t st);
+
+}  // namespace cmsbwt

@@ -1,0 +1,125 @@
+/* cmsbwt.h — C ABI of the MI355X-native CMS-BWT engine (libcmsbwt.so).
+ *
+ * The reference (fmasillo/CMS-BWT) has no plugin/FFI surface: its boundary is
+ * the `cmsbwt` process plus one C++ function,
+ *     void computeBWT(Args, std::string& ref, std::string& coll)
+ * (CMS-BWT.h:69, CMS-BWT-functions.cpp:1788-1797), which is non-reentrant,
+ * owns all memory and reports errors with exit().  This header is what a
+ * maintainer would bind instead (ctypes / cgo / JNI stubs in INTEGRATION.md):
+ *   - cmsbwt_run()      replaces computeBWT() (+ main.cpp's list-file step);
+ *   - the ctx API       exposes the hot path stage by stage for parity tests
+ *                       and for callers that keep inputs resident in HBM.
+ * Plain pointers and sizes only; all functions return 0 on success and a
+ * CMSBWT_E* code otherwise (never exit()).  One context per thread.
+ */
+#ifndef CMSBWT_H
+#define CMSBWT_H
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CMSBWT_OK 0
+#define CMSBWT_EIO 1        /* file missing/unreadable (reference: exit(1))        */
+#define CMSBWT_EARG 2       /* bad argument / call order                            */
+#define CMSBWT_EINPUT 3     /* input on which the reference is undefined            */
+#define CMSBWT_EDEVICE 4    /* HIP runtime error or HIP code object not loadable    */
+#define CMSBWT_ELIMIT 5     /* size limit (reference int32/uint32 limits)           */
+#define CMSBWT_EORDER 6     /* map comparator ambiguity (match.h:27-33) detected    */
+
+/* utils.h:8-14 struct Args, plus engine knobs. */
+typedef struct cmsbwt_args {
+  uint64_t prefix;      /* -p  (UINT64_MAX = whole file), FN:223, FN:1258-1263  */
+  uint32_t buffer_gb;   /* -b  (small path memory knob only; no output effect)  */
+  int32_t rle;          /* -r  1 = <out>.rl_bwt, 0 = <out>.bwt                  */
+  const char* outname;  /* -o  basename (NULL = list file name)                 */
+  int32_t device;       /* HIP device ordinal                                   */
+  int32_t verbose;      /* 1 = stage times on stderr                            */
+} cmsbwt_args;
+
+/* Statistics mirrored from the reference .log (FN:1417-1422, 1452, 1515,
+ * 1606-1608) plus engine timings. */
+typedef struct cmsbwt_stats {
+  uint64_t n;             /* augmented reference length _n                      */
+  uint64_t sn;            /* _sn after the collection pass                      */
+  uint64_t ndocs;         /* documents = D-1                                    */
+  uint64_t chars;         /* collection sequence bytes N (separators excluded)  */
+  uint64_t heads;         /* headNumber                                         */
+  uint64_t positions;     /* phrasesSet.size()                                  */
+  uint64_t keys;          /* uniqueHeadNumber (distinct (pos,len,isaNext))      */
+  uint64_t rank;          /* final Rank                                         */
+  uint64_t current_sum;   /* currentSum                                         */
+  uint64_t counter_bad, counter_good, counter_nothing;
+  uint64_t runs;          /* records in .rl_bwt (or runs of .bwt)               */
+  uint64_t symbols;       /* sum of run lengths                                 */
+  uint64_t order_violations; /* comparator ambiguities seen (must be 0)         */
+  double t_index_s, t_upload_s, t_ms_walk_s, t_merge_s, t_write_s;
+  double ms_walk_kernel_ms;  /* device time of the MS-walk kernel               */
+} cmsbwt_stats;
+
+typedef struct cmsbwt_ctx cmsbwt_ctx;
+
+/* Whole run, replaces computeBWT (FN:1788) for the CLI: index the reference,
+ * read the collection with the reference's getline semantics, compute, write
+ * <outname>.rl_bwt | .bwt (+ .counterSmallerThanHead_true when _n < 1e6,
+ * FN:919-924) and <outname>.log. */
+int cmsbwt_run(const cmsbwt_args* args, const char* ref_path, const char* coll_path,
+               cmsbwt_stats* stats_out);
+
+int cmsbwt_ctx_create(int device, cmsbwt_ctx** out);
+void cmsbwt_ctx_destroy(cmsbwt_ctx* ctx);
+const char* cmsbwt_last_error(const cmsbwt_ctx* ctx);
+
+/* initialize_reference (FN:151-310): read FASTA/raw, trim (FN:208-213),
+ * augment (FN:231-237), SA/ISA/LCP/PLCP/BWT on the host, stage into HBM. */
+int cmsbwt_load_reference_file(cmsbwt_ctx* ctx, const char* ref_path);
+/* Same from bytes already read and trimmed (no augmentation applied yet). */
+int cmsbwt_load_reference(cmsbwt_ctx* ctx, const uint8_t* ref, uint64_t len);
+
+/* Collection reader (FN:1138-1275): getline semantics, '>'/blank lines split
+ * documents, unterminated last line dropped, -p cut.  Uploads to HBM. */
+int cmsbwt_load_collection_file(cmsbwt_ctx* ctx, const char* coll_path, uint64_t prefix);
+/* Documents from host memory: doc k = text[doc_off[k] .. doc_off[k+1]). */
+int cmsbwt_load_collection(cmsbwt_ctx* ctx, const uint8_t* text, const uint64_t* doc_off,
+                           uint64_t ndocs);
+/* Synthetic workload generated directly in HBM (synth.h):
+ * copies [copy_begin, copy_begin+ncopies) of the reference seeded by `seed`. */
+int cmsbwt_load_collection_synth(cmsbwt_ctx* ctx, uint64_t seed, uint64_t copy_begin,
+                                 uint64_t ncopies, double p, int leading_empty_doc);
+
+/* Hot path.  ms_walk = FN:1151-1212 (+ j-scan FN:1359-1385); merge = the
+ * rest of FN:1387-1777 into device-resident runs. */
+int cmsbwt_ms_walk(cmsbwt_ctx* ctx);
+int cmsbwt_merge(cmsbwt_ctx* ctx, int rle);
+/* ms_walk + merge, synchronised; the unit bench.py times. */
+int cmsbwt_step(cmsbwt_ctx* ctx, int rle);
+
+int cmsbwt_get_stats(const cmsbwt_ctx* ctx, cmsbwt_stats* out);
+/* Packed 9-byte (uint64 LE length, uint8 char) records, FN:1708-1709. */
+uint64_t cmsbwt_num_runs(const cmsbwt_ctx* ctx);
+int cmsbwt_copy_runs(cmsbwt_ctx* ctx, uint8_t* out, uint64_t cap_bytes);
+/* Write <outname>.rl_bwt (rle=1, runs of the last merge(rle=1)) or
+ * <outname>.bwt (rle=0, expanded runs of the last merge(rle=0)). */
+int cmsbwt_write_output(cmsbwt_ctx* ctx, const char* outname, int rle);
+
+/* Stage arrays for parity tests, named like the oracle's dumps:
+ * h_start h_pos h_len (u32) h_smaller h_lchar (u8) h_isa h_tonext (u32)
+ * h_nexthead (u16) bucket (i64, pos-indexed) rank2head head2rank (i32, H+1)
+ * bwtheads (u8, H) counters (u64, H+1).  Returns the byte size via *bytes
+ * when out == NULL. */
+int cmsbwt_copy_array(cmsbwt_ctx* ctx, const char* name, void* out, uint64_t* bytes);
+
+/* Host-only helpers (no GPU needed), exposed for tests of the host logic:
+ * the collection reader (FN:1138-1275) and the reference suffix array
+ * (libsais call site FN:247).  For the reader, pass NULL buffers to query
+ * sizes; text excludes separators, doc_off has ndocs+1 entries. */
+int cmsbwt_host_read_collection(const char* path, uint64_t prefix, uint8_t* text, uint64_t text_cap,
+                                uint64_t* text_len, uint64_t* doc_off, uint64_t doc_cap, uint64_t* ndocs,
+                                uint64_t* sn);
+int cmsbwt_host_suffix_array(const uint8_t* s, uint64_t n, int32_t* sa_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CMSBWT_H */

@@ -1,0 +1,101 @@
+"""GPU parity: every stage of the HIP path equals the CPU oracle, bit for bit.
+
+Stages (oracle dump name -> reference file:line):
+  h_start/h_pos/h_len/h_smaller/h_lchar  heads of the MS walk   FN:1151-1212
+  h_isa/h_tonext/h_nexthead              j-scan                 FN:1359-1385
+  bucket                                  per-position counts    FN:1162-1185
+  rank2head / head2rank                   ranks, libsais_int     FN:1432-1459
+  bwtheads                                BWTheads               FN:1468-1472
+  counters                                counterSmallerThanHead FN:1523-1603
+  .rl_bwt / .bwt bytes                    writers                FN:1631-1777
+"""
+import os
+
+import numpy as np
+import pytest
+
+import cases
+
+pytestmark = pytest.mark.gpu
+
+STAGES = ["h_start", "h_pos", "h_len", "h_smaller", "h_lchar", "h_isa", "h_tonext", "h_nexthead",
+          "bucket", "rank2head", "head2rank", "bwtheads", "counters"]
+
+
+def _compare(engine, oracle, tmp_path, case, chunk=None, rle=True):
+    import cmsbwt
+    d, rp, cp, prefix = cases.materialise(tmp_path, case)
+    dump = os.path.join(d, "dump")
+    rc, ost, _ = oracle.run(rp, cp, os.path.join(d, "oracle"), rle=rle, prefix=prefix, dump_dir=dump)
+    assert rc == 0
+    if chunk:
+        os.environ["CMSBWT_CHUNK"] = str(chunk)
+    try:
+        engine.initialize_reference(rp)
+        engine.load_collection_file(cp, prefix)
+        engine.ms_walk()
+        engine.merge(rle)
+    finally:
+        os.environ.pop("CMSBWT_CHUNK", None)
+    for s in STAGES:
+        got, want = engine.array(s), oracle.load_dump(dump, s)
+        assert got.shape == want.shape, f"{case[0]}: {s} shape {got.shape} vs {want.shape}"
+        if not np.array_equal(got, want):
+            bad = np.nonzero(got != want)[0]
+            raise AssertionError(f"{case[0]}: stage {s} differs at {len(bad)} entries, first {bad[:5]} "
+                                 f"got {got[bad[:5]]} want {want[bad[:5]]}")
+    st = engine.stats()
+    assert st.heads == ost["heads"] and st.keys == ost["keys"] and st.rank == ost["rank"]
+    assert (st.counter_bad, st.counter_good, st.counter_nothing) == (ost["bad"], ost["good"], ost["nothing"])
+    out = os.path.join(d, "gpu")
+    engine.write_output(out, rle)
+    ext = ".rl_bwt" if rle else ".bwt"
+    with open(out + ext, "rb") as f1, open(os.path.join(d, "oracle") + ext, "rb") as f2:
+        assert f1.read() == f2.read(), f"{case[0]}: {ext} bytes differ"
+    if st.n < 1_000_000:
+        with open(out + ".counterSmallerThanHead_true", "rb") as f1, \
+                open(os.path.join(d, "oracle.counterSmallerThanHead_true"), "rb") as f2:
+            assert f1.read() == f2.read()
+    return st
+
+
+@pytest.mark.parametrize("case", cases.small_cases(), ids=lambda c: c[0])
+def test_small_cases_rle(engine, oracle, tmp_path, case):
+    _compare(engine, oracle, tmp_path, case, rle=True)
+
+
+@pytest.mark.parametrize("case", cases.small_cases()[:6], ids=lambda c: c[0])
+def test_small_cases_plain_bwt(engine, oracle, tmp_path, case):
+    _compare(engine, oracle, tmp_path, case, rle=False)
+
+
+@pytest.mark.parametrize("chunk", [64, 257, 1000])
+@pytest.mark.parametrize("case", cases.small_cases()[:4], ids=lambda c: c[0])
+def test_chunk_restarts(engine, oracle, tmp_path, case, chunk):
+    """Tiny chunks force many restart points inside documents."""
+    _compare(engine, oracle, tmp_path, case, chunk=chunk)
+
+
+@pytest.mark.parametrize("case", cases.large_cases(), ids=lambda c: c[0])
+def test_large_reference_path(engine, oracle, tmp_path, case):
+    _compare(engine, oracle, tmp_path, case, rle=True)
+
+
+def test_config1_golden(engine, tmp_path):
+    """SURVEY.md config 1 (1 MB ref + 10 copies @0.1%, numpy generator of App. B,
+    seed 11): the reference recorded headNumber 87,853; the committed sha256 of
+    the oracle's .rl_bwt is the golden vector."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import gen_np
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["c1"]
+    pre = str(tmp_path / "c1")
+    gen_np.gen(1_000_000, 10, 0.001, 11, pre)
+    engine.initialize_reference(pre + ".ref.fa")
+    engine.load_collection_file(pre + ".coll.fa")
+    engine.step(rle=True)
+    import hashlib
+    st = engine.stats()
+    assert st.heads == g["headNumber"] == 87853
+    assert hashlib.sha256(engine.runs_bytes()).hexdigest() == g["rl_bwt_sha256"]

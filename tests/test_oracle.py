@@ -1,0 +1,83 @@
+"""CPU: the oracle is pinned before anything is compared against it.
+
+1. Its plain .bwt equals a brute-force multi-string BWT (mathematical definition).
+2. It reproduces outputs of the real reference recorded in SURVEY.md
+   (config 1 headNumber 87,853; the RLE-quirk symbol count 3,001,340 vs
+   3,000,004 plain bytes on t2), using the survey's numpy generator.
+3. It matches the committed small golden files (regression)."""
+import json
+import os
+
+import numpy as np
+import pytest
+
+import cases
+
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def _decode(path):
+    a = np.fromfile(path, dtype=np.uint8).reshape(-1, 9)
+    return a[:, :8].copy().view("<u8").ravel(), a[:, 8].copy()
+
+
+@pytest.mark.parametrize("case", cases.small_cases(), ids=lambda c: c[0])
+def test_oracle_plain_bwt_is_the_multistring_bwt(oracle, tmp_path, case):
+    d, rp, cp, prefix = cases.materialise(tmp_path, case)
+    rc, st, _ = oracle.run(rp, cp, os.path.join(d, "o"), rle=False, prefix=prefix)
+    assert rc == 0
+    docs, _ = cases.py_read_docs(case[2], prefix)
+    got = open(os.path.join(d, "o.bwt"), "rb").read()
+    assert got == cases.brute_force_bwt(docs)
+    assert st["D"] == len(docs) + 1
+
+
+@pytest.mark.parametrize("case", cases.small_cases()[:5], ids=lambda c: c[0])
+def test_oracle_rle_decodes_to_bwt_plus_quirk(oracle, tmp_path, case):
+    """.rl_bwt differs from RLE(.bwt) only by the per-item remainder (App. A-1):
+    it never has fewer symbols, and run chars alternate."""
+    d, rp, cp, prefix = cases.materialise(tmp_path, case)
+    assert oracle.run(rp, cp, os.path.join(d, "o"), rle=True, prefix=prefix)[0] == 0
+    assert oracle.run(rp, cp, os.path.join(d, "o"), rle=False, prefix=prefix)[0] == 0
+    lens, chars = _decode(os.path.join(d, "o.rl_bwt"))
+    assert (lens > 0).all() and (chars[1:] != chars[:-1]).all()
+    assert int(lens.sum()) >= os.path.getsize(os.path.join(d, "o.bwt"))
+
+
+def _gen(tmp_path, key):
+    import sys
+    sys.path.insert(0, GOLD)
+    import gen_np
+    g = json.load(open(os.path.join(GOLD, "golden.json")))
+    L, C, p, seed, w = g["survey"][key]["args"]
+    pre = str(tmp_path / key)
+    gen_np.gen(L, C, p, seed, pre, w)
+    return g, pre
+
+
+def test_oracle_reproduces_reference_config1(oracle, tmp_path):
+    g, pre = _gen(tmp_path, "c1")
+    rc, st, _ = oracle.run(pre + ".ref.fa", pre + ".coll.fa", pre + "_o", rle=True)
+    assert rc == 0
+    assert st["heads"] == g["survey"]["c1"]["headNumber"] == 87853
+    import hashlib
+    assert hashlib.sha256(open(pre + "_o.rl_bwt", "rb").read()).hexdigest() == g["c1"]["rl_bwt_sha256"]
+
+
+def test_oracle_reproduces_reference_rle_quirk_t2(oracle, tmp_path):
+    g, pre = _gen(tmp_path, "t2")
+    assert oracle.run(pre + ".ref.fa", pre + ".coll.fa", pre + "_r", rle=True)[0] == 0
+    assert oracle.run(pre + ".ref.fa", pre + ".coll.fa", pre + "_p", rle=False)[0] == 0
+    lens, _ = _decode(pre + "_r.rl_bwt")
+    assert int(lens.sum()) == g["survey"]["t2"]["rl_symbols"] == 3001340
+    assert os.path.getsize(pre + "_p.bwt") == g["survey"]["t2"]["bwt_bytes"] == 3000004
+
+
+@pytest.mark.parametrize("name", sorted(os.listdir(os.path.join(GOLD, "small"))))
+def test_oracle_matches_committed_small_goldens(oracle, tmp_path, name):
+    d = os.path.join(GOLD, "small", name)
+    prefix = int(open(os.path.join(d, "prefix.txt")).read())
+    out = str(tmp_path / "o")
+    for rle, ext in ((True, ".rl_bwt"), (False, ".bwt")):
+        assert oracle.run(os.path.join(d, "ref.fa"), os.path.join(d, "coll.fa"), out, rle=rle, prefix=prefix)[0] == 0
+        assert open(out + ext, "rb").read() == open(os.path.join(d, "expected" + ext), "rb").read()
