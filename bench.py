@@ -1,0 +1,158 @@
+"""bench.py — collection MB/s of the CMS-BWT hot path on MI355X.
+
+Workload (BASELINE.json configs[2]): one 10 MB synthetic DNA
+reference + 1000 copies mutated at 0.1 % SNP rate (10 GB of collection text),
+-r output.  The collection is generated directly in HBM by the same
+counter-based generator as tools/gen_synth (synth.h), so the timed region
+starts with inputs resident.  One step = MS walk + j-scan + the whole merge to
+packed .rl_bwt run records in HBM (cmsbwt_step); the reference index is built
+once before timing (north_star keeps libsais-equivalent SA on the host).
+
+value = collection sequence bytes / 1e6 / seconds per step, whole job.
+"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "cms-bwt_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
+
+
+def synth_reference(L: int, seed: int) -> bytes:
+    """Same bytes as synth.h: ref[k] = "ACGT"[h(seed, 0, k) >> 62]."""
+    import numpy as np
+    M = np.uint64(0xFFFFFFFFFFFFFFFF)
+
+    def mix(z):
+        z = z + np.uint64(0x9E3779B97F4A7C15)
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+    with np.errstate(over="ignore"):
+        s = mix(np.uint64(seed) + np.uint64(0xD1B54A32D192ED03) * np.uint64(1))
+        k = np.arange(L, dtype=np.uint64)
+        h = mix(s ^ k)
+    del M
+    return np.frombuffer(b"ACGT", dtype=np.uint8)[(h >> np.uint64(62)).astype(np.int64)].tobytes()
+
+
+def cpu_baseline(ref_len, copies, p, seed):
+    """Oracle (single-threaded CPU restatement) on a bounded sample of the same
+    workload, collection stage only (parse .. .rl_bwt closed)."""
+    import oracle_lib
+    gen = oracle_lib.GEN
+    with tempfile.TemporaryDirectory() as td:
+        pre = os.path.join(td, "s")
+        subprocess.run([gen, str(ref_len), str(copies), str(p), str(seed), pre], check=True)
+        rc, st, (t_idx, t_coll) = oracle_lib.run(pre + ".ref.fa", pre + ".coll.fa", pre + "_o", rle=True)
+        if rc:
+            raise RuntimeError(f"oracle rc={rc}")
+    chars = ref_len * copies
+    return {"value": round(chars / 1e6 / t_coll, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+            "sample": f"{ref_len // 10**6} MB ref + {copies} copies @{p * 100:g}% ({chars / 1e6:.0f} MB collection), "
+                      f"oracle collection stage {t_coll:.2f} s, index {t_idx:.2f} s excluded",
+            "seconds": round(t_coll, 3)}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--ref-len", type=int, default=10_000_000)
+    ap.add_argument("--copies", type=int, default=1000)
+    ap.add_argument("--p", type=float, default=0.001)
+    ap.add_argument("--seed", type=int, default=4)
+    ap.add_argument("--cpu-copies", type=int, default=10)
+    ap.add_argument("--no-cpu", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", init_method="env://")
+
+    import cmsbwt
+    eng = cmsbwt.Engine(local)
+    ref = synth_reference(args.ref_len, args.seed)
+    eng.load_reference_bytes(ref)
+    # shard the copies by contiguous ranges (documents are independent in the walk)
+    per = (args.copies + world - 1) // world
+    c0 = rank * per
+    c1 = min(args.copies, c0 + per)
+    eng.load_synth(args.seed, 1 + c0, c1 - c0, args.p, leading_empty_doc=(rank == 0))
+
+    def barrier():
+        torch.cuda.synchronize(local)
+        if dist:
+            dist.barrier()
+
+    for _ in range(args.warmup):
+        eng.step(rle=True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        eng.step(rle=True)
+    barrier()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dt = float(t.item())
+    st = eng.stats()
+    chars_total = args.ref_len * args.copies
+    ms_step = dt / args.steps * 1e3
+    value = chars_total / 1e6 / (dt / args.steps)
+
+    # Roofline of the dominant kernel: the MS walk, priced with SURVEY.md §8(d)'s
+    # per-character streams of the reference algorithm (B_MS = 22 N + 24 H) over
+    # its measured HIP-event duration (last step, on the engine's stream).
+    n_local = st.chars
+    b_ms = 22 * n_local + 24 * st.heads
+    t_ms = st.ms_walk_kernel_ms / 1e3
+    achieved = b_ms / t_ms / 1e9 if t_ms > 0 else 0.0
+    out = {
+        "metric": "collection MB/s to .rl_bwt (10 MB ref + 1000 copies @0.1% SNP)",
+        "value": round(value, 3), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
+        "scaling": "strong", "vs_baseline": None, "dtype": "u8",
+        "data": "synthetic (counter-based generator in HBM, SURVEY.md §8d)",
+        "config": {"workload": f"{args.ref_len // 10**6} MB ref + {args.copies} copies @{args.p * 100:g}% SNP, -r",
+                   "ref_len": args.ref_len, "copies": args.copies, "snp": args.p, "seed": args.seed,
+                   "collection_bytes": chars_total, "heads": st.heads, "keys": st.keys, "runs": st.runs,
+                   "parallelism": f"documents sharded over {world} GPU(s)"},
+        "roofline": {"bound": "hbm", "kernel": "k_ms_walk", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "algorithmic_bytes": b_ms, "kernel_ms": round(st.ms_walk_kernel_ms, 3),
+                     "bytes_model": "22 B/char + 24 B/head (SURVEY.md §8d)"},
+        "stages_ms": {"ms_walk": round(st.t_ms_walk_s * 1e3, 2), "merge": round(st.t_merge_s * 1e3, 2),
+                      "ms_walk_kernel": round(st.ms_walk_kernel_ms, 2),
+                      "counter_kernel": round(st.counter_kernel_ms, 2)},
+    }
+    if rank == 0 and not args.no_cpu:
+        try:
+            out["cpu_baseline"] = cpu_baseline(args.ref_len, args.cpu_copies, args.p, args.seed)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["cpu_baseline"] = {"error": str(e)}
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    eng.close()
+    if dist:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

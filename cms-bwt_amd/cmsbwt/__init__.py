@@ -56,7 +56,8 @@ class Stats(ctypes.Structure):
         "n", "sn", "ndocs", "chars", "heads", "positions", "keys", "rank", "current_sum",
         "counter_bad", "counter_good", "counter_nothing", "runs", "symbols", "order_violations")] + \
         [(k, ctypes.c_double) for k in (
-            "t_index_s", "t_upload_s", "t_ms_walk_s", "t_merge_s", "t_write_s", "ms_walk_kernel_ms")]
+            "t_index_s", "t_upload_s", "t_ms_walk_s", "t_merge_s", "t_write_s", "ms_walk_kernel_ms",
+            "counter_kernel_ms")] + [("counter_work", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -595,6 +595,8 @@ struct Engine {
                                     std::to_string(cs[3]) + " ambiguous comparisons); std::map layout would "
                                     "depend on insertion history"};
     W_work = W;
+    stats.counter_kernel_ms = counter_kernel_ms;
+    stats.counter_work = W;
 
     // ---- buckets (FN:1162-1171) and inversion (FN:1618-1628, done as a gather)
     bucket.alloc(n);

@@ -56,6 +56,8 @@ typedef struct cmsbwt_stats {
   uint64_t order_violations; /* comparator ambiguities seen (must be 0)         */
   double t_index_s, t_upload_s, t_ms_walk_s, t_merge_s, t_write_s;
   double ms_walk_kernel_ms;  /* device time of the MS-walk kernel               */
+  double counter_kernel_ms;  /* device time of the counterSmallerThanHead kernel */
+  uint64_t counter_work;     /* (item, offset) pairs visited by that kernel     */
 } cmsbwt_stats;
 
 typedef struct cmsbwt_ctx cmsbwt_ctx;
