@@ -74,6 +74,11 @@ struct DBuf {
   uint64_t bytes() const { return n * sizeof(T); }
 };
 
+static uint32_t env_u32(const char* name, uint32_t dflt) {
+  const char* v = getenv(name);
+  return v ? (uint32_t)strtoul(v, nullptr, 10) : dflt;
+}
+
 static int bits_for(uint64_t v) {  // bits to represent values in [0, v]
   int b = 1;
   while (b < 64 && (v >> b)) b++;
@@ -563,24 +568,47 @@ struct Engine {
     counter.zero(st);
     uint64_t W = 0;
     {
-      DBuf<uint64_t> wp;
-      wp.alloc((uint64_t)K + 1);
+      // work volume (statistics only): sum of untilNext
+      DBuf<uint64_t> wsum;
+      wsum.alloc(1);
       auto u64in = rocprim::make_transform_iterator(sUntil.p, WidenU64());
-      exscan(u64in, wp.p, (uint64_t)0, K);
-      uint64_t lastWp = read1(wp.p + (K - 1));
-      uint32_t lastU = read1(sUntil.p + (K - 1));
-      W = lastWp + lastU;
-      HIPCHK(hipMemcpyAsync(wp.p + K, &W, 8, hipMemcpyHostToDevice, st));
-      auto te = std::chrono::steady_clock::now();
+      size_t b = 0;
+      HIPCHK(rocprim::reduce(nullptr, b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
+      HIPCHK(rocprim::reduce(scratch(b), b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
+      W = read1(wsum.p);
+      // windows over reference positions
+      DBuf<uint32_t> wflag, wincl, winStart, crossCnt, crossOff, crossList;
+      wflag.alloc(n);
+      wincl.alloc(n);
+      const uint32_t winPos = env_u32("CMSBWT_WINPOS", 2048), slotCap = env_u32("CMSBWT_WINSLOTS", 8192);
+      mk_win_flags(posBegin.p, sSlot.p, n, std::max(1u, winPos), slotCap, wflag.p, st);
+      inscan(wflag.p, wincl.p, n, rocprim::plus<uint32_t>());
+      const uint32_t nw = read1(wincl.p + (n - 1));
+      winStart.alloc((uint64_t)nw + 1);
+      mk_win_starts(wflag.p, wincl.p, n, winStart.p, st);
+      HIPCHK(hipMemcpyAsync(winStart.p + nw, &n, 4, hipMemcpyHostToDevice, st));
+      wflag.release();
+      crossCnt.alloc((uint64_t)nw + 1);
+      crossOff.alloc((uint64_t)nw + 1);
+      crossCnt.zero(st);
+      mk_win_cross(S, K, wincl.p, n, crossCnt.p, nullptr, nullptr, cstats.p + 4, 0, st);
+      exscan(crossCnt.p, crossOff.p, 0u, (uint64_t)nw + 1);
+      const uint32_t ncross = read1(crossOff.p + nw);
+      crossList.alloc(std::max<uint32_t>(ncross, 1));
+      crossCnt.zero(st);
+      mk_win_cross(S, K, wincl.p, n, crossCnt.p, crossOff.p, crossList.p, cstats.p + 4, 1, st);
+      wincl.release();
       HIPCHK(hipEventRecord(ev0, st));
-      mk_counter(S, K, wp.p, W, hasHead.p, posBegin.p, posF.p, nhr.p, counter.p, cstats.p, n, st);
+      mk_counter_win(S, hasHead.p, posBegin.p, posF.p, nhr.p, winStart.p, nw, crossOff.p, crossList.p, counter.p,
+                     cstats.p, n, slotCap, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(ev1, st));
       sync();
       float ms = 0;
       HIPCHK(hipEventElapsedTime(&ms, ev0, ev1));
       counter_kernel_ms = ms;
-      (void)te;
+      windows = nw;
+      crossings = ncross;
     }
     unsigned long long cs[8];
     HIPCHK(hipMemcpyAsync(cs, cstats.p, sizeof(cs), hipMemcpyDeviceToHost, st));
@@ -648,6 +676,7 @@ struct Engine {
     stats.t_merge_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   float counter_kernel_ms = 0;
+  uint32_t windows = 0, crossings = 0;
   uint64_t W_work = 0;
 
   uint64_t count_positions(DBuf<uint32_t>& posBegin) {

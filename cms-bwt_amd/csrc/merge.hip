@@ -7,6 +7,8 @@
 #include "kernels.h"
 #include "merge_kernels.h"
 
+#include <algorithm>
+
 namespace cmsbwt {
 
 __global__ void k_iota(uint32_t* p, uint64_t n) {
@@ -255,22 +257,35 @@ __global__ void k_low32(const uint64_t* __restrict__ key, uint32_t* __restrict__
 }
 
 // ------------------------------------------------------------ counterSmallerThanHead
-// FN:1523-1603.  Work unit (item q, offset k < untilNext): the non-head
-// suffix k+1 positions after the item's heads is placed among the items of
-// position t = pos+1+k by std::map::lower_bound semantics.
+// FN:1523-1603.  Work unit (item q, target t = pos+1+k, k < untilNext): the
+// non-head suffixes k+1 positions after the item's heads are placed among the
+// items of position t with std::map::lower_bound semantics.
+//
+// Target-major: reference positions are cut into windows whose slots fit in
+// LDS.  A block owns one window; the items that reach into it are the items
+// starting inside it plus a precomputed crossing list.  One wave per item,
+// lanes over consecutive targets; every counter update lands in LDS, and the
+// block stores each slot of its window once (no global atomics).  Windows
+// whose slots exceed the LDS budget fall back to global u64 atomics.
+constexpr uint32_t kWinSlots = 8192;  // 64 KB of u64 counters per block
+
 struct CounterArgs {
   ItemsSoA it;
-  uint32_t K;
-  const uint64_t* wp;        // exclusive prefix of untilNext (K+1)
-  uint64_t W;
   const uint8_t* hasHead;    // bucket < 0
   const uint32_t* posBegin;
   const uint32_t* posF;
   const uint32_t* nhr;       // sorted next-head ranks, slot order
+  const uint32_t* winStart;  // nw + 1
+  const uint32_t* crossOff;  // nw + 1
+  const uint32_t* crossList;
   unsigned long long* counter;
   unsigned long long* stats; // bad, good, nothing, violations, errors
   uint32_t n;
-  uint32_t perBlock;         // work units per block
+  uint32_t slotCap;          // windows with more slots use global atomics
+};
+
+struct QueryStats {
+  unsigned long long bad = 0, good = 0, nothing = 0, viol = 0;
 };
 
 __device__ __forceinline__ uint32_t d_upper_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t v) {
@@ -281,109 +296,166 @@ __device__ __forceinline__ uint32_t d_upper_u32(const uint32_t* a, uint32_t lo, 
   return lo;
 }
 
-__global__ void __launch_bounds__(256) k_counter(CounterArgs A) {
+template <class AddFn>
+__device__ __forceinline__ void d_counter_query(const CounterArgs& A, uint32_t q, uint32_t k, uint32_t t,
+                                                QueryStats& qs, AddFn add) {
   const ItemsSoA& it = A.it;
-  uint64_t base = (uint64_t)blockIdx.x * A.perBlock;
-  uint64_t w = base + threadIdx.x;
-  uint64_t wend = min(base + A.perBlock, A.W);
-  unsigned long long bad = 0, good = 0, nothing = 0, viol = 0, errs = 0;
-  if (w < wend) {
-    // item containing w: last q with wp[q] <= w
-    uint32_t lo = 0, hi = A.K;
-    while (hi - lo > 1) {
-      uint32_t m = (lo + hi) >> 1;
-      if (A.wp[m] <= w) lo = m; else hi = m;
+  if (!A.hasHead[t]) { qs.nothing++; return; }
+  const uint32_t L = it.len[q] - 1 - k;  // uint32 wrap as FN:1532
+  const uint32_t I = it.isa[q];
+  const bool S = it.smaller[q] != 0;
+  const uint32_t b0 = A.posBegin[t], b1 = A.posBegin[t + 1], f = A.posF[t];
+  uint32_t ans;
+  if (S) {
+    // smaller=true items: (len < L) || (len == L && isa < I)
+    uint32_t l2 = b0, h2 = f;
+    while (l2 < h2) {
+      uint32_t m = (l2 + h2) >> 1;
+      uint32_t lm = it.len[m];
+      if (lm < L || (lm == L && it.isa[m] < I)) l2 = m + 1; else h2 = m;
     }
-    uint32_t q = lo;
-    for (; w < wend; w += blockDim.x) {
-      while (A.wp[q + 1] <= w) q++;
-      const uint32_t k = (uint32_t)(w - A.wp[q]);
-      const uint32_t p = it.pos[q];
-      const uint64_t t64 = (uint64_t)p + 1 + k;
-      if (t64 >= A.n) { errs++; continue; }
-      const uint32_t t = (uint32_t)t64;
-      if (!A.hasHead[t]) { nothing++; continue; }
-      const uint32_t L = it.len[q] - 1 - k;
-      const uint32_t I = it.isa[q];
-      const bool S = it.smaller[q] != 0;
-      const uint32_t b0 = A.posBegin[t], b1 = A.posBegin[t + 1], f = A.posF[t];
-      uint32_t ans;
-      if (S) {
-        // T part: (len < L) || (len == L && isa < I)
-        uint32_t l2 = b0, h2 = f;
-        while (l2 < h2) {
-          uint32_t m = (l2 + h2) >> 1;
-          uint32_t lm = it.len[m];
-          bool pr = lm < L || (lm == L && it.isa[m] < I);
-          if (pr) l2 = m + 1; else h2 = m;
-        }
-        ans = l2;
-        // violation: an F item with len == L and isa < I
-        uint32_t l3 = f, h3 = b1;
-        while (l3 < h3) {
-          uint32_t m = (l3 + h3) >> 1;
-          if (it.len[m] > L) l3 = m + 1; else h3 = m;
-        }
-        if (l3 < b1 && it.len[l3] == L && it.isa[l3] < I) viol++;
-      } else {
-        // violation: a T item with len == L and isa >= I (last T item of len L)
-        uint32_t l3 = b0, h3 = f;
-        while (l3 < h3) {
-          uint32_t m = (l3 + h3) >> 1;
-          if (it.len[m] <= L) l3 = m + 1; else h3 = m;
-        }
-        if (l3 > b0 && it.len[l3 - 1] == L && it.isa[l3 - 1] >= I) viol++;
-        // F part: (len > L) || (len == L && isa < I)
-        uint32_t l2 = f, h2 = b1;
-        while (l2 < h2) {
-          uint32_t m = (l2 + h2) >> 1;
-          uint32_t lm = it.len[m];
-          bool pr = lm > L || (lm == L && it.isa[m] < I);
-          if (pr) l2 = m + 1; else h2 = m;
-        }
-        ans = l2;
+    ans = l2;
+    // ambiguity: a smaller=false item with len == L and isa < I
+    uint32_t l3 = f, h3 = b1;
+    while (l3 < h3) {
+      uint32_t m = (l3 + h3) >> 1;
+      if (it.len[m] > L) l3 = m + 1; else h3 = m;
+    }
+    if (l3 < b1 && it.len[l3] == L && it.isa[l3] < I) qs.viol++;
+  } else {
+    // ambiguity: a smaller=true item with len == L and isa >= I
+    uint32_t l3 = b0, h3 = f;
+    while (l3 < h3) {
+      uint32_t m = (l3 + h3) >> 1;
+      if (it.len[m] <= L) l3 = m + 1; else h3 = m;
+    }
+    if (l3 > b0 && it.len[l3 - 1] == L && it.isa[l3 - 1] >= I) qs.viol++;
+    // smaller=false items: (len > L) || (len == L && isa < I)
+    uint32_t l2 = f, h2 = b1;
+    while (l2 < h2) {
+      uint32_t m = (l2 + h2) >> 1;
+      uint32_t lm = it.len[m];
+      if (lm > L || (lm == L && it.isa[m] < I)) l2 = m + 1; else h2 = m;
+    }
+    ans = l2;
+  }
+  if (ans >= b1) return;  // lower_bound == end(): FN:1535-1536
+  const uint32_t cq = it.count[q];
+  const uint32_t so = it.slot[ans];
+  if (it.len[ans] == L && it.isa[ans] == I) {  // same key: FN:1537-1589
+    const uint32_t co = it.count[ans];
+    const bool hasNext = ans + 1 < b1;
+    const uint32_t* me = A.nhr + it.slot[q];
+    const uint32_t* ot = A.nhr + so;
+    if (me[cq - 1] < ot[0]) {
+      add(so, (unsigned long long)cq);
+      qs.good++;
+    } else if (me[0] > ot[co - 1]) {
+      if (hasNext) add(so + co, (unsigned long long)cq);
+      qs.good++;
+    } else {
+      qs.bad++;
+      uint32_t rest = 0;
+      for (uint32_t a = 0; a < cq; a++) {
+        uint32_t bpos = d_upper_u32(ot, 0, co, me[a]);
+        if (bpos < co) add(so + bpos, 1ull);
+        else rest++;
       }
-      if (ans >= b1) continue;  // lower_bound == end(): FN:1535-1536
-      const uint32_t cq = it.count[q];
-      const uint32_t sa_ = it.slot[ans];
-      if (it.len[ans] == L && it.isa[ans] == I) {  // same key: FN:1537-1589
-        const uint32_t co = it.count[ans];
-        const bool hasNext = ans + 1 < b1;
-        const uint32_t* me = A.nhr + it.slot[q];
-        const uint32_t* ot = A.nhr + sa_;
-        if (me[cq - 1] < ot[0]) {
-          atomicAdd(&A.counter[sa_], (unsigned long long)cq);
-          good++;
-        } else if (me[0] > ot[co - 1]) {
-          if (hasNext) atomicAdd(&A.counter[sa_ + co], (unsigned long long)cq);
-          good++;
-        } else {
-          bad++;
-          uint32_t rest = 0;
-          for (uint32_t a = 0; a < cq; a++) {
-            uint32_t bpos = d_upper_u32(ot, 0, co, me[a]);
-            if (bpos < co) atomicAdd(&A.counter[sa_ + bpos], 1ull);
-            else rest++;
-          }
-          if (rest && hasNext) atomicAdd(&A.counter[sa_ + co], (unsigned long long)rest);
-        }
-      } else {
-        atomicAdd(&A.counter[sa_], (unsigned long long)cq);
-        good++;
-      }
+      if (rest && hasNext) add(so + co, (unsigned long long)rest);
+    }
+  } else {
+    add(so, (unsigned long long)cq);
+    qs.good++;
+  }
+}
+
+__global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
+  __shared__ unsigned long long cnt[kWinSlots];
+  __shared__ uint32_t s_next;
+  __shared__ unsigned long long red[4];
+  const ItemsSoA& it = A.it;
+  const uint32_t w = blockIdx.x;
+  const uint32_t T0 = A.winStart[w], T1 = A.winStart[w + 1];
+  const uint32_t iBeg = A.posBegin[T0], iEnd = A.posBegin[T1];
+  const uint32_t sb = it.slot[iBeg], se = it.slot[iEnd];
+  const uint32_t nslot = se - sb;
+  const bool lds = nslot <= A.slotCap;
+  if (lds)
+    for (uint32_t i = threadIdx.x; i < nslot; i += blockDim.x) cnt[i] = 0;
+  if (threadIdx.x == 0) s_next = 0;
+  if (threadIdx.x < 4) red[threadIdx.x] = 0;
+  __syncthreads();
+  const uint32_t c0 = A.crossOff[w];
+  const uint32_t nCross = A.crossOff[w + 1] - c0;
+  const uint32_t nItems = nCross + (iEnd - iBeg);
+  const uint32_t lane = threadIdx.x & 63;
+  QueryStats qs;
+  auto addLds = [&](uint32_t s, unsigned long long v) { atomicAdd(&cnt[s - sb], v); };
+  auto addGlb = [&](uint32_t s, unsigned long long v) { atomicAdd(&A.counter[s], v); };
+  while (true) {
+    uint32_t j = 0;
+    if (lane == 0) j = atomicAdd(&s_next, 1u);
+    j = __shfl(j, 0);
+    if (j >= nItems) break;
+    const uint32_t q = j < nCross ? A.crossList[c0 + j] : iBeg + (j - nCross);
+    const uint32_t p = it.pos[q], u = it.until[q];
+    if (!u) continue;
+    const uint64_t lo = max((uint64_t)p + 1, (uint64_t)T0);
+    const uint64_t hi = min((uint64_t)p + u, (uint64_t)T1 - 1);
+    for (uint64_t t0 = lo; t0 <= hi; t0 += 64) {
+      const uint64_t t = t0 + lane;
+      if (t > hi) break;
+      const uint32_t k = (uint32_t)(t - p - 1);
+      if (lds) d_counter_query(A, q, k, (uint32_t)t, qs, addLds);
+      else d_counter_query(A, q, k, (uint32_t)t, qs, addGlb);
     }
   }
-  // block reduction of the statistics
-  __shared__ unsigned long long red[5];
-  if (threadIdx.x < 5) red[threadIdx.x] = 0;
   __syncthreads();
-  if (bad) atomicAdd(&red[0], bad);
-  if (good) atomicAdd(&red[1], good);
-  if (nothing) atomicAdd(&red[2], nothing);
-  if (viol) atomicAdd(&red[3], viol);
-  if (errs) atomicAdd(&red[4], errs);
+  if (lds)
+    for (uint32_t i = threadIdx.x; i < nslot; i += blockDim.x) A.counter[sb + i] = cnt[i];
+  if (qs.bad) atomicAdd(&red[0], qs.bad);
+  if (qs.good) atomicAdd(&red[1], qs.good);
+  if (qs.nothing) atomicAdd(&red[2], qs.nothing);
+  if (qs.viol) atomicAdd(&red[3], qs.viol);
   __syncthreads();
-  if (threadIdx.x < 5 && red[threadIdx.x]) atomicAdd(&A.stats[threadIdx.x], red[threadIdx.x]);
+  if (threadIdx.x < 4 && red[threadIdx.x]) atomicAdd(&A.stats[threadIdx.x], red[threadIdx.x]);
+}
+
+// ---- window construction
+// boundary at p when the first slot of p enters a new half-window block of
+// slots, or every kWinPos positions
+__global__ void k_win_flags(const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ slot, uint32_t n,
+                            uint32_t winPos, uint32_t half, uint32_t* __restrict__ flag) {
+  uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  if (p == 0 || p % winPos == 0) { flag[p] = 1; return; }
+  uint32_t a = slot[posBegin[p - 1]] / half, b = slot[posBegin[p]] / half;
+  flag[p] = a != b ? 1u : 0u;
+}
+
+__global__ void k_win_starts(const uint32_t* __restrict__ flag, const uint32_t* __restrict__ winIncl, uint32_t n,
+                             uint32_t* __restrict__ winStart) {
+  uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  if (flag[p]) winStart[winIncl[p] - 1] = p;
+}
+
+// items crossing the start of later windows: pass 0 counts, pass 1 fills
+__global__ void k_win_cross(const ItemsSoA it, uint32_t K, const uint32_t* __restrict__ winIncl, uint32_t n,
+                            uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
+                            uint32_t* __restrict__ list, unsigned long long* __restrict__ errs, int fill) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= K) return;
+  const uint32_t p = it.pos[q], u = it.until[q];
+  if (!u) return;
+  uint64_t last = (uint64_t)p + u;
+  if (last >= n) { if (!fill) atomicAdd(errs, 1ull); last = n - 1; }
+  const uint32_t wf = winIncl[p];          // = window index of p, plus one
+  const uint32_t wl = winIncl[last] - 1;   // window of the last target
+  for (uint32_t w = wf; w <= wl; w++) {
+    uint32_t k = atomicAdd(&cnt[w], 1u);
+    if (fill) list[off[w] + k] = q;
+  }
 }
 
 // ------------------------------------------------------------ buckets (FN:1162-1171, 1618-1628)
@@ -577,13 +649,26 @@ void mk_nhr_keys(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uin
 void mk_low32(const uint64_t* key, uint32_t* out, uint64_t n, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_low32, g1(n), dim3(256), 0, st, key, out, n);
 }
-void mk_counter(const ItemsSoA& it, uint32_t K, const uint64_t* wp, uint64_t W, const uint8_t* hasHead,
-                const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
-                unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st) {
-  if (!W) return;
-  CounterArgs A{it, K, wp, W, hasHead, posBegin, posF, nhr, counter, stats, n, 256 * 16};
-  uint64_t blocks = (W + A.perBlock - 1) / A.perBlock;
-  hipLaunchKernelGGL(k_counter, dim3((unsigned)blocks), dim3(256), 0, st, A);
+void mk_win_flags(const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t winPos, uint32_t slotCap,
+                  uint32_t* flag, hipStream_t st) {
+  hipLaunchKernelGGL(k_win_flags, g1(n), dim3(256), 0, st, posBegin, slot, n, winPos, std::max(1u, slotCap / 2),
+                     flag);
+}
+void mk_win_starts(const uint32_t* flag, const uint32_t* winIncl, uint32_t n, uint32_t* winStart, hipStream_t st) {
+  hipLaunchKernelGGL(k_win_starts, g1(n), dim3(256), 0, st, flag, winIncl, n, winStart);
+}
+void mk_win_cross(const ItemsSoA& it, uint32_t K, const uint32_t* winIncl, uint32_t n, uint32_t* cnt,
+                  const uint32_t* off, uint32_t* list, unsigned long long* errs, int fill, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_win_cross, g1(K), dim3(256), 0, st, it, K, winIncl, n, cnt, off, list, errs, fill);
+}
+void mk_counter_win(const ItemsSoA& it, const uint8_t* hasHead, const uint32_t* posBegin, const uint32_t* posF,
+                    const uint32_t* nhr, const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff,
+                    const uint32_t* crossList, unsigned long long* counter, unsigned long long* stats, uint32_t n,
+                    uint32_t slotCap, hipStream_t st) {
+  if (!nw) return;
+  CounterArgs A{it, hasHead, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n,
+                std::min(slotCap, kWinSlots)};
+  hipLaunchKernelGGL(k_counter_win, dim3(nw), dim3(512), 0, st, A);
 }
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st) {
   hipLaunchKernelGGL(k_bucket, g1(n), dim3(256), 0, st, countIncl, hasHead, n, bucket);

@@ -55,9 +55,15 @@ void mk_head_ranks(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint32_
 void mk_nhr_keys(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uint32_t* headRank,
                  const uint16_t* nexthead, uint64_t* key, hipStream_t st);
 void mk_low32(const uint64_t* key, uint32_t* out, uint64_t n, hipStream_t st);
-void mk_counter(const ItemsSoA& it, uint32_t K, const uint64_t* wp, uint64_t W, const uint8_t* hasHead,
-                const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
-                unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st);
+void mk_win_flags(const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t winPos, uint32_t slotCap,
+                  uint32_t* flag, hipStream_t st);
+void mk_win_starts(const uint32_t* flag, const uint32_t* winIncl, uint32_t n, uint32_t* winStart, hipStream_t st);
+void mk_win_cross(const ItemsSoA& it, uint32_t K, const uint32_t* winIncl, uint32_t n, uint32_t* cnt,
+                  const uint32_t* off, uint32_t* list, unsigned long long* errs, int fill, hipStream_t st);
+void mk_counter_win(const ItemsSoA& it, const uint8_t* hasHead, const uint32_t* posBegin, const uint32_t* posF,
+                    const uint32_t* nhr, const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff,
+                    const uint32_t* crossList, unsigned long long* counter, unsigned long long* stats, uint32_t n,
+                    uint32_t slotCap, hipStream_t st);
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st);
 void mk_seg_count(const WriterIn& w, unsigned long long* segN, hipStream_t st);
 void mk_seg_emit(const WriterIn& w, const unsigned long long* segOff, uint8_t* sc, unsigned long long* sn,

@@ -22,21 +22,23 @@ STAGES = ["h_start", "h_pos", "h_len", "h_smaller", "h_lchar", "h_isa", "h_tonex
           "bucket", "rank2head", "head2rank", "bwtheads", "counters"]
 
 
-def _compare(engine, oracle, tmp_path, case, chunk=None, rle=True):
-    import cmsbwt
+def _compare(engine, oracle, tmp_path, case, chunk=None, rle=True, env=None):
     d, rp, cp, prefix = cases.materialise(tmp_path, case)
     dump = os.path.join(d, "dump")
     rc, ost, _ = oracle.run(rp, cp, os.path.join(d, "oracle"), rle=rle, prefix=prefix, dump_dir=dump)
     assert rc == 0
+    env = dict(env or {})
     if chunk:
-        os.environ["CMSBWT_CHUNK"] = str(chunk)
+        env["CMSBWT_CHUNK"] = str(chunk)
+    os.environ.update(env)
     try:
         engine.initialize_reference(rp)
         engine.load_collection_file(cp, prefix)
         engine.ms_walk()
         engine.merge(rle)
     finally:
-        os.environ.pop("CMSBWT_CHUNK", None)
+        for k in env:
+            os.environ.pop(k, None)
     for s in STAGES:
         got, want = engine.array(s), oracle.load_dump(dump, s)
         assert got.shape == want.shape, f"{case[0]}: {s} shape {got.shape} vs {want.shape}"
@@ -76,6 +78,15 @@ def test_chunk_restarts(engine, oracle, tmp_path, case, chunk):
     _compare(engine, oracle, tmp_path, case, chunk=chunk)
 
 
+@pytest.mark.parametrize("geom", [{"CMSBWT_WINPOS": "7"}, {"CMSBWT_WINPOS": "64", "CMSBWT_WINSLOTS": "16"},
+                                  {"CMSBWT_WINSLOTS": "1"}], ids=["tiny_windows", "small_lds", "global_atomics"])
+@pytest.mark.parametrize("case", cases.small_cases()[:5], ids=lambda c: c[0])
+def test_counter_window_geometry(engine, oracle, tmp_path, case, geom):
+    """Tiny windows stress the crossing lists; slot caps below a position's
+    slot count force the global-atomic fallback of the counter kernel."""
+    _compare(engine, oracle, tmp_path, case, env=geom)
+
+
 @pytest.mark.parametrize("case", cases.large_cases(), ids=lambda c: c[0])
 def test_large_reference_path(engine, oracle, tmp_path, case):
     _compare(engine, oracle, tmp_path, case, rle=True)
@@ -99,3 +110,21 @@ def test_config1_golden(engine, tmp_path):
     st = engine.stats()
     assert st.heads == g["headNumber"] == 87853
     assert hashlib.sha256(engine.runs_bytes()).hexdigest() == g["rl_bwt_sha256"]
+
+
+def test_bench_workload_generated_in_hbm_matches_files(engine, oracle, tmp_path):
+    """bench.py's data path: the collection generated in HBM (synth.hip) and the
+    reference from bench.synth_reference give the same .rl_bwt as the oracle on
+    the FASTA files written by tools/gen_synth."""
+    import subprocess
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(__file__)))
+    import bench
+    L, C, p, seed = 300_000, 5, 0.002, 4
+    pre = str(tmp_path / "s")
+    subprocess.run([oracle.GEN, str(L), str(C), str(p), str(seed), pre], check=True)
+    assert oracle.run(pre + ".ref.fa", pre + ".coll.fa", pre + "_o", rle=True)[0] == 0
+    engine.load_reference_bytes(bench.synth_reference(L, seed))
+    engine.load_synth(seed, 1, C, p, leading_empty_doc=True)
+    engine.step(rle=True)
+    assert engine.runs_bytes() == open(pre + "_o.rl_bwt", "rb").read()
