@@ -19,7 +19,9 @@
 #include <algorithm>
 #include <chrono>
 #include <fstream>
+#include <map>
 #include <string>
+#include <unordered_map>
 #include <vector>
 
 #include "../../include/cmsbwt.h"
@@ -52,10 +54,62 @@ struct InputError {
   std::string msg;
 };
 
+// Caching device allocator: the step allocates the same sequence of buffers
+// every time, so blocks are kept after release and handed back on the next
+// request of a similar size (all work runs on one stream, so stream order
+// makes reuse safe).  hipMalloc/hipFree of multi-GB buffers otherwise cost
+// tens of milliseconds per step.
+struct DevAlloc {
+  std::multimap<uint64_t, void*> freeBlocks;
+  std::unordered_map<void*, uint64_t> sizes;
+  uint64_t cached = 0;
+  uint64_t limit = 96ull << 30;
+  void* get(uint64_t bytes) {
+    bytes = (std::max<uint64_t>(bytes, 64) + 255) & ~255ull;
+    auto it = freeBlocks.lower_bound(bytes);
+    if (it != freeBlocks.end() && it->first <= bytes + bytes / 4 + (4u << 20)) {
+      void* p = it->second;
+      cached -= it->first;
+      freeBlocks.erase(it);
+      return p;
+    }
+    void* p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) {
+      (void)hipGetLastError();
+      trim();
+      HIPCHK(hipMalloc(&p, bytes));
+    }
+    sizes[p] = bytes;
+    return p;
+  }
+  void put(void* p) {
+    auto s = sizes.find(p);
+    if (s == sizes.end()) { (void)hipFree(p); return; }
+    freeBlocks.emplace(s->second, p);
+    cached += s->second;
+    if (cached > limit) trim();
+  }
+  void trim() {
+    (void)hipDeviceSynchronize();
+    for (auto& kv : freeBlocks) {
+      sizes.erase(kv.second);
+      (void)hipFree(kv.second);
+    }
+    freeBlocks.clear();
+    cached = 0;
+  }
+  ~DevAlloc() {
+    trim();
+    for (auto& kv : sizes) (void)hipFree(kv.first);
+  }
+};
+static thread_local DevAlloc* g_alloc = nullptr;
+
 template <class T>
 struct DBuf {
   T* p = nullptr;
   uint64_t n = 0;
+  DevAlloc* owner = nullptr;
   DBuf() = default;
   DBuf(const DBuf&) = delete;
   DBuf& operator=(const DBuf&) = delete;
@@ -63,13 +117,20 @@ struct DBuf {
   void alloc(uint64_t k) {
     release();
     n = k;
-    if (k) HIPCHK(hipMalloc((void**)&p, std::max<uint64_t>(k * sizeof(T), 64)));
+    if (!k) return;
+    owner = g_alloc;
+    if (owner) p = (T*)owner->get(k * sizeof(T));
+    else HIPCHK(hipMalloc((void**)&p, std::max<uint64_t>(k * sizeof(T), 64)));
   }
   void zero(hipStream_t st) { if (n) HIPCHK(hipMemsetAsync(p, 0, n * sizeof(T), st)); }
   void release() {
-    if (p) (void)hipFree(p);
+    if (p) {
+      if (owner) owner->put(p);
+      else (void)hipFree(p);
+    }
     p = nullptr;
     n = 0;
+    owner = nullptr;
   }
   uint64_t bytes() const { return n * sizeof(T); }
 };
@@ -86,6 +147,7 @@ static int bits_for(uint64_t v) {  // bits to represent values in [0, v]
 }
 
 struct Engine {
+  DevAlloc alloc;  // first member: destroyed last
   int device = 0;
   hipStream_t st = nullptr;
   std::string err;
@@ -132,12 +194,14 @@ struct Engine {
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
 
   explicit Engine(int dev) : device(dev) {
+    g_alloc = &alloc;
     HIPCHK(hipSetDevice(dev));
     HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&ev0));
     HIPCHK(hipEventCreate(&ev1));
   }
   ~Engine() {
+    g_alloc = &alloc;
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (st) (void)hipStreamDestroy(st);
@@ -209,8 +273,8 @@ struct Engine {
     for (uint32_t q = 0; q + 1 < n; q++)
       if ((int64_t)hix.plcp[q + 1] + 1 < (int64_t)hix.plcp[q])
         throw InputError{CMSBWT_EINPUT, "internal: PLCP monotonicity violated"};
-    dx.alloc((uint64_t)n + 64);
-    HIPCHK(hipMemsetAsync(dx.p, 0, n + 64, st));
+    dx.alloc((uint64_t)n + 128);
+    HIPCHK(hipMemsetAsync(dx.p, 0, n + 128, st));
     HIPCHK(hipMemcpyAsync(dx.p, hix.x.data(), n, hipMemcpyHostToDevice, st));
     dsa.alloc(n);
     HIPCHK(hipMemcpyAsync(dsa.p, hix.sa.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
@@ -271,8 +335,8 @@ struct Engine {
       if (len >= (1ull << 32) - 1) throw InputError{CMSBWT_ELIMIT, "document longer than 2^32 (uint32 positions)"};
       check_bytes(c.text.data() + c.off[d], len);
     }
-    dtext.alloc(c.text.size() + 64);
-    HIPCHK(hipMemsetAsync(dtext.p + c.text.size(), kSep, 64, st));
+    dtext.alloc(c.text.size() + 128);
+    HIPCHK(hipMemsetAsync(dtext.p + c.text.size(), kSep, 128, st));
     if (!c.text.empty()) HIPCHK(hipMemcpyAsync(dtext.p, c.text.data(), c.text.size(), hipMemcpyHostToDevice, st));
     hdoc = c.off;
     ddoc.alloc(hdoc.size());
@@ -295,8 +359,8 @@ struct Engine {
         throw InputError{CMSBWT_EARG, "loaded reference is not the synthetic reference of this seed"};
     uint64_t base = leadingEmpty ? 1 : 0;
     uint64_t total = base + ncopies * (L + 1);
-    dtext.alloc(total + 64);
-    HIPCHK(hipMemsetAsync(dtext.p, kSep, total + 64, st));
+    dtext.alloc(total + 128);
+    HIPCHK(hipMemsetAsync(dtext.p, kSep, total + 128, st));
     launch_synth_collection(dtext.p, L, seed, copy_begin, ncopies, synth_threshold(p), base, st);
     HIPCHK(hipGetLastError());
     hdoc.clear();
@@ -316,7 +380,7 @@ struct Engine {
   // MS walk + head finalisation
   uint32_t chunk_size() const {
     if (const char* e = getenv("CMSBWT_CHUNK")) return (uint32_t)std::max(64L, atol(e));
-    uint64_t c = chars / (256ull * 64 * 8);
+    uint64_t c = chars / (256ull * 64 * 64);
     c = std::max<uint64_t>(2048, std::min<uint64_t>(32768, c));
     return (uint32_t)c;
   }
@@ -672,21 +736,20 @@ struct Engine {
     stats.current_sum = H;
     stats.runs = Rn;
     stats.symbols = symbols;
-    stats.positions = count_positions(posBegin);
+    stats.positions = count_positions(sPos);
     stats.t_merge_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   float counter_kernel_ms = 0;
   uint32_t windows = 0, crossings = 0;
   uint64_t W_work = 0;
 
-  uint64_t count_positions(DBuf<uint32_t>& posBegin) {
-    // phrasesSet.size(): positions holding heads (n-1 always present)
-    std::vector<uint32_t> pb(R.n + 1);
-    HIPCHK(hipMemcpyAsync(pb.data(), posBegin.p, pb.size() * 4, hipMemcpyDeviceToHost, st));
-    sync();
-    uint64_t c = 0;
-    for (uint32_t p = 0; p < R.n; p++) c += pb[p + 1] > pb[p];
-    return c;
+  uint64_t count_positions(DBuf<uint32_t>& sPos) {
+    // phrasesSet.size(): distinct positions holding items (n-1 always present)
+    DBuf<unsigned long long> c;
+    c.alloc(1);
+    c.zero(st);
+    mk_count_distinct(sPos.p, K, c.p, st);
+    return read1(c.p);
   }
 
   // =====================================================================
@@ -781,6 +844,10 @@ struct cmsbwt_ctx {
 
 template <class F>
 static int guard(cmsbwt_ctx* c, F&& f) {
+  if (c && c->e) {
+    cmsbwt::g_alloc = &c->e->alloc;
+    (void)hipSetDevice(c->e->device);
+  }
   try {
     f();
     return CMSBWT_OK;

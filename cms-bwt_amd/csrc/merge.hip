@@ -572,6 +572,13 @@ __global__ void k_run_records(const unsigned long long* __restrict__ runEnd, con
   o[8] = runChar[j];
 }
 
+__global__ void k_count_distinct(const uint32_t* __restrict__ v, uint32_t K, unsigned long long* __restrict__ out) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  bool first = q < K && (q == 0 || v[q] != v[q - 1]);
+  unsigned long long b = __ballot(first);
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(out, (unsigned long long)__popcll(b));
+}
+
 // ------------------------------------------------------------ launchers
 static inline dim3 g1(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
@@ -669,6 +676,9 @@ void mk_counter_win(const ItemsSoA& it, const uint8_t* hasHead, const uint32_t* 
   CounterArgs A{it, hasHead, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n,
                 std::min(slotCap, kWinSlots)};
   hipLaunchKernelGGL(k_counter_win, dim3(nw), dim3(512), 0, st, A);
+}
+void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_count_distinct, g1(K), dim3(256), 0, st, v, K, out);
 }
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st) {
   hipLaunchKernelGGL(k_bucket, g1(n), dim3(256), 0, st, countIncl, hasHead, n, bucket);

@@ -64,6 +64,7 @@ void mk_counter_win(const ItemsSoA& it, const uint8_t* hasHead, const uint32_t* 
                     const uint32_t* nhr, const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff,
                     const uint32_t* crossList, unsigned long long* counter, unsigned long long* stats, uint32_t n,
                     uint32_t slotCap, hipStream_t st);
+void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st);
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st);
 void mk_seg_count(const WriterIn& w, unsigned long long* segN, hipStream_t st);
 void mk_seg_emit(const WriterIn& w, const unsigned long long* segOff, uint8_t* sc, unsigned long long* sn,

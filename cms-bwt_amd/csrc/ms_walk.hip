@@ -138,18 +138,44 @@ __device__ __forceinline__ uint64_t d_load8(const uint8_t* p) {
 // Longest common extension of x[q..] and t[j..]: stops at the first mismatch,
 // which always exists (the document separator 0x02 is absent from x).
 __device__ __forceinline__ uint32_t d_lce(const uint8_t* xq, const uint8_t* tj) {
-  uint32_t k = 0;
-  while (true) {
-    uint64_t d = d_load8(xq + k) ^ d_load8(tj + k);
-    if (d) return k + (uint32_t)(__builtin_ctzll(d) >> 3);
-    k += 8;
+  uint64_t d = d_load8(xq) ^ d_load8(tj);
+  if (d) return (uint32_t)(__builtin_ctzll(d) >> 3);
+  uint32_t k = 8;
+  while (true) {  // 32 bytes per step, loads issued together
+    uint64_t d0 = d_load8(xq + k) ^ d_load8(tj + k);
+    uint64_t d1 = d_load8(xq + k + 8) ^ d_load8(tj + k + 8);
+    uint64_t d2 = d_load8(xq + k + 16) ^ d_load8(tj + k + 16);
+    uint64_t d3 = d_load8(xq + k + 24) ^ d_load8(tj + k + 24);
+    if (d0) return k + (uint32_t)(__builtin_ctzll(d0) >> 3);
+    if (d1) return k + 8 + (uint32_t)(__builtin_ctzll(d1) >> 3);
+    if (d2) return k + 16 + (uint32_t)(__builtin_ctzll(d2) >> 3);
+    if (d3) return k + 24 + (uint32_t)(__builtin_ctzll(d3) >> 3);
+    k += 32;
   }
 }
 
 // Smallest s >= 0 with len - s <= PLCP[base + s]  (FN:1176 loop exit).
+// With q = base + s the condition is PLCP[q] + q >= base + len =: T, and
+// PLCP[q] + q is non-decreasing, so the answer is the first q in [base, T]
+// crossing T.  PLCP is short outside long repeats, so the crossing almost
+// always lies in the 32 entries just below T: probe that window with
+// independent loads first, gallop from `base` only when it does not.
 __device__ __forceinline__ uint32_t d_skip(const DevRef& R, uint32_t base, uint32_t len) {
   const int32_t* P = R.plcp;
   if ((int64_t)len <= (int64_t)P[base]) return 0;
+  const int64_t T = (int64_t)base + len;
+  if (len > 32) {
+    const int64_t w0 = T - 32;  // > base
+    int32_t v[33];
+#pragma unroll
+    for (int k = 0; k < 33; k++) v[k] = P[w0 + k];
+    if ((int64_t)v[0] + w0 < T) {  // crossing inside (w0, T]
+      uint32_t c = 0;
+#pragma unroll
+      for (int k = 1; k < 33; k++) c += ((int64_t)v[k] + w0 + k < T) ? 1u : 0u;
+      return (uint32_t)(w0 + 1 + c - base);
+    }
+  }
   uint32_t lo = 0, hi, step = 1;
   while (true) {
     uint64_t t = (uint64_t)lo + step;

@@ -128,3 +128,17 @@ def test_bench_workload_generated_in_hbm_matches_files(engine, oracle, tmp_path)
     engine.load_synth(seed, 1, C, p, leading_empty_doc=True)
     engine.step(rle=True)
     assert engine.runs_bytes() == open(pre + "_o.rl_bwt", "rb").read()
+
+
+def test_repeated_steps_identical(engine, tmp_path):
+    """The caching allocator reuses buffers across steps: three steps on the
+    same inputs must give identical runs (and match across rle/plain reruns)."""
+    case = cases.small_cases()[1]
+    d, rp, cp, prefix = cases.materialise(tmp_path, case)
+    engine.initialize_reference(rp)
+    engine.load_collection_file(cp, prefix)
+    outs = []
+    for rle in (True, False, True, True):
+        engine.step(rle=rle)
+        outs.append(engine.runs_bytes())
+    assert outs[0] == outs[2] == outs[3]
