@@ -142,3 +142,25 @@ def test_repeated_steps_identical(engine, tmp_path):
         engine.step(rle=rle)
         outs.append(engine.runs_bytes())
     assert outs[0] == outs[2] == outs[3]
+
+
+def test_config2_full_size_golden(engine, tmp_path):
+    """SURVEY.md config 2 at full size (10 MB ref + 100 copies @0.1%, 1 GB,
+    numpy generator seed 3): headNumber equals the reference's recorded
+    10,057,656 and the .rl_bwt equals the oracle's (sha256 committed)."""
+    import hashlib
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import gen_np
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+    pre = str(tmp_path / "t3")
+    gen_np.gen(10_000_000, 100, 0.001, 3, pre)
+    engine.initialize_reference(pre + ".ref.fa")
+    engine.load_collection_file(pre + ".coll.fa")
+    engine.step(rle=True)
+    st = engine.stats()
+    assert st.heads == g["survey"]["t3"]["headNumber"] == 10057656
+    assert (st.counter_bad, st.counter_good, st.counter_nothing) == \
+        (g["t3"]["counterBad"], g["t3"]["counterGood"], g["t3"]["counterDoNothing"])
+    assert hashlib.sha256(engine.runs_bytes()).hexdigest() == g["t3"]["rl_bwt_sha256"]
