@@ -86,14 +86,20 @@ def main():
         dist.init_process_group("nccl", init_method="env://")
 
     import cmsbwt
+    import cmsbwt.dist as cdist
     eng = cmsbwt.Engine(local)
     ref = synth_reference(args.ref_len, args.seed)
     eng.load_reference_bytes(ref)
-    # shard the copies by contiguous ranges (documents are independent in the walk)
-    per = (args.copies + world - 1) // world
-    c0 = rank * per
-    c1 = min(args.copies, c0 + per)
+    # documents shard by contiguous ranges (the walk and j-scan are document-local)
+    c0, c1 = cdist.shard_range(args.copies, world, rank)
     eng.load_synth(args.seed, 1 + c0, c1 - c0, args.p, leading_empty_doc=(rank == 0))
+    device = f"cuda:{local}"
+
+    def step():
+        if world == 1:
+            eng.step(rle=True)
+        else:
+            cdist.sharded_step(eng, device, rle=True)
 
     def barrier():
         torch.cuda.synchronize(local)
@@ -101,11 +107,11 @@ def main():
             dist.barrier()
 
     for _ in range(args.warmup):
-        eng.step(rle=True)
+        step()
     barrier()
     t0 = time.perf_counter()
     for _ in range(args.steps):
-        eng.step(rle=True)
+        step()
     barrier()
     dt = time.perf_counter() - t0
     if dist:
@@ -113,6 +119,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     st = eng.stats()
+    if world > 1:  # walk statistics of rank 0's shard; merge statistics are global on rank 0
+        st_walk_chars = args.ref_len * (c1 - c0)
+    else:
+        st_walk_chars = st.chars
     chars_total = args.ref_len * args.copies
     ms_step = dt / args.steps * 1e3
     value = chars_total / 1e6 / (dt / args.steps)
@@ -120,8 +130,9 @@ def main():
     # Roofline of the dominant kernel: the MS walk, priced with SURVEY.md §8(d)'s
     # per-character streams of the reference algorithm (B_MS = 22 N + 24 H) over
     # its measured HIP-event duration (last step, on the engine's stream).
-    n_local = st.chars
-    b_ms = 22 * n_local + 24 * st.heads
+    n_local = st_walk_chars
+    heads_local = st.heads if world == 1 else int(st.heads * (c1 - c0) / max(1, args.copies))
+    b_ms = 22 * n_local + 24 * heads_local
     t_ms = st.ms_walk_kernel_ms / 1e3
     achieved = b_ms / t_ms / 1e9 if t_ms > 0 else 0.0
     out = {
@@ -133,7 +144,8 @@ def main():
         "config": {"workload": f"{args.ref_len // 10**6} MB ref + {args.copies} copies @{args.p * 100:g}% SNP, -r",
                    "ref_len": args.ref_len, "copies": args.copies, "snp": args.p, "seed": args.seed,
                    "collection_bytes": chars_total, "heads": st.heads, "keys": st.keys, "runs": st.runs,
-                   "parallelism": f"documents sharded over {world} GPU(s)"},
+                   "parallelism": (f"documents sharded over {world} GPUs, heads gathered to rank 0 over RCCL, merge on rank 0"
+                                   if world > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "kernel": "k_ms_walk", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": None, "algorithmic_bytes": b_ms, "kernel_ms": round(st.ms_walk_kernel_ms, 3),

@@ -37,7 +37,10 @@ ARRAYS = {  # name -> numpy dtype, as dumped by the oracle
     "h_start": "u4", "h_pos": "u4", "h_len": "u4", "h_smaller": "u1", "h_lchar": "u1",
     "h_isa": "u4", "h_tonext": "u4", "h_nexthead": "u2", "bucket": "i8",
     "rank2head": "i4", "head2rank": "i4", "bwtheads": "u1", "counters": "u8",
+    "diff": "i4", "hashead": "u1",
 }
+WALK_ARRAYS = ["h_start", "h_pos", "h_len", "h_smaller", "h_lchar", "h_isa", "h_tonext", "h_nexthead",
+               "diff", "hashead"]
 
 
 class CmsBwtError(RuntimeError):
@@ -100,6 +103,7 @@ def load_library() -> ctypes.CDLL:
         "cmsbwt_host_read_collection": (I32, [ctypes.c_char_p, U64, VP, U64, ctypes.POINTER(U64), VP, U64,
                                               ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "cmsbwt_host_suffix_array": (I32, [VP, U64, VP]),
+        "cmsbwt_walk_import": (I32, [P, U64, U64, U64, ctypes.POINTER(ctypes.c_void_p)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -114,7 +118,7 @@ EXPORTED = [
     "cmsbwt_load_reference_file", "cmsbwt_load_reference", "cmsbwt_load_collection_file",
     "cmsbwt_load_collection", "cmsbwt_load_collection_synth", "cmsbwt_ms_walk", "cmsbwt_merge",
     "cmsbwt_step", "cmsbwt_get_stats", "cmsbwt_num_runs", "cmsbwt_copy_runs", "cmsbwt_write_output",
-    "cmsbwt_copy_array", "cmsbwt_host_read_collection", "cmsbwt_host_suffix_array",
+    "cmsbwt_copy_array", "cmsbwt_host_read_collection", "cmsbwt_host_suffix_array", "cmsbwt_walk_import",
 ]
 
 
@@ -219,6 +223,21 @@ class Engine:
         buf = ctypes.create_string_buffer(max(1, nr * 9))
         self._chk(self._lib.cmsbwt_copy_runs(self._ctx, buf, nr * 9))
         return buf.raw[: nr * 9]
+
+    def array_size(self, name: str) -> int:
+        nb = ctypes.c_uint64()
+        self._chk(self._lib.cmsbwt_copy_array(self._ctx, name.encode(), None, ctypes.byref(nb)))
+        return nb.value // __import__("numpy").dtype(ARRAYS[name]).itemsize
+
+    def array_into(self, name: str, ptr: int):
+        """Copy a stage array into caller memory (host or device pointer)."""
+        nb = ctypes.c_uint64()
+        self._chk(self._lib.cmsbwt_copy_array(self._ctx, name.encode(), ctypes.c_void_p(ptr), ctypes.byref(nb)))
+
+    def walk_import(self, heads: int, ndocs: int, chars: int, ptrs):
+        """Install merged walk results (pointers in WALK_ARRAYS order, host or device)."""
+        arr = (ctypes.c_void_p * len(WALK_ARRAYS))(*[ctypes.c_void_p(p) for p in ptrs])
+        self._chk(self._lib.cmsbwt_walk_import(self._ctx, heads, ndocs, chars, arr))
 
     def write_output(self, outname: str, rle: bool = True):
         self._chk(self._lib.cmsbwt_write_output(self._ctx, outname.encode(), 1 if rle else 0))

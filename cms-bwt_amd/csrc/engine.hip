@@ -168,6 +168,7 @@ struct Engine {
   DBuf<uint64_t> ddoc;
   std::vector<uint64_t> hdoc;  // doc offsets (ndocs+1), doc k = [hdoc[k], hdoc[k+1]-1)
   uint64_t ndocs = 0, chars = 0, sn = 0;
+  uint64_t collChars = 0;  // chars of the loaded collection (ms_walk input)
 
   // ---- walk outputs
   bool walked = false;
@@ -343,7 +344,7 @@ struct Engine {
     HIPCHK(hipMemcpyAsync(ddoc.p, hdoc.data(), hdoc.size() * 8, hipMemcpyHostToDevice, st));
     sync();
     ndocs = c.ndocs();
-    chars = c.chars;
+    chars = collChars = c.chars;
     sn = c.sn;
     collLoaded = true;
     stats.t_upload_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
@@ -371,7 +372,7 @@ struct Engine {
     HIPCHK(hipMemcpyAsync(ddoc.p, hdoc.data(), hdoc.size() * 8, hipMemcpyHostToDevice, st));
     sync();
     ndocs = hdoc.size() - 1;
-    chars = ncopies * L;
+    chars = collChars = ncopies * L;
     sn = total;
     collLoaded = true;
   }
@@ -389,6 +390,8 @@ struct Engine {
     if (!collLoaded) throw InputError{CMSBWT_EARG, "load a collection first"};
     auto t0 = std::chrono::steady_clock::now();
     walked = merged = false;
+    ndocs = hdoc.size() - 1;  // walk_import may have replaced these with merged totals
+    chars = collChars;
     const uint32_t C = chunk_size();
     std::vector<Chunk> chunks;
     std::vector<uint32_t> lastChunk(ndocs);
@@ -803,11 +806,36 @@ struct Engine {
     stats.t_write_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
 
+  void walk_import(uint64_t heads, uint64_t nd, uint64_t nchars, const void* const* a) {
+    if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
+    if (heads >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^31-1 heads"};
+    walked = merged = false;
+    H = (uint32_t)heads;
+    hStart.alloc(H); hPos.alloc(H); hLen.alloc(H); hIsa.alloc(H); hTonext.alloc(H);
+    hSmall.alloc(H); hChar.alloc(H); hNext.alloc(H);
+    diff.alloc((uint64_t)R.n + 1);
+    hasHead.alloc(R.n);
+    auto in = [&](void* d, const void* s, uint64_t b) {
+      if (b) HIPCHK(hipMemcpyAsync(d, s, b, hipMemcpyDefault, st));
+    };
+    in(hStart.p, a[0], (uint64_t)H * 4); in(hPos.p, a[1], (uint64_t)H * 4); in(hLen.p, a[2], (uint64_t)H * 4);
+    in(hSmall.p, a[3], H); in(hChar.p, a[4], H); in(hIsa.p, a[5], (uint64_t)H * 4);
+    in(hTonext.p, a[6], (uint64_t)H * 4); in(hNext.p, a[7], (uint64_t)H * 2);
+    in(diff.p, a[8], ((uint64_t)R.n + 1) * 4); in(hasHead.p, a[9], R.n);
+    sync();
+    ndocs = nd;
+    chars = nchars;
+    collLoaded = walked = true;
+    stats.heads = H;
+    stats.ndocs = nd;
+    stats.chars = nchars;
+  }
+
   // parity copies
   uint64_t copy_array(const std::string& name, void* out) {
     auto cp = [&](const void* d, uint64_t bytes) -> uint64_t {
       if (out && bytes) {
-        HIPCHK(hipMemcpyAsync(out, d, bytes, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(out, d, bytes, hipMemcpyDefault, st));
         sync();
       }
       return bytes;
@@ -821,6 +849,8 @@ struct Engine {
     if (name == "h_isa") return cp(hIsa.p, (uint64_t)H * 4);
     if (name == "h_tonext") return cp(hTonext.p, (uint64_t)H * 4);
     if (name == "h_nexthead") return cp(hNext.p, (uint64_t)H * 2);
+    if (name == "diff") return cp(diff.p, ((uint64_t)R.n + 1) * 4);
+    if (name == "hashead") return cp(hasHead.p, R.n);
     if (!merged) throw InputError{CMSBWT_EARG, "run merge first"};
     if (name == "bucket") return cp(bucket.p, (uint64_t)R.n * 8);
     if (name == "rank2head") return cp(T.p, ((uint64_t)H + 1) * 4);
@@ -948,6 +978,11 @@ int cmsbwt_step(cmsbwt_ctx* ctx, int rle) {
     ctx->e->ms_walk();
     ctx->e->merge(rle);
   });
+}
+
+int cmsbwt_walk_import(cmsbwt_ctx* ctx, uint64_t heads, uint64_t ndocs, uint64_t chars, const void* const* arrays) {
+  if (!ctx || !arrays) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->walk_import(heads, ndocs, chars, arrays); });
 }
 
 int cmsbwt_get_stats(const cmsbwt_ctx* ctx, cmsbwt_stats* out) {

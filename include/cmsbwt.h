@@ -112,6 +112,17 @@ int cmsbwt_write_output(cmsbwt_ctx* ctx, const char* outname, int rle);
  * when out == NULL. */
 int cmsbwt_copy_array(cmsbwt_ctx* ctx, const char* name, void* out, uint64_t* bytes);
 
+/* Multi-GPU exchange (documents are sharded by contiguous ranges; the walk
+ * and j-scan are document-local, the merge is global).  A shard's walk
+ * results are copied out with cmsbwt_copy_array ("h_*", plus "diff" int32
+ * n+1 and "hashead" uint8 n; dst may be host or device memory).  The merge
+ * rank imports the concatenation of all shards in document order (heads)
+ * with the summed diff and OR-ed hashead, then calls cmsbwt_merge.
+ * arrays[] order: h_start h_pos h_len h_smaller h_lchar h_isa h_tonext
+ * h_nexthead diff hashead. */
+int cmsbwt_walk_import(cmsbwt_ctx* ctx, uint64_t heads, uint64_t ndocs, uint64_t chars,
+                       const void* const* arrays);
+
 /* Host-only helpers (no GPU needed), exposed for tests of the host logic:
  * the collection reader (FN:1138-1275) and the reference suffix array
  * (libsais call site FN:247).  For the reader, pass NULL buffers to query

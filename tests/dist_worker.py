@@ -1,0 +1,80 @@
+"""Worker processes for the multi-rank tests (spawned by tests/test_multirank.py
+and tests/test_gpu_dist.py).  Rendezvous on 127.0.0.1, gloo backend."""
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "cms-bwt_amd"))
+sys.path.insert(0, os.path.join(ROOT, "tests"))
+
+
+def _init(rank, world, port):
+    import torch.distributed as dist
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    return dist
+
+
+def cpu_gather(rank, world, port, work):
+    """Each rank loads its shard's oracle dumps as walk results; rank 0 checks
+    the gathered arrays against the global oracle dumps."""
+    import torch
+    import cmsbwt.dist as cdist
+    import oracle_lib
+    from cmsbwt import ARRAYS
+    dist = _init(rank, world, port)
+    cfg = json.load(open(os.path.join(work, "cfg.json")))
+    sd = os.path.join(work, f"shard{rank}")
+    local = {}
+    for name in cdist.HEAD_ARRAYS:
+        a = oracle_lib.load_dump(sd, name)
+        local[name] = torch.from_numpy(a.view(np.dtype(ARRAYS[name]).newbyteorder("=")).copy()).view(
+            cdist._WIRE[ARRAYS[name]])
+    b = oracle_lib.load_dump(sd, "bucket")
+    count = np.abs(b).astype(np.int64)
+    diff = np.diff(np.concatenate([[0], count, [0]])).astype(np.int32)
+    local["diff"] = torch.from_numpy(diff)
+    local["hashead"] = torch.from_numpy((b < 0).astype(np.uint8))
+    meta = (len(local["h_pos"]), cfg["ndocs"][rank], cfg["chars"][rank])
+    combined, totals = cdist.gather_walk(local, meta, "cpu")
+    if rank == 0:
+        gd = os.path.join(work, "global")
+        for name in cdist.HEAD_ARRAYS:
+            want = oracle_lib.load_dump(gd, name)
+            got = combined[name].numpy().view(ARRAYS[name])
+            assert np.array_equal(got, want), name
+        gb = oracle_lib.load_dump(gd, "bucket")
+        cnt = np.cumsum(combined["diff"].numpy().astype(np.int64))[:-1]
+        assert np.array_equal(np.where(combined["hashead"].numpy() > 0, -cnt, cnt), gb)
+        assert totals == (len(gb) and sum(len(oracle_lib.load_dump(os.path.join(work, f"shard{r}"), "h_pos"))
+                                          for r in range(world)), sum(cfg["ndocs"]), sum(cfg["chars"]))
+        open(os.path.join(work, "ok"), "w").write("ok")
+    dist.destroy_process_group()
+
+
+def gpu_sharded(rank, world, port, work):
+    """Two ranks on one GPU: shard the documents, gather over gloo (host
+    tensors), merge on rank 0; rank 0 writes its runs for comparison."""
+    import cmsbwt
+    import cmsbwt.dist as cdist
+    dist = _init(rank, world, port)
+    cfg = json.load(open(os.path.join(work, "cfg.json")))
+    eng = cmsbwt.Engine(0)
+    eng.initialize_reference(cfg["ref"])
+    docs = cfg["docs"]
+    b, e = cdist.shard_range(len(docs), world, rank)
+    eng.load_collection([bytes.fromhex(d) for d in docs[b:e]])
+    for _ in range(2):  # twice: the second step reuses imported state correctly
+        cdist.sharded_step(eng, "cpu", rle=True)
+    if rank == 0:
+        open(os.path.join(work, "runs.bin"), "wb").write(eng.runs_bytes())
+    eng.close()
+    dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    fn, rank, world, port, work = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
+    globals()[fn](rank, world, port, work)
