@@ -60,7 +60,7 @@ class Stats(ctypes.Structure):
         "counter_bad", "counter_good", "counter_nothing", "runs", "symbols", "order_violations")] + \
         [(k, ctypes.c_double) for k in (
             "t_index_s", "t_upload_s", "t_ms_walk_s", "t_merge_s", "t_write_s", "ms_walk_kernel_ms",
-            "counter_kernel_ms")] + [("counter_work", ctypes.c_uint64)]
+            "counter_kernel_ms")] + [("counter_work", ctypes.c_uint64), ("order_invariant", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -103,7 +103,7 @@ def load_library() -> ctypes.CDLL:
         "cmsbwt_host_read_collection": (I32, [ctypes.c_char_p, U64, VP, U64, ctypes.POINTER(U64), VP, U64,
                                               ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "cmsbwt_host_suffix_array": (I32, [VP, U64, VP]),
-        "cmsbwt_walk_import": (I32, [P, U64, U64, U64, ctypes.POINTER(ctypes.c_void_p)]),
+        "cmsbwt_walk_import": (I32, [P, U64, U64, U64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -234,10 +234,10 @@ class Engine:
         nb = ctypes.c_uint64()
         self._chk(self._lib.cmsbwt_copy_array(self._ctx, name.encode(), ctypes.c_void_p(ptr), ctypes.byref(nb)))
 
-    def walk_import(self, heads: int, ndocs: int, chars: int, ptrs):
+    def walk_import(self, heads: int, ndocs: int, chars: int, ptrs, order_invariant: bool = False):
         """Install merged walk results (pointers in WALK_ARRAYS order, host or device)."""
         arr = (ctypes.c_void_p * len(WALK_ARRAYS))(*[ctypes.c_void_p(p) for p in ptrs])
-        self._chk(self._lib.cmsbwt_walk_import(self._ctx, heads, ndocs, chars, arr))
+        self._chk(self._lib.cmsbwt_walk_import(self._ctx, heads, ndocs, chars, 1 if order_invariant else 0, arr))
 
     def write_output(self, outname: str, rle: bool = True):
         self._chk(self._lib.cmsbwt_write_output(self._ctx, outname.encode(), 1 if rle else 0))

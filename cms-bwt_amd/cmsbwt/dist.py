@@ -48,11 +48,13 @@ def gather_walk(local: dict, meta, device, root: int = 0):
     meta: (heads, ndocs, chars) of this rank.  Returns (combined dict, totals)
     on root, (None, totals) elsewhere."""
     world, rank = dist.get_world_size(), dist.get_rank()
+    meta = tuple(meta) + (1,) * (4 - len(meta))  # (heads, ndocs, chars, order_invariant)
     m = torch.tensor(list(meta), dtype=torch.int64, device=device)
     allm = [torch.zeros_like(m) for _ in range(world)]
     dist.all_gather(allm, m)
     sizes = [int(x[0]) for x in allm]
-    totals = (sum(sizes), sum(int(x[1]) for x in allm), sum(int(x[2]) for x in allm))
+    totals = (sum(sizes), sum(int(x[1]) for x in allm), sum(int(x[2]) for x in allm),
+              int(all(int(x[3]) for x in allm)))
     # per-position arrays: reduce to root
     diff = local["diff"].clone()
     hh = local["hashead"].clone()
@@ -83,7 +85,7 @@ def gather_walk(local: dict, meta, device, root: int = 0):
 def import_walk(eng, combined: dict, totals):
     """Install gathered walk results into the merge rank's engine."""
     ptrs = [combined[name].data_ptr() for name in WALK_ARRAYS]
-    eng.walk_import(totals[0], totals[1], totals[2], ptrs)
+    eng.walk_import(totals[0], totals[1], totals[2], ptrs, order_invariant=bool(totals[3]))
 
 
 def sharded_step(eng, device, rle: bool = True, root: int = 0):
@@ -91,7 +93,7 @@ def sharded_step(eng, device, rle: bool = True, root: int = 0):
     eng.ms_walk()
     st = eng.stats()
     local = export_walk(eng, device)
-    combined, totals = gather_walk(local, (st.heads, st.ndocs, st.chars), device, root)
+    combined, totals = gather_walk(local, (st.heads, st.ndocs, st.chars, st.order_invariant), device, root)
     if dist.get_rank() == root:
         import_walk(eng, combined, totals)
         eng.merge(rle)

@@ -470,12 +470,14 @@ struct Engine {
     DBuf<uint32_t> errf;
     errf.alloc(1);
     errf.zero(st);
-    launch_finalize(R, h, H, docEnd.p, (uint32_t)ndocs, diff.p, hasHead.p, errf.p, st);
+    launch_finalize(R, h, H, docEnd.p, (uint32_t)ndocs, dtext.p, ddoc.p, diff.p, hasHead.p, errf.p, st);
     HIPCHK(hipGetLastError());
     uint32_t ef = read1(errf.p);
+    orderInvariant = (ef & 8u) == 0;
     if (ef & 1) throw InputError{CMSBWT_EINPUT, "internal: match ends not monotone inside a document"};
     if (ef & 6) throw InputError{CMSBWT_EINPUT, "isaNext/run index outside the reference (reference UB)"};
     walked = true;
+    stats.order_invariant = orderInvariant ? 1 : 0;
     stats.heads = H;
     stats.ndocs = ndocs;
     stats.chars = chars;
@@ -517,7 +519,7 @@ struct Engine {
     DBuf<uint8_t> aSmall;
     aPos.alloc(K); aLen.alloc(K); aIsa.alloc(K); aUntil.alloc(K); aCount.alloc(K); aFirst.alloc(K);
     aSmall.alloc(K);
-    ItemsSoA A0{aPos.p, aLen.p, aIsa.p, aSmall.p, aUntil.p, aCount.p, aFirst.p, nullptr, nullptr};
+    ItemsSoA A0{aPos.p, aLen.p, aIsa.p, aSmall.p, aUntil.p, aCount.p, aFirst.p, nullptr, nullptr, nullptr};
     mk_item_fill(P.p, key.p, key2.p, h, H, A0, st);
     mk_item_count(aFirst.p, aCount.p, K, H, st);
     key.release();
@@ -533,10 +535,12 @@ struct Engine {
     ik.release(); ik2.release(); io2.release();
     DBuf<uint32_t> sPos, sLen, sIsa, sUntil, sCount, sFirst, sSlot;
     DBuf<uint8_t> sSmall;
+    DBuf<unsigned long long> sKey;
     sPos.alloc(K); sLen.alloc(K); sIsa.alloc(K); sUntil.alloc(K); sCount.alloc(K); sFirst.alloc(K);
-    sSlot.alloc((uint64_t)K + 1); sSmall.alloc(K);
-    ItemsSoA S{sPos.p, sLen.p, sIsa.p, sSmall.p, sUntil.p, sCount.p, sFirst.p, sSlot.p, nullptr};
+    sSlot.alloc((uint64_t)K + 1); sSmall.alloc(K); sKey.alloc(K);
+    ItemsSoA S{sPos.p, sLen.p, sIsa.p, sSmall.p, sUntil.p, sCount.p, sFirst.p, sSlot.p, nullptr, sKey.p};
     mk_item_permute(A0, io.p, S, K, st);
+    mk_item_sk(S, K, st);
     io.release();
     aPos.release(); aLen.release(); aIsa.release(); aUntil.release(); aCount.release(); aFirst.release();
     aSmall.release();
@@ -554,7 +558,7 @@ struct Engine {
     DBuf<unsigned long long> cstats;
     cstats.alloc(8);
     cstats.zero(st);
-    mk_check_items(S, posBegin.p, posF.p, K, cstats.p + 3, st);
+    if (!orderInvariant || env_u32("CMSBWT_FORCE_CHECK", 0)) mk_check_items(S, posBegin.p, posF.p, K, cstats.p + 3, st);
 
     // ---- ranks (FN:1432-1453)
     DBuf<uint32_t> itemsSA, headsSA, itemRankBase, headBase;
@@ -655,19 +659,26 @@ struct Engine {
       mk_win_starts(wflag.p, wincl.p, n, winStart.p, st);
       HIPCHK(hipMemcpyAsync(winStart.p + nw, &n, 4, hipMemcpyHostToDevice, st));
       wflag.release();
-      crossCnt.alloc((uint64_t)nw + 1);
-      crossOff.alloc((uint64_t)nw + 1);
-      crossCnt.zero(st);
-      mk_win_cross(S, K, wincl.p, n, crossCnt.p, nullptr, nullptr, cstats.p + 4, 0, st);
-      exscan(crossCnt.p, crossOff.p, 0u, (uint64_t)nw + 1);
-      const uint32_t ncross = read1(crossOff.p + nw);
+      // crossing lists: (window, item) pairs sorted by window
+      DBuf<uint32_t> itemOff, keyW, keyW2, valQ;
+      crossCnt.alloc(K);
+      itemOff.alloc(K);
+      mk_win_cross(S, K, wincl.p, n, crossCnt.p, nullptr, nullptr, nullptr, cstats.p + 4, 0, st);
+      exscan(crossCnt.p, itemOff.p, 0u, K);
+      const uint32_t ncross = read1(itemOff.p + (K - 1)) + read1(crossCnt.p + (K - 1));
+      keyW.alloc(std::max<uint32_t>(ncross, 1));
+      keyW2.alloc(std::max<uint32_t>(ncross, 1));
+      valQ.alloc(std::max<uint32_t>(ncross, 1));
       crossList.alloc(std::max<uint32_t>(ncross, 1));
-      crossCnt.zero(st);
-      mk_win_cross(S, K, wincl.p, n, crossCnt.p, crossOff.p, crossList.p, cstats.p + 4, 1, st);
+      mk_win_cross(S, K, wincl.p, n, crossCnt.p, itemOff.p, keyW.p, valQ.p, cstats.p + 4, 1, st);
+      sort_pairs(keyW.p, keyW2.p, valQ.p, crossList.p, ncross, bits_for(nw));
+      crossOff.alloc((uint64_t)nw + 1);
+      mk_win_cross_off(keyW2.p, ncross, nw, crossOff.p, st);
       wincl.release();
+      const bool check = !orderInvariant || env_u32("CMSBWT_FORCE_CHECK", 0) != 0;
       HIPCHK(hipEventRecord(ev0, st));
-      mk_counter_win(S, hasHead.p, posBegin.p, posF.p, nhr.p, winStart.p, nw, crossOff.p, crossList.p, counter.p,
-                     cstats.p, n, slotCap, st);
+      mk_counter_win(S, posBegin.p, posF.p, nhr.p, winStart.p, nw, crossOff.p, crossList.p, counter.p, cstats.p, n,
+                     slotCap, check, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(ev1, st));
       sync();
@@ -744,6 +755,7 @@ struct Engine {
   }
   float counter_kernel_ms = 0;
   uint32_t windows = 0, crossings = 0;
+  bool orderInvariant = false;  // set by ms_walk (k_finalize), false for imported shards
   uint64_t W_work = 0;
 
   uint64_t count_positions(DBuf<uint32_t>& sPos) {
@@ -806,7 +818,7 @@ struct Engine {
     stats.t_write_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
 
-  void walk_import(uint64_t heads, uint64_t nd, uint64_t nchars, const void* const* a) {
+  void walk_import(uint64_t heads, uint64_t nd, uint64_t nchars, uint32_t flags, const void* const* a) {
     if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
     if (heads >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^31-1 heads"};
     walked = merged = false;
@@ -826,6 +838,7 @@ struct Engine {
     ndocs = nd;
     chars = nchars;
     collLoaded = walked = true;
+    orderInvariant = (flags & 1u) != 0;
     stats.heads = H;
     stats.ndocs = nd;
     stats.chars = nchars;
@@ -980,9 +993,10 @@ int cmsbwt_step(cmsbwt_ctx* ctx, int rle) {
   });
 }
 
-int cmsbwt_walk_import(cmsbwt_ctx* ctx, uint64_t heads, uint64_t ndocs, uint64_t chars, const void* const* arrays) {
+int cmsbwt_walk_import(cmsbwt_ctx* ctx, uint64_t heads, uint64_t ndocs, uint64_t chars, uint32_t flags,
+                       const void* const* arrays) {
   if (!ctx || !arrays) return CMSBWT_EARG;
-  return guard(ctx, [&] { ctx->e->walk_import(heads, ndocs, chars, arrays); });
+  return guard(ctx, [&] { ctx->e->walk_import(heads, ndocs, chars, flags, arrays); });
 }
 
 int cmsbwt_get_stats(const cmsbwt_ctx* ctx, cmsbwt_stats* out) {

@@ -29,7 +29,8 @@ struct ItemsSoA {
   uint32_t* count;     // heads in the item
   uint32_t* first;     // offset of its members in `perm`
   uint32_t* slot;      // exclusive prefix of count (prefixSumForPositions)
-  uint32_t* fbegin;    // per item: first F-class item of its position (class split)
+  uint32_t* fbegin;    // unused
+  unsigned long long* sk;  // per item search key: smaller ? len<<32|isa : ~len<<32|isa
 };
 
 // ms_walk.hip
@@ -41,7 +42,8 @@ void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t nd
                         const uint32_t* docLastChunk, const uint32_t* chunkCount, const uint32_t* chunkBase,
                         uint32_t n, const HeadsSoA& h, uint32_t* docEndIdx, hipStream_t st);
 void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint32_t* docEndIdx,
-                     uint32_t ndocs, int32_t* diff, uint8_t* hasHead, uint32_t* errFlags, hipStream_t st);
+                     uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, int32_t* diff, uint8_t* hasHead,
+                     uint32_t* errFlags, hipStream_t st);
 
 // synth.hip
 void launch_synth_collection(uint8_t* text, uint64_t L, uint64_t seed, uint64_t copy_begin, uint64_t ncopies,

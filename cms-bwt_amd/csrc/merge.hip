@@ -267,11 +267,16 @@ __global__ void k_low32(const uint64_t* __restrict__ key, uint32_t* __restrict__
 // lanes over consecutive targets; every counter update lands in LDS, and the
 // block stores each slot of its window once (no global atomics).  Windows
 // whose slots exceed the LDS budget fall back to global u64 atomics.
+//
+// Items of a position are in map order: smaller=true keys by (len, isa)
+// ascending, then smaller=false keys by (~len, isa) ascending, so each class
+// is sorted by one 64-bit search key sk and `item < query` is `sk < qk`
+// inside the query's class.  CHECK adds the ambiguity tests of DESIGN.md §5
+// (only needed when k_finalize's order invariant failed).
 constexpr uint32_t kWinSlots = 8192;  // 64 KB of u64 counters per block
 
 struct CounterArgs {
   ItemsSoA it;
-  const uint8_t* hasHead;    // bucket < 0
   const uint32_t* posBegin;
   const uint32_t* posF;
   const uint32_t* nhr;       // sorted next-head ranks, slot order
@@ -296,56 +301,51 @@ __device__ __forceinline__ uint32_t d_upper_u32(const uint32_t* a, uint32_t lo, 
   return lo;
 }
 
-template <class AddFn>
-__device__ __forceinline__ void d_counter_query(const CounterArgs& A, uint32_t q, uint32_t k, uint32_t t,
+__device__ __forceinline__ uint32_t d_lower_u64(const unsigned long long* a, uint32_t lo, uint32_t hi,
+                                                unsigned long long v) {
+  while (lo < hi) {
+    uint32_t m = (lo + hi) >> 1;
+    if (a[m] < v) lo = m + 1; else hi = m;
+  }
+  return lo;
+}
+
+// Query of one (item, target) pair.  ql/qi/qs/cq/slq: the item's len, isa,
+// smaller, count and slot (wave-uniform).
+template <bool CHECK, class AddFn>
+__device__ __forceinline__ void d_counter_query(const CounterArgs& A, uint32_t ql, uint32_t qi, bool S,
+                                                uint32_t cq, uint32_t slq, uint32_t k, uint32_t t,
                                                 QueryStats& qs, AddFn add) {
   const ItemsSoA& it = A.it;
-  if (!A.hasHead[t]) { qs.nothing++; return; }
-  const uint32_t L = it.len[q] - 1 - k;  // uint32 wrap as FN:1532
-  const uint32_t I = it.isa[q];
-  const bool S = it.smaller[q] != 0;
-  const uint32_t b0 = A.posBegin[t], b1 = A.posBegin[t + 1], f = A.posF[t];
+  const uint32_t b0 = A.posBegin[t], b1 = A.posBegin[t + 1];
+  if (b0 == b1) { qs.nothing++; return; }  // bucket >= 0: no heads at t (FN:1530)
+  const uint32_t f = A.posF[t];
+  const uint32_t L = ql - 1 - k;  // uint32 wrap as FN:1532
+  const unsigned long long kT = ((unsigned long long)L << 32) | qi;
+  const unsigned long long kF = ((unsigned long long)(~L) << 32) | qi;
   uint32_t ans;
   if (S) {
-    // smaller=true items: (len < L) || (len == L && isa < I)
-    uint32_t l2 = b0, h2 = f;
-    while (l2 < h2) {
-      uint32_t m = (l2 + h2) >> 1;
-      uint32_t lm = it.len[m];
-      if (lm < L || (lm == L && it.isa[m] < I)) l2 = m + 1; else h2 = m;
+    ans = d_lower_u64(it.sk, b0, f, kT);
+    if (CHECK) {  // an F item with len == L and isa < I breaks monotonicity
+      uint32_t l3 = d_lower_u64(it.sk, f, b1, ((unsigned long long)(~L) << 32));
+      if (l3 < b1 && it.len[l3] == L && it.isa[l3] < qi) qs.viol++;
     }
-    ans = l2;
-    // ambiguity: a smaller=false item with len == L and isa < I
-    uint32_t l3 = f, h3 = b1;
-    while (l3 < h3) {
-      uint32_t m = (l3 + h3) >> 1;
-      if (it.len[m] > L) l3 = m + 1; else h3 = m;
-    }
-    if (l3 < b1 && it.len[l3] == L && it.isa[l3] < I) qs.viol++;
   } else {
-    // ambiguity: a smaller=true item with len == L and isa >= I
-    uint32_t l3 = b0, h3 = f;
-    while (l3 < h3) {
-      uint32_t m = (l3 + h3) >> 1;
-      if (it.len[m] <= L) l3 = m + 1; else h3 = m;
+    if (CHECK) {  // a T item with len == L and isa >= I breaks monotonicity
+      uint32_t l3 = d_lower_u64(it.sk, b0, f, ((unsigned long long)(L + 1ull) << 32));
+      if ((unsigned long long)L + 1 > 0xffffffffull) l3 = f;
+      if (l3 > b0 && it.len[l3 - 1] == L && it.isa[l3 - 1] >= qi) qs.viol++;
     }
-    if (l3 > b0 && it.len[l3 - 1] == L && it.isa[l3 - 1] >= I) qs.viol++;
-    // smaller=false items: (len > L) || (len == L && isa < I)
-    uint32_t l2 = f, h2 = b1;
-    while (l2 < h2) {
-      uint32_t m = (l2 + h2) >> 1;
-      uint32_t lm = it.len[m];
-      if (lm > L || (lm == L && it.isa[m] < I)) l2 = m + 1; else h2 = m;
-    }
-    ans = l2;
+    ans = d_lower_u64(it.sk, f, b1, kF);
   }
   if (ans >= b1) return;  // lower_bound == end(): FN:1535-1536
-  const uint32_t cq = it.count[q];
+  const unsigned long long ka = it.sk[ans];
+  const bool eq = ka == (ans < f ? kT : kF);  // MatchInSet::operator== (len, isaNext)
   const uint32_t so = it.slot[ans];
-  if (it.len[ans] == L && it.isa[ans] == I) {  // same key: FN:1537-1589
+  if (eq) {  // same key: FN:1537-1589
     const uint32_t co = it.count[ans];
     const bool hasNext = ans + 1 < b1;
-    const uint32_t* me = A.nhr + it.slot[q];
+    const uint32_t* me = A.nhr + slq;
     const uint32_t* ot = A.nhr + so;
     if (me[cq - 1] < ot[0]) {
       add(so, (unsigned long long)cq);
@@ -369,6 +369,7 @@ __device__ __forceinline__ void d_counter_query(const CounterArgs& A, uint32_t q
   }
 }
 
+template <bool CHECK>
 __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
   __shared__ unsigned long long cnt[kWinSlots];
   __shared__ uint32_t s_next;
@@ -395,19 +396,21 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
   while (true) {
     uint32_t j = 0;
     if (lane == 0) j = atomicAdd(&s_next, 1u);
-    j = __shfl(j, 0);
+    j = __builtin_amdgcn_readfirstlane(__shfl(j, 0));
     if (j >= nItems) break;
-    const uint32_t q = j < nCross ? A.crossList[c0 + j] : iBeg + (j - nCross);
+    const uint32_t q = __builtin_amdgcn_readfirstlane(j < nCross ? A.crossList[c0 + j] : iBeg + (j - nCross));
     const uint32_t p = it.pos[q], u = it.until[q];
     if (!u) continue;
+    const uint32_t ql = it.len[q], qi = it.isa[q], cq = it.count[q], slq = it.slot[q];
+    const bool S = it.smaller[q] != 0;
     const uint64_t lo = max((uint64_t)p + 1, (uint64_t)T0);
     const uint64_t hi = min((uint64_t)p + u, (uint64_t)T1 - 1);
     for (uint64_t t0 = lo; t0 <= hi; t0 += 64) {
       const uint64_t t = t0 + lane;
       if (t > hi) break;
       const uint32_t k = (uint32_t)(t - p - 1);
-      if (lds) d_counter_query(A, q, k, (uint32_t)t, qs, addLds);
-      else d_counter_query(A, q, k, (uint32_t)t, qs, addGlb);
+      if (lds) d_counter_query<CHECK>(A, ql, qi, S, cq, slq, k, (uint32_t)t, qs, addLds);
+      else d_counter_query<CHECK>(A, ql, qi, S, cq, slq, k, (uint32_t)t, qs, addGlb);
     }
   }
   __syncthreads();
@@ -421,9 +424,16 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
   if (threadIdx.x < 4 && red[threadIdx.x]) atomicAdd(&A.stats[threadIdx.x], red[threadIdx.x]);
 }
 
+__global__ void k_item_sk(ItemsSoA it, uint32_t K) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= K) return;
+  const uint32_t L = it.len[q];
+  it.sk[q] = ((unsigned long long)(it.smaller[q] ? L : ~L) << 32) | it.isa[q];
+}
+
 // ---- window construction
 // boundary at p when the first slot of p enters a new half-window block of
-// slots, or every kWinPos positions
+// slots, or every winPos positions
 __global__ void k_win_flags(const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ slot, uint32_t n,
                             uint32_t winPos, uint32_t half, uint32_t* __restrict__ flag) {
   uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -440,22 +450,39 @@ __global__ void k_win_starts(const uint32_t* __restrict__ flag, const uint32_t* 
   if (flag[p]) winStart[winIncl[p] - 1] = p;
 }
 
-// items crossing the start of later windows: pass 0 counts, pass 1 fills
+// Items crossing the start of later windows, as (window, item) pairs: pass 0
+// counts per item, pass 1 writes at the item's exclusive offset; the pairs are
+// then radix-sorted by window (no contended atomics).
 __global__ void k_win_cross(const ItemsSoA it, uint32_t K, const uint32_t* __restrict__ winIncl, uint32_t n,
                             uint32_t* __restrict__ cnt, const uint32_t* __restrict__ off,
-                            uint32_t* __restrict__ list, unsigned long long* __restrict__ errs, int fill) {
+                            uint32_t* __restrict__ keyW, uint32_t* __restrict__ valQ,
+                            unsigned long long* __restrict__ errs, int fill) {
   uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= K) return;
   const uint32_t p = it.pos[q], u = it.until[q];
-  if (!u) return;
-  uint64_t last = (uint64_t)p + u;
-  if (last >= n) { if (!fill) atomicAdd(errs, 1ull); last = n - 1; }
-  const uint32_t wf = winIncl[p];          // = window index of p, plus one
-  const uint32_t wl = winIncl[last] - 1;   // window of the last target
-  for (uint32_t w = wf; w <= wl; w++) {
-    uint32_t k = atomicAdd(&cnt[w], 1u);
-    if (fill) list[off[w] + k] = q;
+  uint32_t c = 0, wf = 0;
+  if (u) {
+    uint64_t last = (uint64_t)p + u;
+    if (last >= n) { if (!fill) atomicAdd(errs, 1ull); last = n - 1; }
+    wf = winIncl[p];                         // = window index of p, plus one
+    const uint32_t wl = winIncl[last] - 1;   // window of the last target
+    c = wl >= wf ? wl - wf + 1 : 0;
   }
+  if (!fill) { cnt[q] = c; return; }
+  const uint32_t o = off[q];
+  for (uint32_t k = 0; k < c; k++) { keyW[o + k] = wf + k; valQ[o + k] = q; }
+}
+
+__global__ void k_win_cross_off(const uint32_t* __restrict__ keyW, uint32_t ncross, uint32_t nw,
+                                uint32_t* __restrict__ crossOff) {
+  uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w > nw) return;
+  uint32_t lo = 0, hi = ncross;
+  while (lo < hi) {
+    uint32_t m = (lo + hi) >> 1;
+    if (keyW[m] < w) lo = m + 1; else hi = m;
+  }
+  crossOff[w] = lo;
 }
 
 // ------------------------------------------------------------ buckets (FN:1162-1171, 1618-1628)
@@ -573,10 +600,15 @@ __global__ void k_run_records(const unsigned long long* __restrict__ runEnd, con
 }
 
 __global__ void k_count_distinct(const uint32_t* __restrict__ v, uint32_t K, unsigned long long* __restrict__ out) {
+  __shared__ unsigned int acc;
+  if (threadIdx.x == 0) acc = 0;
+  __syncthreads();
   uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   bool first = q < K && (q == 0 || v[q] != v[q - 1]);
   unsigned long long b = __ballot(first);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(out, (unsigned long long)__popcll(b));
+  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&acc, (unsigned int)__popcll(b));
+  __syncthreads();
+  if (threadIdx.x == 0 && acc) atomicAdd(out, (unsigned long long)acc);
 }
 
 // ------------------------------------------------------------ launchers
@@ -665,17 +697,26 @@ void mk_win_starts(const uint32_t* flag, const uint32_t* winIncl, uint32_t n, ui
   hipLaunchKernelGGL(k_win_starts, g1(n), dim3(256), 0, st, flag, winIncl, n, winStart);
 }
 void mk_win_cross(const ItemsSoA& it, uint32_t K, const uint32_t* winIncl, uint32_t n, uint32_t* cnt,
-                  const uint32_t* off, uint32_t* list, unsigned long long* errs, int fill, hipStream_t st) {
-  if (K) hipLaunchKernelGGL(k_win_cross, g1(K), dim3(256), 0, st, it, K, winIncl, n, cnt, off, list, errs, fill);
+                  const uint32_t* off, uint32_t* keyW, uint32_t* valQ, unsigned long long* errs, int fill,
+                  hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_win_cross, g1(K), dim3(256), 0, st, it, K, winIncl, n, cnt, off, keyW, valQ, errs,
+                            fill);
 }
-void mk_counter_win(const ItemsSoA& it, const uint8_t* hasHead, const uint32_t* posBegin, const uint32_t* posF,
-                    const uint32_t* nhr, const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff,
-                    const uint32_t* crossList, unsigned long long* counter, unsigned long long* stats, uint32_t n,
-                    uint32_t slotCap, hipStream_t st) {
+void mk_win_cross_off(const uint32_t* keyW, uint32_t ncross, uint32_t nw, uint32_t* crossOff, hipStream_t st) {
+  hipLaunchKernelGGL(k_win_cross_off, g1((uint64_t)nw + 1), dim3(256), 0, st, keyW, ncross, nw, crossOff);
+}
+void mk_item_sk(const ItemsSoA& it, uint32_t K, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_item_sk, g1(K), dim3(256), 0, st, it, K);
+}
+void mk_counter_win(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
+                    const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
+                    unsigned long long* counter, unsigned long long* stats, uint32_t n, uint32_t slotCap, bool check,
+                    hipStream_t st) {
   if (!nw) return;
-  CounterArgs A{it, hasHead, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n,
+  CounterArgs A{it, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n,
                 std::min(slotCap, kWinSlots)};
-  hipLaunchKernelGGL(k_counter_win, dim3(nw), dim3(512), 0, st, A);
+  if (check) hipLaunchKernelGGL(k_counter_win<true>, dim3(nw), dim3(512), 0, st, A);
+  else hipLaunchKernelGGL(k_counter_win<false>, dim3(nw), dim3(512), 0, st, A);
 }
 void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st) {
   if (K) hipLaunchKernelGGL(k_count_distinct, g1(K), dim3(256), 0, st, v, K, out);

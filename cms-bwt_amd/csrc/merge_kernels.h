@@ -59,11 +59,14 @@ void mk_win_flags(const uint32_t* posBegin, const uint32_t* slot, uint32_t n, ui
                   uint32_t* flag, hipStream_t st);
 void mk_win_starts(const uint32_t* flag, const uint32_t* winIncl, uint32_t n, uint32_t* winStart, hipStream_t st);
 void mk_win_cross(const ItemsSoA& it, uint32_t K, const uint32_t* winIncl, uint32_t n, uint32_t* cnt,
-                  const uint32_t* off, uint32_t* list, unsigned long long* errs, int fill, hipStream_t st);
-void mk_counter_win(const ItemsSoA& it, const uint8_t* hasHead, const uint32_t* posBegin, const uint32_t* posF,
-                    const uint32_t* nhr, const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff,
-                    const uint32_t* crossList, unsigned long long* counter, unsigned long long* stats, uint32_t n,
-                    uint32_t slotCap, hipStream_t st);
+                  const uint32_t* off, uint32_t* keyW, uint32_t* valQ, unsigned long long* errs, int fill,
+                  hipStream_t st);
+void mk_win_cross_off(const uint32_t* keyW, uint32_t ncross, uint32_t nw, uint32_t* crossOff, hipStream_t st);
+void mk_item_sk(const ItemsSoA& it, uint32_t K, hipStream_t st);
+void mk_counter_win(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
+                    const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
+                    unsigned long long* counter, unsigned long long* stats, uint32_t n, uint32_t slotCap, bool check,
+                    hipStream_t st);
 void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st);
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st);
 void mk_seg_count(const WriterIn& w, unsigned long long* segN, hipStream_t st);

@@ -318,7 +318,8 @@ __global__ void k_end_phrases(const uint8_t* __restrict__ text, const uint64_t* 
 // nextHead (uint16, FN:1128/1379), and the run (pos, start_{i+1}-start_i) that
 // replaces the per-position bucket increments.
 __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __restrict__ docEndIdx,
-                           uint32_t ndocs, int32_t* __restrict__ diff, uint8_t* __restrict__ hasHead,
+                           uint32_t ndocs, const uint8_t* __restrict__ text, const uint64_t* __restrict__ docOff,
+                           int32_t* __restrict__ diff, uint8_t* __restrict__ hasHead,
                            uint32_t* __restrict__ errFlags) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= H) return;
@@ -361,6 +362,14 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
   uint32_t q = h.pos[j] + (ei - h.start[j]);
   if (q >= R.n) { atomicOr(errFlags, 2u); q = R.n - 1; }
   h.isa[i] = R.isa[q];
+  // Order invariant: the isaNext suffix starts with the mismatching text byte
+  // (or the head ends at the document separator and isaNext is the smallest
+  // suffix).  When it holds for every head, MatchInSet::operator< is a strict
+  // weak order on every position's keys and queries.
+  {
+    const uint8_t c = text[docOff[lo] + ei];
+    if (!(c == R.x[q] || (c == kSep && q == R.n - 1))) atomicOr(errFlags, 8u);
+  }
   h.nexthead[i] = (uint16_t)(j - i);
   const uint32_t p = h.pos[i];
   const uint64_t endp = (uint64_t)p + (s1 - si);
@@ -395,10 +404,11 @@ void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t nd
 }
 
 void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint32_t* docEndIdx,
-                     uint32_t ndocs, int32_t* diff, uint8_t* hasHead, uint32_t* errFlags, hipStream_t st) {
+                     uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, int32_t* diff, uint8_t* hasHead,
+                     uint32_t* errFlags, hipStream_t st) {
   if (!H) return;
-  hipLaunchKernelGGL(k_finalize, dim3((H + 255) / 256), dim3(256), 0, st, R, h, H, docEndIdx, ndocs, diff,
-                     hasHead, errFlags);
+  hipLaunchKernelGGL(k_finalize, dim3((H + 255) / 256), dim3(256), 0, st, R, h, H, docEndIdx, ndocs, text, docOff,
+                     diff, hasHead, errFlags);
 }
 
 }  // namespace cmsbwt

@@ -58,6 +58,8 @@ typedef struct cmsbwt_stats {
   double ms_walk_kernel_ms;  /* device time of the MS-walk kernel               */
   double counter_kernel_ms;  /* device time of the counterSmallerThanHead kernel */
   uint64_t counter_work;     /* (item, offset) pairs visited by that kernel     */
+  uint64_t order_invariant;  /* 1: every isaNext suffix starts with its head's   */
+                             /* mismatch byte, comparator provably consistent   */
 } cmsbwt_stats;
 
 typedef struct cmsbwt_ctx cmsbwt_ctx;
@@ -119,8 +121,9 @@ int cmsbwt_copy_array(cmsbwt_ctx* ctx, const char* name, void* out, uint64_t* by
  * rank imports the concatenation of all shards in document order (heads)
  * with the summed diff and OR-ed hashead, then calls cmsbwt_merge.
  * arrays[] order: h_start h_pos h_len h_smaller h_lchar h_isa h_tonext
- * h_nexthead diff hashead. */
-int cmsbwt_walk_import(cmsbwt_ctx* ctx, uint64_t heads, uint64_t ndocs, uint64_t chars,
+ * h_nexthead diff hashead.  flags bit 0: every shard reported
+ * stats.order_invariant (lets the merge skip per-query ambiguity checks). */
+int cmsbwt_walk_import(cmsbwt_ctx* ctx, uint64_t heads, uint64_t ndocs, uint64_t chars, uint32_t flags,
                        const void* const* arrays);
 
 /* Host-only helpers (no GPU needed), exposed for tests of the host logic:

@@ -49,8 +49,8 @@ def cpu_gather(rank, world, port, work):
         gb = oracle_lib.load_dump(gd, "bucket")
         cnt = np.cumsum(combined["diff"].numpy().astype(np.int64))[:-1]
         assert np.array_equal(np.where(combined["hashead"].numpy() > 0, -cnt, cnt), gb)
-        assert totals == (len(gb) and sum(len(oracle_lib.load_dump(os.path.join(work, f"shard{r}"), "h_pos"))
-                                          for r in range(world)), sum(cfg["ndocs"]), sum(cfg["chars"]))
+        nh = sum(len(oracle_lib.load_dump(os.path.join(work, f"shard{r}"), "h_pos")) for r in range(world))
+        assert totals[:3] == (nh, sum(cfg["ndocs"]), sum(cfg["chars"]))
         open(os.path.join(work, "ok"), "w").write("ok")
     dist.destroy_process_group()
 

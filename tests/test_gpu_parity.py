@@ -79,7 +79,8 @@ def test_chunk_restarts(engine, oracle, tmp_path, case, chunk):
 
 
 @pytest.mark.parametrize("geom", [{"CMSBWT_WINPOS": "7"}, {"CMSBWT_WINPOS": "64", "CMSBWT_WINSLOTS": "16"},
-                                  {"CMSBWT_WINSLOTS": "1"}], ids=["tiny_windows", "small_lds", "global_atomics"])
+                                  {"CMSBWT_WINSLOTS": "1"}, {"CMSBWT_FORCE_CHECK": "1", "CMSBWT_WINPOS": "33"}],
+                         ids=["tiny_windows", "small_lds", "global_atomics", "checked_queries"])
 @pytest.mark.parametrize("case", cases.small_cases()[:5], ids=lambda c: c[0])
 def test_counter_window_geometry(engine, oracle, tmp_path, case, geom):
     """Tiny windows stress the crossing lists; slot caps below a position's
