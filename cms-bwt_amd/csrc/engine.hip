@@ -325,6 +325,7 @@ struct Engine {
   }
   void reset_collection() {
     collLoaded = walked = merged = false;
+    plan.valid = false;
     H = K = 0;
   }
   void upload_collection(const Collection& c) {
@@ -393,25 +394,8 @@ struct Engine {
     ndocs = hdoc.size() - 1;  // walk_import may have replaced these with merged totals
     chars = collChars;
     const uint32_t C = chunk_size();
-    std::vector<Chunk> chunks;
-    std::vector<uint32_t> lastChunk(ndocs);
-    for (uint64_t d = 0; d < ndocs; d++) {
-      uint64_t L = hdoc[d + 1] - hdoc[d] - 1;
-      uint64_t nc = std::max<uint64_t>(1, (L + C - 1) / C);
-      for (uint64_t k = 0; k < nc; k++) {
-        Chunk ch;
-        ch.doc = (uint32_t)d;
-        ch.a = (uint32_t)(k * C);
-        ch.b = (uint32_t)std::min<uint64_t>(L, (k + 1) * C);
-        ch.last = k + 1 == nc;
-        chunks.push_back(ch);
-      }
-      lastChunk[d] = (uint32_t)chunks.size() - 1;
-    }
-    const uint32_t nch = (uint32_t)chunks.size();
-    DBuf<Chunk> dch;
-    dch.alloc(nch);
-    HIPCHK(hipMemcpyAsync(dch.p, chunks.data(), nch * sizeof(Chunk), hipMemcpyHostToDevice, st));
+    if (!plan.valid || plan.C != C) build_plan(C);
+    const uint32_t nch = plan.nch;
     DBuf<uint32_t> chunkCount, used;
     chunkCount.alloc(nch);
     used.alloc(1);
@@ -428,7 +412,7 @@ struct Engine {
       used.zero(st);
       Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
       HIPCHK(hipEventRecord(ev0, st));
-      launch_ms_walk(R, dtext.p, ddoc.p, dch.p, nch, pool, chunkCount.p, st);
+      launch_ms_walk(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.laneChunk.p, pool, chunkCount.p, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(ev1, st));
       usedBlocks = read1(used.p);
@@ -439,30 +423,25 @@ struct Engine {
       cap = (uint64_t)usedBlocks + (uint64_t)nch + 1024;
     }
     // chunk bases (end phrase counted in the last chunk of each document)
-    DBuf<uint32_t> withEnd, chunkBase;
+    DBuf<unsigned long long> withEnd, chunkBase;
     withEnd.alloc(nch);
     chunkBase.alloc(nch);
+    launch_chunk_with_end(plan.dch.p, chunkCount.p, nch, withEnd.p, st);
+    exscan(withEnd.p, chunkBase.p, 0ull, nch);
     {
-      std::vector<uint32_t> cc(nch);
-      HIPCHK(hipMemcpyAsync(cc.data(), chunkCount.p, nch * 4, hipMemcpyDeviceToHost, st));
-      sync();
-      uint64_t tot = 0;
-      for (uint32_t c = 0; c < nch; c++) { cc[c] += chunks[c].last; tot += cc[c]; }
+      const unsigned long long tot = read1(chunkBase.p + (nch - 1)) + read1(withEnd.p + (nch - 1));
       if (tot >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^31-1 heads (int32 ranks, FN:1436)"};
       H = (uint32_t)tot;
-      HIPCHK(hipMemcpyAsync(withEnd.p, cc.data(), nch * 4, hipMemcpyHostToDevice, st));
     }
-    exscan(withEnd.p, chunkBase.p, 0u, nch);
     hStart.alloc(H); hPos.alloc(H); hLen.alloc(H); hIsa.alloc(H); hTonext.alloc(H);
     hSmall.alloc(H); hChar.alloc(H); hNext.alloc(H);
     HeadsSoA h = heads();
     Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
     launch_scatter_heads(pool, usedBlocks, chunkCount.p, chunkBase.p, h, st);
-    DBuf<uint32_t> dLast, docEnd;
-    dLast.alloc(ndocs);
-    HIPCHK(hipMemcpyAsync(dLast.p, lastChunk.data(), ndocs * 4, hipMemcpyHostToDevice, st));
+    DBuf<uint32_t> docEnd;
     docEnd.alloc(ndocs);
-    launch_end_phrases(dtext.p, ddoc.p, (uint32_t)ndocs, dLast.p, chunkCount.p, chunkBase.p, R.n, h, docEnd.p, st);
+    launch_end_phrases(dtext.p, ddoc.p, (uint32_t)ndocs, plan.dLast.p, chunkCount.p, chunkBase.p, R.n, h, docEnd.p,
+                       st);
     diff.alloc((uint64_t)R.n + 1);
     diff.zero(st);
     hasHead.alloc(R.n);
@@ -483,6 +462,60 @@ struct Engine {
     stats.chars = chars;
     stats.sn = sn;
     stats.t_ms_walk_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+
+  // Restart chunks of the loaded collection; rebuilt when the collection or
+  // the chunk size changes.
+  struct ChunkPlan {
+    bool valid = false;
+    uint32_t C = 0, nch = 0;
+    DBuf<Chunk> dch;
+    DBuf<uint32_t> dLast, laneChunk;
+  } plan;
+
+  void build_plan(uint32_t C) {
+    std::vector<Chunk> chunks;
+    std::vector<uint32_t> lastChunk(ndocs), firstChunk(ndocs);
+    uint32_t maxc = 0;
+    for (uint64_t d = 0; d < ndocs; d++) {
+      uint64_t L = hdoc[d + 1] - hdoc[d] - 1;
+      uint64_t nc = std::max<uint64_t>(1, (L + C - 1) / C);
+      firstChunk[d] = (uint32_t)chunks.size();
+      for (uint64_t k = 0; k < nc; k++) {
+        Chunk ch;
+        ch.doc = (uint32_t)d;
+        ch.a = (uint32_t)(k * C);
+        ch.b = (uint32_t)std::min<uint64_t>(L, (k + 1) * C);
+        ch.last = k + 1 == nc;
+        chunks.push_back(ch);
+      }
+      lastChunk[d] = (uint32_t)chunks.size() - 1;
+      maxc = std::max<uint32_t>(maxc, (uint32_t)nc);
+    }
+    const uint32_t nch = (uint32_t)chunks.size();
+    // Lane order: document-major by default.  CMSBWT_OFFSET_MAJOR=1 puts the
+    // same offset of consecutive documents in one wave (shared reference
+    // lines, but same-offset text of equal-length copies collides in memory
+    // channels; measured slower on the benchmark).
+    std::vector<uint32_t> order(nch);
+    if (!env_u32("CMSBWT_OFFSET_MAJOR", 0)) {
+      for (uint32_t c = 0; c < nch; c++) order[c] = c;
+    } else {
+      uint32_t o = 0;
+      for (uint32_t k = 0; k < maxc; k++)
+        for (uint64_t d = 0; d < ndocs; d++)
+          if (firstChunk[d] + k <= lastChunk[d]) order[o++] = firstChunk[d] + k;
+    }
+    plan.dch.alloc(nch);
+    HIPCHK(hipMemcpyAsync(plan.dch.p, chunks.data(), nch * sizeof(Chunk), hipMemcpyHostToDevice, st));
+    plan.dLast.alloc(ndocs);
+    HIPCHK(hipMemcpyAsync(plan.dLast.p, lastChunk.data(), ndocs * 4, hipMemcpyHostToDevice, st));
+    plan.laneChunk.alloc(nch);
+    HIPCHK(hipMemcpyAsync(plan.laneChunk.p, order.data(), nch * 4, hipMemcpyHostToDevice, st));
+    sync();
+    plan.C = C;
+    plan.nch = nch;
+    plan.valid = true;
   }
 
   HeadsSoA heads() {

@@ -35,12 +35,16 @@ struct ItemsSoA {
 
 // ms_walk.hip
 void launch_ms_walk(const DevRef& R, const uint8_t* text, const uint64_t* docOff, const Chunk* chunks,
-                    uint32_t nchunks, const Pool& pool, uint32_t* chunkCount, hipStream_t st);
+                    uint32_t nchunks, const uint32_t* laneChunk, const Pool& pool, uint32_t* chunkCount,
+                    hipStream_t st);
+void launch_chunk_with_end(const Chunk* chunks, const uint32_t* chunkCount, uint32_t nch, unsigned long long* out,
+                           hipStream_t st);
 void launch_scatter_heads(const Pool& pool, uint32_t blocksUsed, const uint32_t* chunkCount,
-                          const uint32_t* chunkBase, const HeadsSoA& h, hipStream_t st);
+                          const unsigned long long* chunkBase, const HeadsSoA& h, hipStream_t st);
 void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t ndocs,
-                        const uint32_t* docLastChunk, const uint32_t* chunkCount, const uint32_t* chunkBase,
-                        uint32_t n, const HeadsSoA& h, uint32_t* docEndIdx, hipStream_t st);
+                        const uint32_t* docLastChunk, const uint32_t* chunkCount,
+                        const unsigned long long* chunkBase, uint32_t n, const HeadsSoA& h, uint32_t* docEndIdx,
+                        hipStream_t st);
 void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint32_t* docEndIdx,
                      uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, int32_t* diff, uint8_t* hasHead,
                      uint32_t* errFlags, hipStream_t st);

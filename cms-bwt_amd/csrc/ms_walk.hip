@@ -158,21 +158,18 @@ __device__ __forceinline__ uint32_t d_lce(const uint8_t* xq, const uint8_t* tj) 
 // With q = base + s the condition is PLCP[q] + q >= base + len =: T, and
 // PLCP[q] + q is non-decreasing, so the answer is the first q in [base, T]
 // crossing T.  PLCP is short outside long repeats, so the crossing almost
-// always lies in the 32 entries just below T: probe that window with
+// always lies in the 16 entries just below T: probe that window with
 // independent loads first, gallop from `base` only when it does not.
 __device__ __forceinline__ uint32_t d_skip(const DevRef& R, uint32_t base, uint32_t len) {
   const int32_t* P = R.plcp;
   if ((int64_t)len <= (int64_t)P[base]) return 0;
   const int64_t T = (int64_t)base + len;
-  if (len > 32) {
-    const int64_t w0 = T - 32;  // > base
-    int32_t v[33];
-#pragma unroll
-    for (int k = 0; k < 33; k++) v[k] = P[w0 + k];
-    if ((int64_t)v[0] + w0 < T) {  // crossing inside (w0, T]
+  if (len > 16) {
+    const int64_t w0 = T - 16;  // > base
+    if ((int64_t)P[w0] + w0 < T) {  // crossing inside (w0, T]: count entries below T
       uint32_t c = 0;
 #pragma unroll
-      for (int k = 1; k < 33; k++) c += ((int64_t)v[k] + w0 + k < T) ? 1u : 0u;
+      for (int k = 1; k <= 16; k++) c += ((int64_t)P[w0 + k] + w0 + k < T) ? 1u : 0u;
       return (uint32_t)(w0 + 1 + c - base);
     }
   }
@@ -195,9 +192,11 @@ __device__ __forceinline__ uint32_t d_skip(const DevRef& R, uint32_t base, uint3
 __global__ void __launch_bounds__(256) k_ms_walk(DevRef R, const uint8_t* __restrict__ text,
                                                  const uint64_t* __restrict__ docOff,
                                                  const Chunk* __restrict__ chunks, uint32_t nchunks,
+                                                 const uint32_t* __restrict__ laneChunk,
                                                  Pool pool, uint32_t* __restrict__ chunkCount) {
-  uint32_t cid = blockIdx.x * blockDim.x + threadIdx.x;
-  if (cid >= nchunks) return;
+  const uint32_t lane_id = blockIdx.x * blockDim.x + threadIdx.x;
+  if (lane_id >= nchunks) return;
+  const uint32_t cid = laneChunk[lane_id];
   const Chunk ch = chunks[cid];
   const uint8_t* t = text + docOff[ch.doc];
   const uint32_t a = ch.a, b = ch.b;
@@ -275,15 +274,21 @@ __global__ void __launch_bounds__(256) k_ms_walk(DevRef R, const uint8_t* __rest
 }
 
 // ------------------------------------------------------------ pool -> idx order
+__global__ void k_chunk_with_end(const Chunk* __restrict__ chunks, const uint32_t* __restrict__ chunkCount,
+                                 uint32_t nch, unsigned long long* __restrict__ out) {
+  uint32_t c = blockIdx.x * blockDim.x + threadIdx.x;
+  if (c < nch) out[c] = (unsigned long long)chunkCount[c] + chunks[c].last;
+}
+
 __global__ void k_scatter_heads(Pool pool, uint32_t blocksUsed, const uint32_t* __restrict__ chunkCount,
-                                const uint32_t* __restrict__ chunkBase, HeadsSoA h) {
+                                const unsigned long long* __restrict__ chunkBase, HeadsSoA h) {
   uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t blk = slot / kPoolB;
   if (blk >= blocksUsed) return;
   uint32_t cid = pool.blkChunk[blk];
   uint32_t local = pool.blkSeq[blk] * kPoolB + (uint32_t)(slot % kPoolB);
   if (local >= chunkCount[cid]) return;
-  uint32_t idx = chunkBase[cid] + local;
+  uint32_t idx = (uint32_t)chunkBase[cid] + local;
   HeadRec r = pool.rec[slot];
   h.start[idx] = r.start;
   h.pos[idx] = r.pos;
@@ -296,12 +301,13 @@ __global__ void k_scatter_heads(Pool pool, uint32_t blocksUsed, const uint32_t* 
 // last sequence byte or 0x02 for an empty document.
 __global__ void k_end_phrases(const uint8_t* __restrict__ text, const uint64_t* __restrict__ docOff,
                               uint32_t ndocs, const uint32_t* __restrict__ docLastChunk,
-                              const uint32_t* __restrict__ chunkCount, const uint32_t* __restrict__ chunkBase,
-                              uint32_t n, HeadsSoA h, uint32_t* __restrict__ docEndIdx) {
+                              const uint32_t* __restrict__ chunkCount,
+                              const unsigned long long* __restrict__ chunkBase, uint32_t n, HeadsSoA h,
+                              uint32_t* __restrict__ docEndIdx) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= ndocs) return;
   uint32_t c = docLastChunk[d];
-  uint32_t idx = chunkBase[c] + chunkCount[c];
+  uint32_t idx = (uint32_t)chunkBase[c] + chunkCount[c];
   uint64_t len = docOff[d + 1] - docOff[d] - 1;
   h.start[idx] = (uint32_t)len;
   h.pos[idx] = n - 1;
@@ -381,14 +387,20 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
 
 // ------------------------------------------------------------ host launchers
 void launch_ms_walk(const DevRef& R, const uint8_t* text, const uint64_t* docOff, const Chunk* chunks,
-                    uint32_t nchunks, const Pool& pool, uint32_t* chunkCount, hipStream_t st) {
+                    uint32_t nchunks, const uint32_t* laneChunk, const Pool& pool, uint32_t* chunkCount,
+                    hipStream_t st) {
   if (!nchunks) return;
   hipLaunchKernelGGL(k_ms_walk, dim3((nchunks + 255) / 256), dim3(256), 0, st, R, text, docOff, chunks,
-                     nchunks, pool, chunkCount);
+                     nchunks, laneChunk, pool, chunkCount);
+}
+
+void launch_chunk_with_end(const Chunk* chunks, const uint32_t* chunkCount, uint32_t nch, unsigned long long* out,
+                           hipStream_t st) {
+  if (nch) hipLaunchKernelGGL(k_chunk_with_end, dim3((nch + 255) / 256), dim3(256), 0, st, chunks, chunkCount, nch, out);
 }
 
 void launch_scatter_heads(const Pool& pool, uint32_t blocksUsed, const uint32_t* chunkCount,
-                          const uint32_t* chunkBase, const HeadsSoA& h, hipStream_t st) {
+                          const unsigned long long* chunkBase, const HeadsSoA& h, hipStream_t st) {
   uint64_t slots = (uint64_t)blocksUsed * kPoolB;
   if (!slots) return;
   hipLaunchKernelGGL(k_scatter_heads, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, pool,
@@ -396,8 +408,9 @@ void launch_scatter_heads(const Pool& pool, uint32_t blocksUsed, const uint32_t*
 }
 
 void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t ndocs,
-                        const uint32_t* docLastChunk, const uint32_t* chunkCount, const uint32_t* chunkBase,
-                        uint32_t n, const HeadsSoA& h, uint32_t* docEndIdx, hipStream_t st) {
+                        const uint32_t* docLastChunk, const uint32_t* chunkCount,
+                        const unsigned long long* chunkBase, uint32_t n, const HeadsSoA& h, uint32_t* docEndIdx,
+                        hipStream_t st) {
   if (!ndocs) return;
   hipLaunchKernelGGL(k_end_phrases, dim3((ndocs + 255) / 256), dim3(256), 0, st, text, docOff, ndocs,
                      docLastChunk, chunkCount, chunkBase, n, h, docEndIdx);
