@@ -200,6 +200,15 @@ class Engine:
         buf = ctypes.create_string_buffer(text, max(1, len(text)))
         self._chk(self._lib.cmsbwt_load_collection(self._ctx, buf, off.ctypes.data, len(docs)))
 
+    def load_collection_array(self, text, doc_off):
+        """Documents from a contiguous uint8 numpy array and uint64 offsets
+        (doc k = text[doc_off[k]:doc_off[k+1]]), without intermediate copies."""
+        import numpy as np
+        text = np.ascontiguousarray(text, dtype=np.uint8)
+        off = np.ascontiguousarray(doc_off, dtype=np.uint64)
+        self._chk(self._lib.cmsbwt_load_collection(self._ctx, text.ctypes.data if text.size else None,
+                                                   off.ctypes.data, len(off) - 1))
+
     def load_synth(self, seed: int, copy_begin: int, ncopies: int, p: float, leading_empty_doc: bool = True):
         self._chk(self._lib.cmsbwt_load_collection_synth(self._ctx, seed, copy_begin, ncopies, p,
                                                          1 if leading_empty_doc else 0))

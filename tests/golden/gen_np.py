@@ -24,3 +24,22 @@ if __name__ == "__main__":
     L, C, p, seed, pre = int(sys.argv[1]), int(sys.argv[2]), float(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
     width = int(sys.argv[6]) if len(sys.argv) > 6 else 0
     gen(L, C, p, seed, pre, width)
+
+
+def gen_arrays(L, C, p, seed, leading_empty=True):
+    """Same draws as gen(), returned as (ref bytes, concatenated copies as a
+    uint8 array, document offsets) -- FASTA's leading '>' gives an empty first
+    document, reproduced by leading_empty."""
+    rng = np.random.default_rng(seed)
+    A = np.frombuffer(b"ACGT", dtype=np.uint8)
+    code = rng.integers(0, 4, L)
+    ref = A[code].tobytes()
+    text = np.empty(C * L, dtype=np.uint8)
+    for k in range(C):
+        c = code.copy()
+        m = rng.random(L) < p
+        c[m] = (c[m] + rng.integers(1, 4, int(m.sum()))) % 4
+        text[k * L:(k + 1) * L] = A[c]
+    off = [0] if leading_empty else []
+    off = np.array(off + [k * L for k in range(C + 1)], dtype=np.uint64)
+    return ref, text, off

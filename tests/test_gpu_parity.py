@@ -165,3 +165,28 @@ def test_config2_full_size_golden(engine, tmp_path):
     assert (st.counter_bad, st.counter_good, st.counter_nothing) == \
         (g["t3"]["counterBad"], g["t3"]["counterGood"], g["t3"]["counterDoNothing"])
     assert hashlib.sha256(engine.runs_bytes()).hexdigest() == g["t3"]["rl_bwt_sha256"]
+
+
+def test_config3_full_size_golden(engine):
+    """The headline workload at full size: 10 MB ref + 1000 copies @0.1 %
+    (10 GB, numpy generator seed 4, SURVEY App. B run t4).  headNumber, Rank
+    and run count equal the reference's recorded values; the .rl_bwt equals the
+    oracle's (sha256 committed; the oracle took 1125 s on one core)."""
+    import hashlib
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import gen_np
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+    ref, text, off = gen_np.gen_arrays(10_000_000, 1000, 0.001, 4)
+    engine.load_reference_bytes(ref)
+    engine.load_collection_array(text, off)
+    del text
+    engine.step(rle=True)
+    st = engine.stats()
+    assert st.heads == g["survey"]["t4"]["headNumber"] == 100530836
+    assert st.rank == g["survey"]["t4"]["Rank"]
+    assert st.runs == g["survey"]["t4"]["rl_runs"] == 135580980
+    assert (st.counter_bad, st.counter_good, st.counter_nothing) == \
+        (g["t4"]["counterBad"], g["t4"]["counterGood"], g["t4"]["counterDoNothing"])
+    assert hashlib.sha256(engine.runs_bytes()).hexdigest() == g["t4"]["rl_bwt_sha256"]
