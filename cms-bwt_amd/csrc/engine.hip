@@ -684,7 +684,8 @@ struct Engine {
       DBuf<uint32_t> wflag, wincl, winStart, crossCnt, crossOff, crossList;
       wflag.alloc(n);
       wincl.alloc(n);
-      const uint32_t winPos = env_u32("CMSBWT_WINPOS", 2048), slotCap = env_u32("CMSBWT_WINSLOTS", 8192);
+      const uint32_t winPos = std::min(1024u, env_u32("CMSBWT_WINPOS", 1024)),
+                     slotCap = std::min(4096u, env_u32("CMSBWT_WINSLOTS", 4096));
       mk_win_flags(posBegin.p, sSlot.p, n, std::max(1u, winPos), slotCap, wflag.p, st);
       inscan(wflag.p, wincl.p, n, rocprim::plus<uint32_t>());
       const uint32_t nw = read1(wincl.p + (n - 1));

@@ -273,7 +273,7 @@ __global__ void k_low32(const uint64_t* __restrict__ key, uint32_t* __restrict__
 // is sorted by one 64-bit search key sk and `item < query` is `sk < qk`
 // inside the query's class.  CHECK adds the ambiguity tests of DESIGN.md §5
 // (only needed when k_finalize's order invariant failed).
-constexpr uint32_t kWinSlots = 8192;  // 64 KB of u64 counters per block
+constexpr uint32_t kWinSlots = 4096;  // slot cap of an LDS window (see kWinItems)
 
 struct CounterArgs {
   ItemsSoA it;
@@ -311,67 +311,104 @@ __device__ __forceinline__ uint32_t d_lower_u64(const unsigned long long* a, uin
 }
 
 // Query of one (item, target) pair.  ql/qi/qs/cq/slq: the item's len, isa,
-// smaller, count and slot (wave-uniform).
-template <bool CHECK, class AddFn>
-__device__ __forceinline__ void d_counter_query(const CounterArgs& A, uint32_t ql, uint32_t qi, bool S,
-                                                uint32_t cq, uint32_t slq, uint32_t k, uint32_t t,
-                                                QueryStats& qs, AddFn add) {
-  const ItemsSoA& it = A.it;
-  const uint32_t b0 = A.posBegin[t], b1 = A.posBegin[t + 1];
+// smaller, count and slot (wave-uniform).  V gives the target's items and
+// positions either from LDS (staged window) or from global memory.
+template <bool CHECK, class View, class AddFn>
+__device__ __forceinline__ void d_counter_query(const View& V, uint32_t ql, uint32_t qi, bool S, uint32_t cq,
+                                                uint32_t slq, uint32_t k, uint32_t t, QueryStats& qs,
+                                                AddFn add) {
+  const uint32_t b0 = V.begin(t), b1 = V.begin(t + 1);
   if (b0 == b1) { qs.nothing++; return; }  // bucket >= 0: no heads at t (FN:1530)
-  const uint32_t f = A.posF[t];
+  const uint32_t f = V.fbeg(t);
   const uint32_t L = ql - 1 - k;  // uint32 wrap as FN:1532
   const unsigned long long kT = ((unsigned long long)L << 32) | qi;
   const unsigned long long kF = ((unsigned long long)(~L) << 32) | qi;
+  auto lower = [&](uint32_t lo, uint32_t hi, unsigned long long v) {
+    while (lo < hi) {
+      uint32_t m = (lo + hi) >> 1;
+      if (V.sk(m) < v) lo = m + 1; else hi = m;
+    }
+    return lo;
+  };
   uint32_t ans;
   if (S) {
-    ans = d_lower_u64(it.sk, b0, f, kT);
+    ans = lower(b0, f, kT);
     if (CHECK) {  // an F item with len == L and isa < I breaks monotonicity
-      uint32_t l3 = d_lower_u64(it.sk, f, b1, ((unsigned long long)(~L) << 32));
-      if (l3 < b1 && it.len[l3] == L && it.isa[l3] < qi) qs.viol++;
+      uint32_t l3 = lower(f, b1, (unsigned long long)(~L) << 32);
+      if (l3 < b1 && (uint32_t)~(V.sk(l3) >> 32) == L && (uint32_t)V.sk(l3) < qi) qs.viol++;
     }
   } else {
     if (CHECK) {  // a T item with len == L and isa >= I breaks monotonicity
-      uint32_t l3 = d_lower_u64(it.sk, b0, f, ((unsigned long long)(L + 1ull) << 32));
-      if ((unsigned long long)L + 1 > 0xffffffffull) l3 = f;
-      if (l3 > b0 && it.len[l3 - 1] == L && it.isa[l3 - 1] >= qi) qs.viol++;
+      uint32_t l3 = (unsigned long long)L + 1 > 0xffffffffull ? f
+                                                              : lower(b0, f, (unsigned long long)(L + 1u) << 32);
+      if (l3 > b0 && (uint32_t)(V.sk(l3 - 1) >> 32) == L && (uint32_t)V.sk(l3 - 1) >= qi) qs.viol++;
     }
-    ans = d_lower_u64(it.sk, f, b1, kF);
+    ans = lower(f, b1, kF);
   }
   if (ans >= b1) return;  // lower_bound == end(): FN:1535-1536
-  const unsigned long long ka = it.sk[ans];
+  const unsigned long long ka = V.sk(ans);
   const bool eq = ka == (ans < f ? kT : kF);  // MatchInSet::operator== (len, isaNext)
-  const uint32_t so = it.slot[ans];
+  const uint32_t so = V.slot(ans);
   if (eq) {  // same key: FN:1537-1589
-    const uint32_t co = it.count[ans];
+    const uint32_t co = V.slot(ans + 1) - so;
     const bool hasNext = ans + 1 < b1;
-    const uint32_t* me = A.nhr + slq;
-    const uint32_t* ot = A.nhr + so;
+    const uint32_t* me = V.nhr + slq;
+    const uint32_t* ot = V.nhr + so;
     if (me[cq - 1] < ot[0]) {
-      add(so, (unsigned long long)cq);
+      add(so, cq);
       qs.good++;
     } else if (me[0] > ot[co - 1]) {
-      if (hasNext) add(so + co, (unsigned long long)cq);
+      if (hasNext) add(so + co, cq);
       qs.good++;
     } else {
       qs.bad++;
       uint32_t rest = 0;
       for (uint32_t a = 0; a < cq; a++) {
         uint32_t bpos = d_upper_u32(ot, 0, co, me[a]);
-        if (bpos < co) add(so + bpos, 1ull);
+        if (bpos < co) add(so + bpos, 1u);
         else rest++;
       }
-      if (rest && hasNext) add(so + co, (unsigned long long)rest);
+      if (rest && hasNext) add(so + co, rest);
     }
   } else {
-    add(so, (unsigned long long)cq);
+    add(so, cq);
     qs.good++;
   }
 }
 
+// item/position views: global memory, or the block's staged window in LDS
+struct GlobalView {
+  const ItemsSoA* it;
+  const uint32_t* pb;
+  const uint32_t* pf;
+  const uint32_t* nhr;
+  __device__ uint32_t begin(uint32_t t) const { return pb[t]; }
+  __device__ uint32_t fbeg(uint32_t t) const { return pf[t]; }
+  __device__ unsigned long long sk(uint32_t q) const { return it->sk[q]; }
+  __device__ uint32_t slot(uint32_t q) const { return it->slot[q]; }
+};
+struct LdsView {  // items and positions rebased to the window
+  const unsigned long long* skL;
+  const uint32_t* slotL;
+  const uint32_t* pbL;
+  const uint32_t* pfL;
+  const uint32_t* nhr;
+  uint32_t iBeg, T0;
+  __device__ uint32_t begin(uint32_t t) const { return pbL[t - T0] ; }
+  __device__ uint32_t fbeg(uint32_t t) const { return pfL[t - T0]; }
+  __device__ unsigned long long sk(uint32_t q) const { return skL[q - iBeg]; }
+  __device__ uint32_t slot(uint32_t q) const { return slotL[q - iBeg]; }
+};
+
+constexpr uint32_t kWinItems = 4096;  // staged items (= max slots) per window
+constexpr uint32_t kWinPositions = 1024;
+
 template <bool CHECK>
 __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
-  __shared__ unsigned long long cnt[kWinSlots];
+  __shared__ uint32_t cnt[kWinItems];                   // 16 KB; per target the adds sum to <= H < 2^31
+  __shared__ unsigned long long skL[kWinItems];         // 32 KB
+  __shared__ uint32_t slotL[kWinItems + 1];             // 16 KB
+  __shared__ uint32_t pbL[kWinPositions + 1], pfL[kWinPositions];  // 8 KB
   __shared__ uint32_t s_next;
   __shared__ unsigned long long red[4];
   const ItemsSoA& it = A.it;
@@ -380,9 +417,14 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
   const uint32_t iBeg = A.posBegin[T0], iEnd = A.posBegin[T1];
   const uint32_t sb = it.slot[iBeg], se = it.slot[iEnd];
   const uint32_t nslot = se - sb;
-  const bool lds = nslot <= A.slotCap;
-  if (lds)
+  const bool lds = nslot <= A.slotCap && T1 - T0 <= kWinPositions;
+  if (lds) {
     for (uint32_t i = threadIdx.x; i < nslot; i += blockDim.x) cnt[i] = 0;
+    for (uint32_t i = threadIdx.x; i < iEnd - iBeg; i += blockDim.x) skL[i] = it.sk[iBeg + i];
+    for (uint32_t i = threadIdx.x; i <= iEnd - iBeg; i += blockDim.x) slotL[i] = it.slot[iBeg + i];
+    for (uint32_t i = threadIdx.x; i <= T1 - T0; i += blockDim.x) pbL[i] = A.posBegin[T0 + i];
+    for (uint32_t i = threadIdx.x; i < T1 - T0; i += blockDim.x) pfL[i] = A.posF[T0 + i];
+  }
   if (threadIdx.x == 0) s_next = 0;
   if (threadIdx.x < 4) red[threadIdx.x] = 0;
   __syncthreads();
@@ -391,8 +433,10 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
   const uint32_t nItems = nCross + (iEnd - iBeg);
   const uint32_t lane = threadIdx.x & 63;
   QueryStats qs;
-  auto addLds = [&](uint32_t s, unsigned long long v) { atomicAdd(&cnt[s - sb], v); };
-  auto addGlb = [&](uint32_t s, unsigned long long v) { atomicAdd(&A.counter[s], v); };
+  const LdsView LV{skL, slotL, pbL, pfL, A.nhr, iBeg, T0};
+  const GlobalView GV{&A.it, A.posBegin, A.posF, A.nhr};
+  auto addLds = [&](uint32_t s, uint32_t v) { atomicAdd(&cnt[s - sb], v); };
+  auto addGlb = [&](uint32_t s, uint32_t v) { atomicAdd(&A.counter[s], (unsigned long long)v); };
   while (true) {
     uint32_t j = 0;
     if (lane == 0) j = atomicAdd(&s_next, 1u);
@@ -409,8 +453,8 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
       const uint64_t t = t0 + lane;
       if (t > hi) break;
       const uint32_t k = (uint32_t)(t - p - 1);
-      if (lds) d_counter_query<CHECK>(A, ql, qi, S, cq, slq, k, (uint32_t)t, qs, addLds);
-      else d_counter_query<CHECK>(A, ql, qi, S, cq, slq, k, (uint32_t)t, qs, addGlb);
+      if (lds) d_counter_query<CHECK>(LV, ql, qi, S, cq, slq, k, (uint32_t)t, qs, addLds);
+      else d_counter_query<CHECK>(GV, ql, qi, S, cq, slq, k, (uint32_t)t, qs, addGlb);
     }
   }
   __syncthreads();
