@@ -7,7 +7,7 @@ OUT := cms-bwt_amd/build
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-function
 HOSTFLAGS := -O3 -std=c++17 -fPIC -Wall
 
-OBJS := $(OUT)/engine.o $(OUT)/ms_walk.o $(OUT)/merge.o $(OUT)/synth.o $(OUT)/host_index.o $(OUT)/host_reader.o
+OBJS := $(OUT)/engine.o $(OUT)/ms_walk.o $(OUT)/ms_walk2.o $(OUT)/merge.o $(OUT)/synth.o $(OUT)/host_index.o $(OUT)/host_reader.o
 HDRS := $(wildcard $(SRC)/*.h) include/cmsbwt.h
 
 all: lib cli oracle
@@ -20,6 +20,12 @@ $(OUT):
 
 $(OUT)/%.o: $(SRC)/%.hip $(HDRS) | $(OUT)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+# the uniform-step walk keeps its addresses in registers only without
+# SimplifyCFG store sinking (which otherwise moves them to scratch)
+W2WAVES ?= 6
+$(OUT)/ms_walk2.o: $(SRC)/ms_walk2.hip $(HDRS) | $(OUT)
+	$(HIPCC) $(HIPFLAGS) -mllvm -simplifycfg-sink-common=false -DCMSBWT_W2_WAVES=$(W2WAVES) -c -o $@ $<
 
 $(OUT)/host_%.o: $(SRC)/host_%.cpp $(HDRS) | $(OUT)
 	g++ $(HOSTFLAGS) -c -o $@ $<

@@ -8,6 +8,9 @@ namespace cmsbwt {
 constexpr int kMaxLevels = 6;   // block-minima levels over LCP (64^6 > 2^32)
 constexpr uint32_t kPoolB = 16; // head records per pool block
 constexpr uint8_t kSep = 2;     // CMS-BWT.h:28
+// Readable tail after x and after the collection text: the cooperative LCE
+// of the walk reads up to 1 KiB (+16 B) past its current position.
+constexpr uint64_t kTextPad = 2048;
 
 // Reference index staged in HBM; int32/uint32 arrays,
 // x as bytes with 64 bytes of padding so the LCE loop can read 16 B past n.
@@ -20,8 +23,15 @@ struct DevRef {
   const uint8_t* bwt;
   const int32_t* lvl[kMaxLevels];  // lvl[0][b] = min lcp[64b..64b+63], lvl[k] = min of 64 lvl[k-1]
   uint32_t lvlLen[kMaxLevels];
+  uint32_t lvlOff[kMaxLevels];     // lvl[k] == lcp + lvlOff[k] (one buffer, 16-B aligned levels)
   int nlvl;
   uint32_t n;
+  // Restart table (walk only): SA interval [kmer[c].x, kmer[c].y] of every
+  // K-mer over the reference's own alphabet, c = sum kmap[byte] << (B*(K-1-d));
+  // empty intervals have x > y.  kmer == nullptr disables it.
+  const int2* kmer;
+  const uint8_t* kmap;  // 256 entries, 0xff = byte absent from the reference text
+  uint32_t kmerK, kmerB;
 };
 
 // One restart chunk of the MS walk: positions [a, b) of document `doc`.

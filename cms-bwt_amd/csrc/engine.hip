@@ -159,7 +159,8 @@ struct Engine {
   DBuf<uint8_t> dx, dbwt;
   DBuf<int32_t> dsa, dlcp, dplcp;
   DBuf<uint32_t> disa;
-  DBuf<int32_t> dlvl[kMaxLevels];
+  DBuf<int2> dkmer;
+  DBuf<uint8_t> dkmap;
   DevRef R{};
 
   // ---- collection
@@ -274,33 +275,48 @@ struct Engine {
     for (uint32_t q = 0; q + 1 < n; q++)
       if ((int64_t)hix.plcp[q + 1] + 1 < (int64_t)hix.plcp[q])
         throw InputError{CMSBWT_EINPUT, "internal: PLCP monotonicity violated"};
-    dx.alloc((uint64_t)n + 128);
-    HIPCHK(hipMemsetAsync(dx.p, 0, n + 128, st));
+    dx.alloc((uint64_t)n + kTextPad);
+    HIPCHK(hipMemsetAsync(dx.p, 0, n + kTextPad, st));
     HIPCHK(hipMemcpyAsync(dx.p, hix.x.data(), n, hipMemcpyHostToDevice, st));
-    dsa.alloc(n);
+    // +16 entries: the uniform-step walk loads whole aligned 16-B blocks (and
+    // 8-entry windows) around an index, so arrays carry a readable tail
+    dsa.alloc((uint64_t)n + 16);
     HIPCHK(hipMemcpyAsync(dsa.p, hix.sa.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
-    disa.alloc(n);
+    disa.alloc((uint64_t)n + 16);
     HIPCHK(hipMemcpyAsync(disa.p, hix.isa.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
-    dlcp.alloc((uint64_t)n + 1);
-    HIPCHK(hipMemcpyAsync(dlcp.p, hix.lcp.data(), ((size_t)n + 1) * 4, hipMemcpyHostToDevice, st));
-    dplcp.alloc((uint64_t)n + 1);
+    dplcp.alloc((uint64_t)n + 17);
     HIPCHK(hipMemcpyAsync(dplcp.p, hix.plcp.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
     dbwt.alloc(n);
     HIPCHK(hipMemcpyAsync(dbwt.p, hix.bwt.data(), n, hipMemcpyHostToDevice, st));
-    // block minima levels over lcp[0..n)
-    std::vector<int32_t> prev(hix.lcp.begin(), hix.lcp.begin() + n), cur;
-    int L = 0;
+    // LCP and its block-minima levels in one buffer: [lcp | lvl0 | lvl1 ...],
+    // each part 16-B aligned with >= 16 readable entries of tail
     memset(&R, 0, sizeof(R));
-    do {
-      cur.assign((prev.size() + 63) / 64, INT32_MAX);
-      for (size_t i = 0; i < prev.size(); i++) cur[i / 64] = std::min(cur[i / 64], prev[i]);
-      dlvl[L].alloc(cur.size());
-      HIPCHK(hipMemcpyAsync(dlvl[L].p, cur.data(), cur.size() * 4, hipMemcpyHostToDevice, st));
-      R.lvl[L] = dlvl[L].p;
-      R.lvlLen[L] = (uint32_t)cur.size();
+    std::vector<std::vector<int32_t>> levels;
+    {
+      std::vector<int32_t> prev(hix.lcp.begin(), hix.lcp.begin() + n), cur;
+      do {
+        cur.assign((prev.size() + 63) / 64, INT32_MAX);
+        for (size_t i = 0; i < prev.size(); i++) cur[i / 64] = std::min(cur[i / 64], prev[i]);
+        levels.push_back(cur);
+        prev.swap(cur);
+      } while (prev.size() > 64 && (int)levels.size() < kMaxLevels);
+    }
+    auto pad = [](uint64_t k) { return (k + 16 + 3) & ~3ull; };
+    uint64_t total = pad((uint64_t)n + 1);
+    for (auto& v : levels) total += pad(v.size());
+    dlcp.alloc(total);
+    HIPCHK(hipMemcpyAsync(dlcp.p, hix.lcp.data(), ((size_t)n + 1) * 4, hipMemcpyHostToDevice, st));
+    uint64_t off = pad((uint64_t)n + 1);
+    int L = 0;
+    for (auto& v : levels) {
+      HIPCHK(hipMemcpyAsync(dlcp.p + off, v.data(), v.size() * 4, hipMemcpyHostToDevice, st));
+      R.lvl[L] = dlcp.p + off;
+      R.lvlOff[L] = (uint32_t)off;
+      R.lvlLen[L] = (uint32_t)v.size();
+      off += pad(v.size());
       L++;
-      prev.swap(cur);
-    } while (prev.size() > 64 && L < kMaxLevels);
+    }
+    sync();  // `levels` is pageable host memory
     R.nlvl = L;
     R.x = dx.p;
     R.sa = dsa.p;
@@ -309,10 +325,64 @@ struct Engine {
     R.plcp = dplcp.p;
     R.bwt = dbwt.p;
     R.n = n;
+    build_kmer_table();
     sync();
     refLoaded = true;
     stats.n = n;
     stats.t_index_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+
+  // Restart table of the uniform-step walk: a chunk restart at the SA root
+  // (K extensions by binary search, ~2 K log n dependent loads) becomes one
+  // table lookup when the K text bytes are all reference bytes and the K-mer
+  // occurs.  The table is exactly the SA range of each K-prefix, i.e. the
+  // state computeMSFactorAt (FN:45-88) reaches after K matched characters.
+  void build_kmer_table() {
+    R.kmer = nullptr;
+    R.kmap = nullptr;
+    R.kmerK = R.kmerB = 0;
+    if (!env_u32("CMSBWT_KMER", 1)) return;
+    const uint32_t n = hix.n;
+    uint64_t cnt[256] = {0};
+    for (uint64_t k = 0; k < hix.ref_len; k++) cnt[(uint8_t)hix.x[k]]++;
+    std::vector<uint8_t> map(256, 0xff);
+    uint32_t sigma = 0;
+    for (int c = 0; c < 256; c++)
+      if (cnt[c]) map[c] = (uint8_t)sigma++;
+    if (sigma < 2 || sigma > 64) return;
+    uint32_t B = 1;
+    while ((1u << B) < sigma) B++;
+    uint32_t lg = 1;
+    while ((1ull << lg) < n) lg++;
+    const uint32_t maxBits = std::min<uint32_t>(env_u32("CMSBWT_KMER_BITS", 24), std::max<uint32_t>(lg + 1, 12));
+    const uint32_t K = std::min<uint32_t>(maxBits / B, 16);
+    if (K < 3) return;
+    const uint64_t entries = 1ull << (B * K);
+    std::vector<int2> tab(entries + 2, make_int2(1, 0));
+    for (uint32_t i = 0; i < n; i++) {
+      const uint32_t s0 = (uint32_t)hix.sa[i];
+      if ((uint64_t)s0 + K > n) continue;
+      uint64_t code = 0;
+      bool ok = true;
+      for (uint32_t d = 0; d < K && ok; d++) {
+        const uint8_t m = map[(uint8_t)hix.x[s0 + d]];
+        ok = m != 0xff;
+        code = (code << B) | m;
+      }
+      if (!ok) continue;
+      int2& e = tab[code];
+      if (e.x > e.y) e = make_int2((int)i, (int)i);
+      else e.y = (int)i;  // SA order: ranges of one K-prefix are contiguous
+    }
+    dkmer.alloc(entries + 2);
+    HIPCHK(hipMemcpyAsync(dkmer.p, tab.data(), (entries + 2) * sizeof(int2), hipMemcpyHostToDevice, st));
+    dkmap.alloc(256);
+    HIPCHK(hipMemcpyAsync(dkmap.p, map.data(), 256, hipMemcpyHostToDevice, st));
+    sync();  // `tab` and `map` are pageable
+    R.kmer = dkmer.p;
+    R.kmap = dkmap.p;
+    R.kmerK = K;
+    R.kmerB = B;
   }
 
   // =====================================================================
@@ -337,8 +407,8 @@ struct Engine {
       if (len >= (1ull << 32) - 1) throw InputError{CMSBWT_ELIMIT, "document longer than 2^32 (uint32 positions)"};
       check_bytes(c.text.data() + c.off[d], len);
     }
-    dtext.alloc(c.text.size() + 128);
-    HIPCHK(hipMemsetAsync(dtext.p + c.text.size(), kSep, 128, st));
+    dtext.alloc(c.text.size() + kTextPad);
+    HIPCHK(hipMemsetAsync(dtext.p + c.text.size(), kSep, kTextPad, st));
     if (!c.text.empty()) HIPCHK(hipMemcpyAsync(dtext.p, c.text.data(), c.text.size(), hipMemcpyHostToDevice, st));
     hdoc = c.off;
     ddoc.alloc(hdoc.size());
@@ -361,8 +431,8 @@ struct Engine {
         throw InputError{CMSBWT_EARG, "loaded reference is not the synthetic reference of this seed"};
     uint64_t base = leadingEmpty ? 1 : 0;
     uint64_t total = base + ncopies * (L + 1);
-    dtext.alloc(total + 128);
-    HIPCHK(hipMemsetAsync(dtext.p, kSep, total + 128, st));
+    dtext.alloc(total + kTextPad);
+    HIPCHK(hipMemsetAsync(dtext.p, kSep, total + kTextPad, st));
     launch_synth_collection(dtext.p, L, seed, copy_begin, ncopies, synth_threshold(p), base, st);
     HIPCHK(hipGetLastError());
     hdoc.clear();
@@ -380,8 +450,17 @@ struct Engine {
 
   // =====================================================================
   // MS walk + head finalisation
+  // CMSBWT_WALK=1 selects the per-lane walk (k_ms_walk); default is the
+  // uniform-step walk (k_ms_walk2) over a chunk queue.
+  static bool walk_v1() { return env_u32("CMSBWT_WALK", 2) == 1; }
+  static uint32_t walk_lanes() { return std::max<uint32_t>(256, env_u32("CMSBWT_WALK_LANES", 256u * 32 * 64)); }
+
   uint32_t chunk_size() const {
     if (const char* e = getenv("CMSBWT_CHUNK")) return (uint32_t)std::max(64L, atol(e));
+    if (!walk_v1()) {  // queue-fed: ~4 chunks per lane
+      uint64_t c = chars / ((uint64_t)walk_lanes() * 4);
+      return (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(16384, c));
+    }
     uint64_t c = chars / (256ull * 64 * 64);
     c = std::max<uint64_t>(2048, std::min<uint64_t>(32768, c));
     return (uint32_t)c;
@@ -396,9 +475,16 @@ struct Engine {
     const uint32_t C = chunk_size();
     if (!plan.valid || plan.C != C) build_plan(C);
     const uint32_t nch = plan.nch;
-    DBuf<uint32_t> chunkCount, used;
+    DBuf<uint32_t> chunkCount, used, nextChunk;
     chunkCount.alloc(nch);
     used.alloc(1);
+    nextChunk.alloc(1);
+    const bool v1 = walk_v1();
+    DBuf<unsigned long long> w2stats;  // CMSBWT_W2_STATS=1: step counts of the uniform-step walk
+    if (!v1 && env_u32("CMSBWT_W2_STATS", 0)) {
+      w2stats.alloc(32);
+      w2stats.zero(st);
+    }
     // pool sized for ~3% heads + one partial block per chunk; grown on overflow
     uint64_t cap = (uint64_t)nch + chars / 32 / kPoolB + 1024;
     DBuf<HeadRec> rec;
@@ -410,9 +496,12 @@ struct Engine {
       blkChunk.alloc(cap);
       blkSeq.alloc(cap);
       used.zero(st);
+      nextChunk.zero(st);
       Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
       HIPCHK(hipEventRecord(ev0, st));
-      launch_ms_walk(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.laneChunk.p, pool, chunkCount.p, st);
+      if (v1) launch_ms_walk(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.laneChunk.p, pool, chunkCount.p, st);
+      else launch_ms_walk2(R, dtext.p, ddoc.p, plan.dch.p, nch, nextChunk.p, pool, chunkCount.p, walk_lanes(),
+                           w2stats.p, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(ev1, st));
       usedBlocks = read1(used.p);
@@ -421,6 +510,16 @@ struct Engine {
       stats.ms_walk_kernel_ms = ms;
       if (usedBlocks <= cap) break;
       cap = (uint64_t)usedBlocks + (uint64_t)nch + 1024;
+    }
+    if (w2stats.p) {
+      static const char* names[32] = {"done", "next", "bs_text", "bs_sa", "bs_x", "fail_sa", "lce_sa", "lce",
+                                       "skip1", "gallop", "skipbs", "isa1", "con1", "con2", "adj", "lce_coop",
+                                       "kmer_text", "kmer_tab", "scan0", "scan1", "scan2", "scan3", "-", "-", "wave_steps",
+                                       "coop_steps"};
+      std::vector<unsigned long long> h(32);
+      HIPCHK(hipMemcpy(h.data(), w2stats.p, 32 * 8, hipMemcpyDeviceToHost));
+      for (int k = 0; k < 32; k++)
+        if (h[k]) fprintf(stderr, "[w2stats] %-10s %llu\n", names[k] ? names[k] : "?", h[k]);
     }
     // chunk bases (end phrase counted in the last chunk of each document)
     DBuf<unsigned long long> withEnd, chunkBase;
@@ -437,7 +536,7 @@ struct Engine {
     hSmall.alloc(H); hChar.alloc(H); hNext.alloc(H);
     HeadsSoA h = heads();
     Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
-    launch_scatter_heads(pool, usedBlocks, chunkCount.p, chunkBase.p, h, st);
+    launch_scatter_heads(pool, usedBlocks, chunkCount.p, chunkBase.p, h, plan.dch.p, dtext.p, ddoc.p, st);
     DBuf<uint32_t> docEnd;
     docEnd.alloc(ndocs);
     launch_end_phrases(dtext.p, ddoc.p, (uint32_t)ndocs, plan.dLast.p, chunkCount.p, chunkBase.p, R.n, h, docEnd.p,

@@ -437,24 +437,43 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
   const GlobalView GV{&A.it, A.posBegin, A.posF, A.nhr};
   auto addLds = [&](uint32_t s, uint32_t v) { atomicAdd(&cnt[s - sb], v); };
   auto addGlb = [&](uint32_t s, uint32_t v) { atomicAdd(&A.counter[s], (unsigned long long)v); };
+  // Items are claimed 64 at a time: lane b loads item b's fields with one
+  // coalesced load per field, then the wave walks the batch reading them with
+  // readlane (no memory latency per item).
   while (true) {
-    uint32_t j = 0;
-    if (lane == 0) j = atomicAdd(&s_next, 1u);
-    j = __builtin_amdgcn_readfirstlane(__shfl(j, 0));
-    if (j >= nItems) break;
-    const uint32_t q = __builtin_amdgcn_readfirstlane(j < nCross ? A.crossList[c0 + j] : iBeg + (j - nCross));
-    const uint32_t p = it.pos[q], u = it.until[q];
-    if (!u) continue;
-    const uint32_t ql = it.len[q], qi = it.isa[q], cq = it.count[q], slq = it.slot[q];
-    const bool S = it.smaller[q] != 0;
-    const uint64_t lo = max((uint64_t)p + 1, (uint64_t)T0);
-    const uint64_t hi = min((uint64_t)p + u, (uint64_t)T1 - 1);
-    for (uint64_t t0 = lo; t0 <= hi; t0 += 64) {
-      const uint64_t t = t0 + lane;
-      if (t > hi) break;
-      const uint32_t k = (uint32_t)(t - p - 1);
-      if (lds) d_counter_query<CHECK>(LV, ql, qi, S, cq, slq, k, (uint32_t)t, qs, addLds);
-      else d_counter_query<CHECK>(GV, ql, qi, S, cq, slq, k, (uint32_t)t, qs, addGlb);
+    uint32_t j0 = 0;
+    if (lane == 0) j0 = atomicAdd(&s_next, 64u);
+    j0 = __builtin_amdgcn_readfirstlane(__shfl(j0, 0));
+    if (j0 >= nItems) break;
+    const uint32_t nb = min(64u, nItems - j0);
+    uint32_t bp = 0, bu = 0, bl = 0, bi = 0, bc = 0, bs = 0, bS = 0;
+    if (lane < nb) {
+      const uint32_t j = j0 + lane;
+      const uint32_t q = j < nCross ? A.crossList[c0 + j] : iBeg + (j - nCross);
+      bp = it.pos[q];
+      bu = it.until[q];
+      bl = it.len[q];
+      bi = it.isa[q];
+      bc = it.count[q];
+      bs = it.slot[q];
+      bS = it.smaller[q];
+    }
+    for (uint32_t e = 0; e < nb; e++) {
+      const uint32_t u = __builtin_amdgcn_readlane(bu, e);
+      if (!u) continue;
+      const uint32_t p = __builtin_amdgcn_readlane(bp, e);
+      const uint32_t ql = __builtin_amdgcn_readlane(bl, e), qi = __builtin_amdgcn_readlane(bi, e);
+      const uint32_t cq = __builtin_amdgcn_readlane(bc, e), slq = __builtin_amdgcn_readlane(bs, e);
+      const bool S = __builtin_amdgcn_readlane(bS, e) != 0;
+      const uint64_t lo = max((uint64_t)p + 1, (uint64_t)T0);
+      const uint64_t hi = min((uint64_t)p + u, (uint64_t)T1 - 1);
+      for (uint64_t t0 = lo; t0 <= hi; t0 += 64) {
+        const uint64_t t = t0 + lane;
+        if (t > hi) break;
+        const uint32_t k = (uint32_t)(t - p - 1);
+        if (lds) d_counter_query<CHECK>(LV, ql, qi, S, cq, slq, k, (uint32_t)t, qs, addLds);
+        else d_counter_query<CHECK>(GV, ql, qi, S, cq, slq, k, (uint32_t)t, qs, addGlb);
+      }
     }
   }
   __syncthreads();

@@ -252,7 +252,7 @@ __global__ void __launch_bounds__(256) k_ms_walk(DevRef R, const uint8_t* __rest
         r.start = i;
         r.pos = pos;
         r.len = len;
-        r.flags = (smaller ? 1u : 0u) | ((uint32_t)(i == 0 ? kSep : t[i - 1]) << 8);
+        r.flags = smaller ? 1u : 0u;
         pool.rec[(uint64_t)blk * kPoolB + fill] = r;
       }
       fill++;
@@ -281,7 +281,9 @@ __global__ void k_chunk_with_end(const Chunk* __restrict__ chunks, const uint32_
 }
 
 __global__ void k_scatter_heads(Pool pool, uint32_t blocksUsed, const uint32_t* __restrict__ chunkCount,
-                                const unsigned long long* __restrict__ chunkBase, HeadsSoA h) {
+                                const unsigned long long* __restrict__ chunkBase, HeadsSoA h,
+                                const Chunk* __restrict__ chunks, const uint8_t* __restrict__ text,
+                                const uint64_t* __restrict__ docOff) {
   uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t blk = slot / kPoolB;
   if (blk >= blocksUsed) return;
@@ -294,7 +296,8 @@ __global__ void k_scatter_heads(Pool pool, uint32_t blocksUsed, const uint32_t* 
   h.pos[idx] = r.pos;
   h.len[idx] = r.len;
   h.smaller[idx] = (uint8_t)(r.flags & 1u);
-  h.lchar[idx] = (uint8_t)(r.flags >> 8);
+  // BWT character of the phrase: the text byte before it, 0x02 at a document start
+  h.lchar[idx] = r.start == 0 ? (uint8_t)kSep : text[docOff[chunks[cid].doc] + r.start - 1];
 }
 
 // End-of-document phrase (FN:1198-1212): (docLen, n-1, 0, false), char =
@@ -400,11 +403,12 @@ void launch_chunk_with_end(const Chunk* chunks, const uint32_t* chunkCount, uint
 }
 
 void launch_scatter_heads(const Pool& pool, uint32_t blocksUsed, const uint32_t* chunkCount,
-                          const unsigned long long* chunkBase, const HeadsSoA& h, hipStream_t st) {
+                          const unsigned long long* chunkBase, const HeadsSoA& h, const Chunk* chunks,
+                          const uint8_t* text, const uint64_t* docOff, hipStream_t st) {
   uint64_t slots = (uint64_t)blocksUsed * kPoolB;
   if (!slots) return;
   hipLaunchKernelGGL(k_scatter_heads, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, pool,
-                     blocksUsed, chunkCount, chunkBase, h);
+                     blocksUsed, chunkCount, chunkBase, h, chunks, text, docOff);
 }
 
 void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t ndocs,

@@ -1,0 +1,679 @@
+// ms_walk2.hip — uniform-step MS walk (the default walk kernel).
+//
+// Same semantics as k_ms_walk (FN:45-149, FN:1151-1212, rmq_tree.h:184-225),
+// restructured for SIMT.  In the per-lane walk the nested loops (binary
+// searches, LCE, PLCP skip, PSV/NSV scans) make the 64 lanes of a wave issue
+// their dependent loads in separate, mostly-inactive instructions.  Here
+// every iteration each lane issues up to four 16-byte loads (slots 0/1 = the
+// aligned block holding address A and the next one, slots 2/3 the same for
+// address B; the LCE loads 16 unaligned bytes at A and B) and advances its own state machine by exactly one step, so one memory
+// latency moves every lane forward.  Lanes pull restart chunks from a global
+// queue (one atomic per wave) until it is empty.
+//
+//   phase     loads                          next
+//   BS_TEXT   t[j], SA[first probe]          BS_X          (FN:94-149)
+//   BS_SA     SA[m]                          BS_X
+//   BS_X      x[SA[m]+off]                   BS_SA / result
+//   FAIL_SA   SA[insertion point]            head record   (FN:65-76)
+//   LCE_SA    SA[lb]                         LCE           (FN:52-62)
+//   LCE       16 B of x and of the text      LCE_COOP / head record
+//   LCE_COOP  (no lane load) the whole wave compares 1 KiB per step of one
+//             lane's long extension with coalesced loads, lane by lane
+//   SKIP1     PLCP[pos+1], PLCP[T-7..T]      ISA1 / GALLOP (FN:1176-1185)
+//   GALLOP/SKIPBS  one PLCP probe            ISA1
+//   ISA1      ISA[pos+1]                     ADJ           (FN:1187)
+//   CON1/CON2 SA[lb],SA[rb] / ISA[..+1]      ADJ / root    (FN:34-43)
+//   ADJ       8 entries for PSV + 8 for NSV  ADJ / next position (FN:11-25)
+//   KMER_TEXT/KMER_TAB  restart: K text bytes, then the K-mer's SA interval
+//             (= the state after K matched characters from the root)
+//
+// Registers: the phase-local variables share ten 32-bit slots (u0..u9).
+// Cost model (measured): the walk is bound by per-lane divergent load
+// instructions (each a separate cache-line request), not by latency -- 5..7
+// waves per SIMD time the same, and widening each lane's window to 64 B with
+// more 16-B loads made it 2.6x slower.  Hence: few loads per step, and the
+// long extensions (about one per SNP, ~1000 bytes) moved to coalesced
+// wave-wide compares.
+#include "device_common.h"
+#include "kernels.h"
+
+namespace cmsbwt {
+
+namespace {
+
+enum : uint32_t {
+  PH_DONE = 0,
+  PH_NEXT,  // needs a new chunk (no load)
+  PH_BS_TEXT,
+  PH_BS_SA,
+  PH_BS_X,
+  PH_FAIL_SA,
+  PH_LCE_SA,
+  PH_LCE,
+  PH_SKIP1,
+  PH_GALLOP,
+  PH_SKIPBS,
+  PH_ISA1,
+  PH_CON1,
+  PH_CON2,
+  PH_ADJ,
+  PH_LCE_COOP,  // long extension, served by the whole wave (no lane load)
+  PH_KMER_TEXT, // restart: K text bytes
+  PH_KMER_TAB,  // restart: SA interval of the K-mer
+};
+
+// Loads through global-address-space pointers (global_load_*, not flat), each
+// as narrow as the step needs.
+#define GPTR(T, a) ((const __attribute__((address_space(1))) T*)(a))
+__device__ __forceinline__ uint32_t ld1(uintptr_t a) { return *GPTR(uint8_t, a); }
+__device__ __forceinline__ uint32_t ld4(uintptr_t a) { return *GPTR(uint32_t, a); }
+// 16 bytes at any address (gfx950 global loads allow unaligned dwordx4)
+__device__ __forceinline__ uint4 ldu16(uintptr_t a) {
+  typedef uint32_t u4u __attribute__((ext_vector_type(4), aligned(1)));
+  const u4u v = *GPTR(u4u, a);
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+// slot loads of one step (`use` bits)
+enum : uint32_t {
+  U0B = 1,   // byte at A
+  U0D = 2,   // dword at A
+  U0Q = 4,   // 16 B at A
+  U1Q = 8,   // 16 B at A + 16
+  U2D = 16,  // dword at B
+  U2Q = 32,  // 16 B at B
+  U3Q = 64,  // 16 B at B + 16
+};
+// First differing byte of two 16-byte strings: 16 if equal.
+__device__ __forceinline__ uint32_t diff16(const uint4& x, const uint4& t, uint8_t& xc, uint8_t& tc) {
+  const uint64_t x0 = x.x | ((uint64_t)x.y << 32), x1 = x.z | ((uint64_t)x.w << 32);
+  const uint64_t t0 = t.x | ((uint64_t)t.y << 32), t1 = t.z | ((uint64_t)t.w << 32);
+  const uint64_t d0 = x0 ^ t0, d1 = x1 ^ t1;
+  if (!(d0 | d1)) return 16;
+  const uint64_t d = d0 ? d0 : d1;
+  const uint32_t bit = (uint32_t)__builtin_ctzll(d) & ~7u;
+  xc = (uint8_t)((d0 ? x0 : x1) >> bit);
+  tc = (uint8_t)((d0 ? t0 : t1) >> bit);
+  return (d0 ? 0 : 8) + bit / 8;
+}
+
+__device__ __forceinline__ uint32_t lvl_len(const DevRef& R, uint32_t L) {
+  uint32_t v = R.lvlLen[0];
+#pragma unroll
+  for (uint32_t k = 1; k < (uint32_t)kMaxLevels; k++)
+    if (L == k) v = R.lvlLen[k];
+  return v;
+}
+__device__ __forceinline__ uint32_t lvl_off(const DevRef& R, uint32_t L) {
+  uint32_t v = R.lvlOff[0];
+#pragma unroll
+  for (uint32_t k = 1; k < (uint32_t)kMaxLevels; k++)
+    if (L == k) v = R.lvlOff[k];
+  return v;
+}
+
+// ---- PSV (UP=false) / NSV (UP=true) as a state machine over 8-entry windows
+// (rmq_tree.h:184-225).  State: cur/lim = remaining range of the current
+// array (down: cur..lim, up: cur..lim), res = answer, idx = climbing index,
+// ls = level | stage << 4.  Stages: 0 = LCP block of the start, 1 = climb
+// level L, 2 = descend level L, 3 = final LCP block, 4 = done.
+constexpr uint32_t kScanDone = 4u << 4;
+
+template <bool UP>
+__device__ __forceinline__ int32_t window_base(int32_t cur) {
+  const int32_t b = UP ? (cur & ~3) : (cur & ~3) - 4;
+  return b < 0 ? 0 : b;
+}
+
+template <bool UP>
+__device__ __forceinline__ uintptr_t scan_addr(const DevRef& R, int32_t cur, uint32_t ls) {
+  const uint32_t stg = ls >> 4;
+  const uint32_t off = (stg == 0 || stg == 3) ? 0u : lvl_off(R, ls & 15);
+  return (uintptr_t)(R.lcp + off + (uint32_t)window_base<UP>(cur));
+}
+
+// Stage transitions that need no memory access.
+template <bool UP>
+__device__ __forceinline__ void scan_settle(const DevRef& R, int32_t& cur, int32_t& lim, int32_t& res,
+                                            int32_t& idx, uint32_t& ls) {
+  for (int guard = 0; guard < kMaxLevels + 2; guard++) {
+    uint32_t stg = ls >> 4, L = ls & 15;
+    if (stg == 4) return;
+    if (UP ? (cur <= lim) : (cur >= lim)) return;  // range left: needs a load
+    if (stg == 0) {
+      stg = 1;
+      L = 0;
+    } else if (stg == 1) {
+      const int32_t len = (int32_t)lvl_len(R, L);
+      const bool top = UP ? (min(idx | 63, len - 1) >= len - 1) : ((idx & ~63) == 0);
+      idx >>= 6;
+      L++;
+      if (top || (int)L >= R.nlvl) { res = -1; ls = kScanDone; return; }
+    } else {  // a descent always finds (block minimum < ub); defensive
+      res = -1;
+      ls = kScanDone;
+      return;
+    }
+    const int32_t len = (int32_t)lvl_len(R, L);
+    if (!UP) { cur = idx - 1; lim = idx & ~63; }
+    else { cur = idx + 1; lim = min(idx | 63, len - 1); }
+    ls = L | (stg << 4);
+  }
+}
+
+template <bool UP>
+__device__ __forceinline__ void scan_start(const DevRef& R, int32_t i, int32_t& cur, int32_t& lim, int32_t& res,
+                                           int32_t& idx, uint32_t& ls) {
+  const int32_t n = (int32_t)R.n;
+  res = -1;
+  if (UP && i >= n) { ls = kScanDone; return; }
+  ls = 0;
+  idx = i >> 6;
+  cur = i;
+  lim = UP ? min(i | 63, n - 1) : (i & ~63);
+  scan_settle<UP>(R, cur, lim, res, idx, ls);
+}
+
+template <bool UP>
+__device__ __forceinline__ void scan_step(const DevRef& R, const uint4& v0, const uint4& v1, int32_t ub,
+                                          int32_t& cur, int32_t& lim, int32_t& res, int32_t& idx, uint32_t& ls) {
+  const int32_t n = (int32_t)R.n;
+  const int32_t base = window_base<UP>(cur);
+  const int32_t e[8] = {(int32_t)v0.x, (int32_t)v0.y, (int32_t)v0.z, (int32_t)v0.w,
+                        (int32_t)v1.x, (int32_t)v1.y, (int32_t)v1.z, (int32_t)v1.w};
+  const int32_t klo = (UP ? max(cur, base) : max(lim, base)) - base;
+  const int32_t khi = (UP ? min(lim, base + 7) : min(cur, base + 7)) - base;
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 8; k++)
+    if (k >= klo && k <= khi && e[k] < ub) m |= 1u << k;
+  if (m) {
+    const int32_t k = UP ? base + __builtin_ctz(m) : base + 31 - __builtin_clz(m);
+    const uint32_t stg = ls >> 4, L = ls & 15;
+    if (stg == 0 || stg == 3) { res = k; ls = kScanDone; return; }
+    // hit in a level array: descend into block k of the level below
+    int32_t top;
+    uint32_t nls;
+    if (L == 0) { top = n - 1; nls = 3u << 4; }
+    else { top = (int32_t)lvl_len(R, L - 1) - 1; nls = (L - 1) | (2u << 4); }
+    const int32_t lo = k * 64, hi = min(k * 64 + 63, top);
+    if (UP) { cur = lo; lim = hi; } else { cur = hi; lim = lo; }
+    ls = nls;
+    return;
+  }
+  cur = UP ? base + 8 : base - 1;
+  scan_settle<UP>(R, cur, lim, res, idx, ls);
+}
+
+}  // namespace
+
+struct Walk2Args {
+  DevRef R;
+  const uint8_t* text;
+  const uint64_t* docOff;
+  const Chunk* chunks;
+  uint32_t nchunks;
+  uint32_t* nextChunk;
+  Pool pool;
+  uint32_t* chunkCount;
+  unsigned long long* stats;  // STATS builds: per-phase lane-steps, wave-steps, ...
+};
+
+#ifndef CMSBWT_W2_WAVES
+#define CMSBWT_W2_WAVES 6
+#endif
+// 6 waves/SIMD fit without spills (80 VGPRs); more waves spill (measured).
+template <bool STATS>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CMSBWT_W2_WAVES, 8)))
+k_ms_walk2(Walk2Args A) {
+  __shared__ unsigned long long sc[STATS ? 32 : 1];
+  __shared__ uint8_t kmapL[256];
+  if (STATS && threadIdx.x < 32) sc[threadIdx.x] = 0;
+  if (A.R.kmer) kmapL[threadIdx.x] = A.R.kmap[threadIdx.x];  // blockDim == 256
+  __syncthreads();
+  const DevRef& R = A.R;
+  const uint32_t n = R.n;
+  const uintptr_t X = (uintptr_t)R.x;
+  const uintptr_t SA = (uintptr_t)R.sa;
+  const uintptr_t P = (uintptr_t)R.plcp;
+  const uint32_t lane = threadIdx.x & 63;
+
+  // chunk
+  uint32_t cid = 0, a = 0, b = 0;
+  uintptr_t T = 0;
+  // walk state (FN:1151-1196)
+  uint32_t i = 0, len = 0, pos = 0, prevPos = 0;
+  int32_t lb = 0, rb = 0;
+  bool smaller = false;
+  // emission
+  uint32_t count = 0, blk = 0xffffffffu, fill = kPoolB, seq = 0;
+  uint32_t phase = PH_NEXT, use = 0;
+  uintptr_t ad0 = X, ad2 = X;
+  // phase-local slots
+  int32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0, u4 = 0, u5 = 0, u6 = 0, u7 = 0, u8 = 0;
+  uint32_t u9 = 0;
+  // binary search (BS_*): u0 = c | ansVal << 8 | ansSet << 16 | ubMode << 17,
+  //   u1 = lo, u2 = hi (exclusive), u3 = probe, u5 = new lb while searching the right end
+  // skip (SKIP1/GALLOP/SKIPBS): u1 = lo, u2 = hi, u3 = probe, u4 = gallop step
+  // ADJ: PSV = (u0 cur, u1 lim, u2 res, u3 idx, u4 ls), NSV = (u5, u6, u7, u8, u9)
+  // `len` doubles as `off` during an extension (FN:48: off starts at len).
+
+  auto begin_char = [&]() {  // next character of computeMSFactorAt at j = i + len
+    if (lb == rb) {
+      phase = PH_LCE_SA;
+      ad0 = SA + 4ull * (uint32_t)lb;
+      use = U0D;
+    } else {
+      phase = PH_BS_TEXT;
+      u1 = lb;
+      u2 = rb + 1;
+      u3 = (u1 + u2) >> 1;
+      u0 = 0;
+      ad0 = T + i + len;
+      ad2 = SA + 4ull * (uint32_t)u3;
+      use = U0B | U2D;
+    }
+  };
+  auto emit = [&]() {
+    if (fill == kPoolB) {
+      blk = atomicAdd(A.pool.used, 1u);
+      fill = 0;
+      if (blk < A.pool.capBlocks) { A.pool.blkChunk[blk] = cid; A.pool.blkSeq[blk] = seq; }
+      seq++;
+    }
+    if (blk < A.pool.capBlocks) {
+      HeadRec r;
+      r.start = i;
+      r.pos = pos;
+      r.len = len;
+      r.flags = smaller ? 1u : 0u;
+      A.pool.rec[(uint64_t)blk * kPoolB + fill] = r;
+    }
+    fill++;
+    count++;
+  };
+  auto advance = [&]() {
+    i++;
+    prevPos = pos;
+    if (i >= b) {
+      A.chunkCount[cid] = count;
+      phase = PH_NEXT;
+      use = 0;
+    } else {
+      begin_char();
+    }
+  };
+  auto adj_or_finish = [&]() {
+    if ((uint32_t)u4 == kScanDone && u9 == kScanDone) {
+      lb = u2 == -1 ? 0 : u2;
+      rb = u7 == -1 ? (int32_t)n - 1 : u7 - 1;
+      advance();
+    } else {
+      phase = PH_ADJ;
+      use = 0;
+      if ((uint32_t)u4 != kScanDone) { ad0 = scan_addr<false>(R, u0, (uint32_t)u4); use |= U0Q | U1Q; }
+      if (u9 != kScanDone) { ad2 = scan_addr<true>(R, u5, u9); use |= U2Q | U3Q; }
+    }
+  };
+  auto start_adj = [&](int32_t lo, int32_t hi) {  // adjustInterval (FN:11-25)
+    uint32_t ls0;
+    scan_start<false>(R, lo, u0, u1, u2, u3, ls0);
+    scan_start<true>(R, hi + 1, u5, u6, u7, u8, u9);
+    u4 = (int32_t)ls0;
+    adj_or_finish();
+  };
+  auto post_ext = [&]() {  // head test and record (FN:1154-1171), then contraction
+    if (i >= a && pos != prevPos + 1) emit();
+    len--;
+    if (lb == rb) {  // FN:1175-1189
+      phase = PH_SKIP1;
+      ad0 = P + 4ull * (pos + 1);
+      use = U0D;
+      if (len > 8) {
+        const uint64_t TT = (uint64_t)pos + 1 + len;
+        ad2 = P + 4ull * ((TT & ~3ull) - 4);
+        use = U0D | U2Q | U3Q;
+      }
+    } else {  // FN:1190-1194
+      phase = PH_CON1;
+      ad0 = SA + 4ull * (uint32_t)lb;
+      ad2 = SA + 4ull * (uint32_t)rb;
+      use = U0D | U2D;
+    }
+  };
+  auto skip_done = [&](uint32_t s) {
+    i += s;
+    len -= s;
+    pos += s;
+    phase = PH_ISA1;
+    ad0 = (uintptr_t)(R.isa + pos + 1);
+    use = U0D;
+  };
+  // gallop (u4 = step, u1 = lo) then binary search on (u1, u2]
+  auto skip_probe = [&](bool galloping) {
+    if (galloping) {
+      const uint64_t t = (uint64_t)(uint32_t)u1 + (uint32_t)u4;
+      if (t < len) {
+        u3 = (int32_t)t;
+        phase = PH_GALLOP;
+        ad0 = P + 4ull * (pos + 1 + (uint32_t)u3);
+        use = U0D;
+        return;
+      }
+      u2 = (int32_t)len;
+    }
+    if ((uint32_t)u2 - (uint32_t)u1 > 1) {
+      u3 = (int32_t)((uint32_t)u1 + (((uint32_t)u2 - (uint32_t)u1) >> 1));
+      phase = PH_SKIPBS;
+      ad0 = P + 4ull * (pos + 1 + (uint32_t)u3);
+      use = U0D;
+    } else {
+      skip_done((uint32_t)u2);
+    }
+  };
+  // lower_bound / upper_bound driver: next probe or result
+  auto bs_next = [&]() {
+    while (true) {
+      if (u1 < u2) {
+        u3 = (u1 + u2) >> 1;
+        phase = PH_BS_SA;
+        ad0 = SA + 4ull * (uint32_t)u3;
+        use = U0D;
+        return;
+      }
+      const uint32_t f = (uint32_t)u0;
+      if (!(f & (1u << 17))) {  // lower bound done
+        if ((f & (1u << 16)) && ((f >> 8) & 0xff) == (f & 0xff)) {
+          u5 = u1;  // new lb; now the right end in [lb'+1, rb+1)
+          u0 = (int32_t)(f | (1u << 17));
+          u1 = u5 + 1;
+          u2 = rb + 1;
+          continue;
+        }
+        int32_t mm = u1;  // mismatch: insertion point (FN:65-76)
+        smaller = true;
+        if (mm == rb + 1) { mm = rb; smaller = false; }
+        phase = PH_FAIL_SA;
+        ad0 = SA + 4ull * (uint32_t)mm;
+        use = U0D;
+        return;
+      }
+      // upper bound done: interval [u5, u1 - 1], one more matched character
+      lb = u5;
+      rb = u1 - 1;
+      len++;
+      begin_char();
+      return;
+    }
+  };
+
+  while (true) {
+    // ---- refill lanes from the chunk queue (one atomic per wave)
+    const uint64_t need = __ballot(phase == PH_NEXT);
+    if (need) {
+      const uint32_t first = (uint32_t)__builtin_ctzll(need);
+      uint32_t base = 0;
+      if (lane == first) base = atomicAdd(A.nextChunk, (uint32_t)__popcll(need));
+      base = __shfl(base, first);
+      if (phase == PH_NEXT) {
+        const uint32_t my = base + (uint32_t)__popcll(need & ((1ull << lane) - 1));
+        if (my >= A.nchunks) {
+          phase = PH_DONE;
+          use = 0;
+        } else {
+          cid = my;
+          const Chunk ch = A.chunks[cid];
+          T = (uintptr_t)(A.text + A.docOff[ch.doc]);
+          a = ch.a;
+          b = ch.b;
+          count = 0;
+          fill = kPoolB;
+          seq = 0;
+          i = a > 0 ? a - 1 : 0;
+          if (i >= b) {
+            A.chunkCount[cid] = 0;  // empty document: stays PH_NEXT
+          } else {
+            len = 0;
+            pos = n - 1;
+            lb = 0;
+            rb = (int32_t)n - 1;
+            prevPos = 0xfffffffeu;  // prevPos + 1 never equals a position
+            smaller = false;
+            if (R.kmer) {
+              phase = PH_KMER_TEXT;
+              ad0 = T + i;
+              use = U0Q;
+            } else {
+              begin_char();
+            }
+          }
+        }
+      }
+    }
+    if (!__ballot(phase != PH_DONE)) break;
+    if (STATS) {
+      if (phase != PH_DONE) atomicAdd(&sc[phase], 1ull);
+      if (phase == PH_ADJ) {
+        if ((uint32_t)u4 != kScanDone) atomicAdd(&sc[18 + ((uint32_t)u4 >> 4)], 1ull);
+        if (u9 != kScanDone) atomicAdd(&sc[18 + (u9 >> 4)], 1ull);
+      }
+      if (lane == 0) atomicAdd(&sc[24], 1ull);
+    }
+    // ---- one memory step
+    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0, v2 = v0, v3 = v0;
+    if (use & U0B) v0.x = ld1(ad0);
+    if (use & U0D) v0.x = ld4(ad0);
+    if (use & U0Q) v0 = ldu16(ad0);
+    if (use & U1Q) v1 = ldu16(ad0 + 16);
+    if (use & U2D) v2.x = ld4(ad2);
+    if (use & U2Q) v2 = ldu16(ad2);
+    if (use & U3Q) v3 = ldu16(ad2 + 16);
+    // ---- one state-machine step
+    switch (phase) {
+      case PH_BS_TEXT: {  // c = t[j]; the first probe's SA value is in slot 2
+        u0 = (int32_t)v0.x;
+        ad0 = X + v2.x + len;
+        phase = PH_BS_X;
+        use = U0B;
+        break;
+      }
+      case PH_BS_SA: {
+        ad0 = X + v0.x + len;
+        phase = PH_BS_X;
+        use = U0B;
+        break;
+      }
+      case PH_BS_X: {
+        const uint32_t v = v0.x;
+        const uint32_t f = (uint32_t)u0, c = f & 0xff;
+        if (!(f & (1u << 17))) {
+          if (v < c) u1 = u3 + 1;
+          else { u2 = u3; u0 = (int32_t)(c | (v << 8) | (1u << 16)); }
+        } else {
+          if (v <= c) u1 = u3 + 1;
+          else u2 = u3;
+        }
+        bs_next();
+        break;
+      }
+      case PH_FAIL_SA: {
+        pos = v0.x;
+        post_ext();
+        break;
+      }
+      case PH_LCE_SA: {
+        pos = v0.x;
+        phase = PH_LCE;
+        ad0 = X + pos + len;
+        ad2 = T + i + len;
+        use = U0Q | U2Q;
+        break;
+      }
+      case PH_LCE: {
+        uint8_t xc = 0, tc = 0;
+        const uint32_t m = diff16(v0, v2, xc, tc);
+        if (m < 16) {
+          len += m;
+          smaller = (int8_t)xc > (int8_t)tc;  // FN:55, char compare
+          post_ext();
+        } else {  // long extension: hand it to the wave
+          len += 16;
+          ad0 += 16;
+          ad2 += 16;
+          phase = PH_LCE_COOP;
+          use = 0;
+        }
+        break;
+      }
+      case PH_SKIP1: {
+        const int64_t p0 = (int32_t)v0.x;
+        if ((int64_t)len <= p0) { skip_done(0); break; }
+        if (len > 8) {
+          // entries B..B+7 around TT (TT - B in [4, 7]); PLCP[q] + q is
+          // non-decreasing, so if B is below TT every crossing lies in (B, TT]
+          const int64_t TT = (int64_t)pos + 1 + len;
+          const int64_t B = (TT & ~3ll) - 4;
+          const int32_t e[8] = {(int32_t)v2.x, (int32_t)v2.y, (int32_t)v2.z, (int32_t)v2.w,
+                                (int32_t)v3.x, (int32_t)v3.y, (int32_t)v3.z, (int32_t)v3.w};
+          if ((int64_t)e[0] + B < TT) {
+            uint32_t cc = 0;
+#pragma unroll
+            for (int k = 1; k < 8; k++) cc += (B + k < TT && (int64_t)e[k] + B + k < TT) ? 1u : 0u;
+            skip_done((uint32_t)(B + 1 + cc - ((int64_t)pos + 1)));
+            break;
+          }
+        }
+        u1 = 0;
+        u4 = 1;
+        skip_probe(true);
+        break;
+      }
+      case PH_GALLOP: {
+        const int64_t v = (int32_t)v0.x;
+        if ((int64_t)len - (int64_t)(uint32_t)u3 <= v) {
+          u2 = u3;
+          skip_probe(false);
+        } else {
+          u1 = u3;
+          u4 <<= 1;
+          skip_probe(true);
+        }
+        break;
+      }
+      case PH_SKIPBS: {
+        const int64_t v = (int32_t)v0.x;
+        if ((int64_t)len - (int64_t)(uint32_t)u3 <= v) u2 = u3; else u1 = u3;
+        skip_probe(false);
+        break;
+      }
+      case PH_ISA1: {
+        const int32_t v = (int32_t)v0.x;
+        start_adj(v, v);
+        break;
+      }
+      case PH_CON1: {
+        const uint32_t sl = v0.x, sh = v2.x;
+        if (sl == n - 1 || sh == n - 1) {  // root (FN:37-39)
+          lb = 0;
+          rb = (int32_t)n - 1;
+          advance();
+        } else {
+          phase = PH_CON2;
+          ad0 = (uintptr_t)(R.isa + sl + 1);
+          ad2 = (uintptr_t)(R.isa + sh + 1);
+          use = U0D | U2D;
+        }
+        break;
+      }
+      case PH_CON2: {
+        start_adj((int32_t)v0.x, (int32_t)v2.x);
+        break;
+      }
+      case PH_KMER_TEXT: {
+        const uint32_t K = R.kmerK, Bb = R.kmerB;
+        uint64_t code = 0;
+        bool ok = true;
+#pragma unroll
+        for (uint32_t d = 0; d < 16; d++) {
+          if (d < K) {
+            const uint32_t w = d < 4 ? v0.x : d < 8 ? v0.y : d < 12 ? v0.z : v0.w;
+            const uint32_t m = kmapL[(w >> (8 * (d & 3))) & 0xff];
+            ok = ok && m != 0xff;
+            code = (code << Bb) | (m & 0xff);
+          }
+        }
+        if (ok) {
+          phase = PH_KMER_TAB;
+          ad0 = (uintptr_t)(R.kmer + code);
+          use = U0Q;
+        } else {
+          begin_char();  // from the root
+        }
+        break;
+      }
+      case PH_KMER_TAB: {
+        if ((int32_t)v0.x <= (int32_t)v0.y) {
+          lb = (int32_t)v0.x;
+          rb = (int32_t)v0.y;
+          len = R.kmerK;
+        }
+        begin_char();
+        break;
+      }
+      case PH_ADJ: {
+        uint32_t ls0 = (uint32_t)u4;
+        if (ls0 != kScanDone) scan_step<false>(R, v0, v1, (int32_t)len, u0, u1, u2, u3, ls0);
+        u4 = (int32_t)ls0;
+        if (u9 != kScanDone) scan_step<true>(R, v2, v3, (int32_t)len, u5, u6, u7, u8, u9);
+        adj_or_finish();
+        break;
+      }
+      default:
+        break;
+    }
+    // ---- long extensions: the wave compares 1 KiB per step for one lane at
+    // a time, lane k loading bytes [16k, 16k+16) of x and of the text
+    uint64_t coop = __ballot(phase == PH_LCE_COOP);
+    while (coop) {
+      const uint32_t L = (uint32_t)__builtin_ctzll(coop);
+      coop &= coop - 1;
+      const uintptr_t xa = ((uintptr_t)__shfl((uint32_t)(ad0 >> 32), L) << 32) | __shfl((uint32_t)ad0, L);
+      const uintptr_t ta = ((uintptr_t)__shfl((uint32_t)(ad2 >> 32), L) << 32) | __shfl((uint32_t)ad2, L);
+      uint32_t run = 0;
+      while (true) {
+        uint8_t xc = 0, tc = 0;
+        const uint4 xv = ldu16(xa + run + 16 * lane), tv = ldu16(ta + run + 16 * lane);
+        const uint32_t m = diff16(xv, tv, xc, tc);
+        const uint64_t mis = __ballot(m < 16);
+        if (STATS && lane == 0) atomicAdd(&sc[25], 1ull);
+        if (mis) {
+          const uint32_t f = (uint32_t)__builtin_ctzll(mis);
+          const uint32_t mm = (uint32_t)__shfl((int)m, f);
+          const uint32_t cc = (uint32_t)__shfl((int)((uint32_t)xc | ((uint32_t)tc << 8)), f);
+          if (lane == L) {
+            len += run + 16 * f + mm;
+            smaller = (int8_t)(uint8_t)cc > (int8_t)(uint8_t)(cc >> 8);  // FN:55
+            post_ext();
+          }
+          break;
+        }
+        run += 1024;
+      }
+    }
+  }
+  if (STATS) {
+    __syncthreads();
+    if (threadIdx.x < 32) atomicAdd(&A.stats[threadIdx.x], sc[threadIdx.x]);
+  }
+}
+
+void launch_ms_walk2(const DevRef& R, const uint8_t* text, const uint64_t* docOff, const Chunk* chunks,
+                     uint32_t nchunks, uint32_t* nextChunk, const Pool& pool, uint32_t* chunkCount,
+                     uint32_t lanes, unsigned long long* stats, hipStream_t st) {
+  if (!nchunks) return;
+  Walk2Args A{R, text, docOff, chunks, nchunks, nextChunk, pool, chunkCount, stats};
+  const uint32_t blocks = (std::min<uint32_t>(lanes, nchunks) + 255) / 256;
+  if (stats) hipLaunchKernelGGL(k_ms_walk2<true>, dim3(blocks), dim3(256), 0, st, A);
+  else hipLaunchKernelGGL(k_ms_walk2<false>, dim3(blocks), dim3(256), 0, st, A);
+}
+
+}  // namespace cmsbwt
