@@ -252,6 +252,15 @@ struct Engine {
     HIPCHK(rocprim::radix_sort_keys(nullptr, b, kin, kout, (size_t)n, 0u, (unsigned)bits, st));
     HIPCHK(rocprim::radix_sort_keys(scratch(b), b, kin, kout, (size_t)n, 0u, (unsigned)bits, st));
   }
+  uint32_t max_u32(const uint32_t* in, uint64_t n) {
+    if (!n) return 0;
+    DBuf<uint32_t> out;
+    out.alloc(1);
+    size_t b = 0;
+    HIPCHK(rocprim::reduce(nullptr, b, in, out.p, 0u, (size_t)n, rocprim::maximum<uint32_t>(), st));
+    HIPCHK(rocprim::reduce(scratch(b), b, in, out.p, 0u, (size_t)n, rocprim::maximum<uint32_t>(), st));
+    return read1(out.p);
+  }
   uint32_t select_flagged(const uint32_t* in, const uint32_t* flags, uint32_t* out, uint32_t n) {
     if (!n) return 0;
     DBuf<uint32_t> cnt;
@@ -457,8 +466,8 @@ struct Engine {
 
   uint32_t chunk_size() const {
     if (const char* e = getenv("CMSBWT_CHUNK")) return (uint32_t)std::max(64L, atol(e));
-    if (!walk_v1()) {  // queue-fed: ~4 chunks per lane
-      uint64_t c = chars / ((uint64_t)walk_lanes() * 4);
+    if (!walk_v1()) {  // queue-fed: ~2 chunks per lane (measured best at 8-16 K)
+      uint64_t c = chars / ((uint64_t)walk_lanes() * 2);
       return (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(16384, c));
     }
     uint64_t c = chars / (256ull * 64 * 64);
@@ -632,19 +641,30 @@ struct Engine {
     HeadsSoA h = heads();
 
     // ---- grouping: perm sorted by (pos, len, isaNext, idx)   FN:1387-1416
+    const int bL = bits_for(max_u32(hLen.p, H));
+    const bool packed = 2 * bN + bL <= 64 && !env_u32("CMSBWT_GROUP3", 0);
     DBuf<uint32_t> perm, perm2, key, key2;
     perm.alloc(H); perm2.alloc(H); key.alloc(H); key2.alloc(H);
+    DBuf<unsigned long long> gk, gk2;
     mk_iota(perm.p, H, st);
-    mk_gather(hIsa.p, perm.p, key.p, H, st);
-    sort_pairs(key.p, key2.p, perm.p, perm2.p, H, bN);
-    mk_gather(hLen.p, perm2.p, key.p, H, st);
-    sort_pairs(key.p, key2.p, perm2.p, perm.p, H, 32);
-    mk_gather(hPos.p, perm.p, key.p, H, st);
-    sort_pairs(key.p, key2.p, perm.p, perm2.p, H, bN);
+    if (packed) {  // one sort on the composite key
+      gk.alloc(H); gk2.alloc(H);
+      mk_group_key(h, H, bN, bL, gk.p, st);
+      sort_pairs(gk.p, gk2.p, perm.p, perm2.p, H, 2 * bN + bL);
+      gk.release();
+    } else {       // LSD: isaNext, len, pos
+      mk_gather(hIsa.p, perm.p, key.p, H, st);
+      sort_pairs(key.p, key2.p, perm.p, perm2.p, H, bN);
+      mk_gather(hLen.p, perm2.p, key.p, H, st);
+      sort_pairs(key.p, key2.p, perm2.p, perm.p, H, bL);
+      mk_gather(hPos.p, perm.p, key.p, H, st);
+      sort_pairs(key.p, key2.p, perm.p, perm2.p, H, bN);
+    }
     perm.release();
     DBuf<uint32_t>& P = perm2;  // sorted members
     // items
-    mk_item_flags(P.p, h, key.p, H, st);
+    if (packed) mk_item_flags64(gk2.p, key.p, H, st);
+    else mk_item_flags(P.p, h, key.p, H, st);
     inscan(key.p, key2.p, H, rocprim::plus<uint32_t>());
     K = read1(key2.p + (H - 1));
     DBuf<uint32_t> aPos, aLen, aIsa, aUntil, aCount, aFirst, aSlot;
@@ -652,7 +672,9 @@ struct Engine {
     aPos.alloc(K); aLen.alloc(K); aIsa.alloc(K); aUntil.alloc(K); aCount.alloc(K); aFirst.alloc(K);
     aSmall.alloc(K);
     ItemsSoA A0{aPos.p, aLen.p, aIsa.p, aSmall.p, aUntil.p, aCount.p, aFirst.p, nullptr, nullptr, nullptr};
-    mk_item_fill(P.p, key.p, key2.p, h, H, A0, st);
+    if (packed) mk_item_fill64(gk2.p, P.p, key.p, key2.p, h, H, bN, bL, A0, st);
+    else mk_item_fill(P.p, key.p, key2.p, h, H, A0, st);
+    gk2.release();
     mk_item_count(aFirst.p, aCount.p, K, H, st);
     key.release();
     key2.release();

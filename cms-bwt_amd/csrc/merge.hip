@@ -44,6 +44,35 @@ __global__ void k_item_flags(const uint32_t* __restrict__ perm, const uint32_t* 
   flag[k] = (pos[a] != pos[b] || len[a] != len[b] || isa[a] != isa[b]) ? 1u : 0u;
 }
 
+// Composite grouping key (pos, len, isaNext) in one 64-bit word when the
+// fields fit: one stable radix sort replaces three, and item boundaries and
+// item fields come from the sorted keys (no per-head gathers).
+__global__ void k_group_key(const HeadsSoA h, uint64_t H, int bN, int bL, unsigned long long* __restrict__ key) {
+  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= H) return;
+  key[i] = ((unsigned long long)h.pos[i] << (bN + bL)) | ((unsigned long long)h.len[i] << bN) | h.isa[i];
+}
+__global__ void k_item_flags64(const unsigned long long* __restrict__ key, uint32_t* __restrict__ flag, uint64_t H) {
+  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= H) return;
+  flag[k] = (k == 0 || key[k] != key[k - 1]) ? 1u : 0u;
+}
+__global__ void k_item_fill64(const unsigned long long* __restrict__ key, const uint32_t* __restrict__ perm,
+                              const uint32_t* __restrict__ flag, const uint32_t* __restrict__ itemIncl, HeadsSoA h,
+                              uint64_t H, int bN, int bL, ItemsSoA it) {
+  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= H || !flag[k]) return;
+  const uint32_t q = itemIncl[k] - 1;
+  const uint32_t a = perm[k];
+  const unsigned long long v = key[k];
+  it.pos[q] = (uint32_t)(v >> (bN + bL));
+  it.len[q] = (uint32_t)((v >> bN) & ((1ull << bL) - 1));
+  it.isa[q] = (uint32_t)(v & ((1ull << bN) - 1));
+  it.smaller[q] = h.smaller[a];
+  it.until[q] = h.tonext[a];
+  it.first[q] = (uint32_t)k;
+}
+
 // One item per flagged position; the first member (smallest idx) supplies
 // untilNext and smaller, as the first std::map insertion does (FN:1406-1413).
 __global__ void k_item_fill(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ flag,
@@ -691,6 +720,16 @@ void mk_item_flags(const uint32_t* perm, const HeadsSoA& h, uint32_t* flag, uint
 void mk_item_fill(const uint32_t* perm, const uint32_t* flag, const uint32_t* incl, const HeadsSoA& h,
                   uint64_t H, const ItemsSoA& it, hipStream_t st) {
   if (H) hipLaunchKernelGGL(k_item_fill, g1(H), dim3(256), 0, st, perm, flag, incl, h, H, it);
+}
+void mk_group_key(const HeadsSoA& h, uint64_t H, int bN, int bL, unsigned long long* key, hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_group_key, g1(H), dim3(256), 0, st, h, H, bN, bL, key);
+}
+void mk_item_flags64(const unsigned long long* key, uint32_t* flag, uint64_t H, hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_item_flags64, g1(H), dim3(256), 0, st, key, flag, H);
+}
+void mk_item_fill64(const unsigned long long* key, const uint32_t* perm, const uint32_t* flag, const uint32_t* incl,
+                    const HeadsSoA& h, uint64_t H, int bN, int bL, const ItemsSoA& it, hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_item_fill64, g1(H), dim3(256), 0, st, key, perm, flag, incl, h, H, bN, bL, it);
 }
 void mk_item_count(const uint32_t* first, uint32_t* count, uint32_t K, uint32_t H, hipStream_t st) {
   if (K) hipLaunchKernelGGL(k_item_count, g1(K), dim3(256), 0, st, first, count, K, H);

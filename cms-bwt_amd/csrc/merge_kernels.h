@@ -26,6 +26,10 @@ void mk_gather(const uint32_t* src, const uint32_t* perm, uint32_t* dst, uint64_
 void mk_item_key(const uint32_t* len, const uint8_t* sm, const uint32_t* perm, uint32_t* key, uint64_t n,
                  hipStream_t st);
 void mk_item_flags(const uint32_t* perm, const HeadsSoA& h, uint32_t* flag, uint64_t H, hipStream_t st);
+void mk_group_key(const HeadsSoA& h, uint64_t H, int bN, int bL, unsigned long long* key, hipStream_t st);
+void mk_item_flags64(const unsigned long long* key, uint32_t* flag, uint64_t H, hipStream_t st);
+void mk_item_fill64(const unsigned long long* key, const uint32_t* perm, const uint32_t* flag, const uint32_t* incl,
+                    const HeadsSoA& h, uint64_t H, int bN, int bL, const ItemsSoA& it, hipStream_t st);
 void mk_item_fill(const uint32_t* perm, const uint32_t* flag, const uint32_t* incl, const HeadsSoA& h,
                   uint64_t H, const ItemsSoA& it, hipStream_t st);
 void mk_item_count(const uint32_t* first, uint32_t* count, uint32_t K, uint32_t H, hipStream_t st);
