@@ -32,6 +32,9 @@ struct DevRef {
   const int2* kmer;
   const uint8_t* kmap;  // 256 entries, 0xff = byte absent from the reference text
   uint32_t kmerK, kmerB;
+  // Child table (walk only): ld[k] = min(LCP[k], 2^24-1) << 8 | x[SA[k]+LCP[k]]
+  // for k >= 1; nullptr disables the small-interval extension.
+  const uint32_t* ld;
 };
 
 // One restart chunk of the MS walk: positions [a, b) of document `doc`.

@@ -160,6 +160,7 @@ struct Engine {
   DBuf<int32_t> dsa, dlcp, dplcp;
   DBuf<uint32_t> disa;
   DBuf<int2> dkmer;
+  DBuf<uint32_t> dld;
   DBuf<uint8_t> dkmap;
   DevRef R{};
 
@@ -335,6 +336,7 @@ struct Engine {
     R.bwt = dbwt.p;
     R.n = n;
     build_kmer_table();
+    build_child_table();
     sync();
     refLoaded = true;
     stats.n = n;
@@ -392,6 +394,29 @@ struct Engine {
     R.kmap = dkmap.p;
     R.kmerK = K;
     R.kmerB = B;
+  }
+
+  // Child table of the uniform-step walk: ld[k] packs LCP[k] (clipped to 24
+  // bits) with D[k] = x[SA[k] + LCP[k]], the first character in which suffix
+  // SA[k] differs from SA[k-1].  Inside an lcp-interval of depth off, the
+  // children start at lb and at every k with LCP[k] == off, and D[k] is the
+  // child's character, so one character of computeMSFactorAt over a small
+  // interval needs one window of ld instead of two binary searches.
+  void build_child_table() {
+    R.ld = nullptr;
+    if (!env_u32("CMSBWT_EXT8", 1)) return;
+    const uint32_t n = hix.n;
+    std::vector<uint32_t> ld((size_t)n + 16, 0);
+    for (uint32_t k = 1; k < n; k++) {
+      const uint32_t l = (uint32_t)std::max<int32_t>(hix.lcp[k], 0);
+      const uint64_t at = (uint64_t)(uint32_t)hix.sa[k] + l;
+      const uint8_t d = at < n ? (uint8_t)hix.x[at] : 0;
+      ld[k] = (std::min<uint32_t>(l, 0xffffffu) << 8) | d;
+    }
+    dld.alloc((uint64_t)n + 16);
+    HIPCHK(hipMemcpyAsync(dld.p, ld.data(), ((size_t)n + 16) * 4, hipMemcpyHostToDevice, st));
+    sync();  // `ld` is pageable
+    R.ld = dld.p;
   }
 
   // =====================================================================
@@ -466,8 +491,8 @@ struct Engine {
 
   uint32_t chunk_size() const {
     if (const char* e = getenv("CMSBWT_CHUNK")) return (uint32_t)std::max(64L, atol(e));
-    if (!walk_v1()) {  // queue-fed: ~2 chunks per lane (measured best at 8-16 K)
-      uint64_t c = chars / ((uint64_t)walk_lanes() * 2);
+    if (!walk_v1()) {  // queue-fed: ~1 chunk per lane (restarts cost; measured best at 16 K)
+      uint64_t c = chars / (uint64_t)walk_lanes();
       return (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(16384, c));
     }
     uint64_t c = chars / (256ull * 64 * 64);
@@ -487,7 +512,7 @@ struct Engine {
     DBuf<uint32_t> chunkCount, used, nextChunk;
     chunkCount.alloc(nch);
     used.alloc(1);
-    nextChunk.alloc(1);
+    nextChunk.alloc(16 * 8);
     const bool v1 = walk_v1();
     DBuf<unsigned long long> w2stats;  // CMSBWT_W2_STATS=1: step counts of the uniform-step walk
     if (!v1 && env_u32("CMSBWT_W2_STATS", 0)) {
@@ -509,8 +534,8 @@ struct Engine {
       Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
       HIPCHK(hipEventRecord(ev0, st));
       if (v1) launch_ms_walk(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.laneChunk.p, pool, chunkCount.p, st);
-      else launch_ms_walk2(R, dtext.p, ddoc.p, plan.dch.p, nch, nextChunk.p, pool, chunkCount.p, walk_lanes(),
-                           w2stats.p, st);
+      else launch_ms_walk2(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.bandOrder.p, plan.bandStart.p, plan.nbands,
+                           nextChunk.p, pool, chunkCount.p, walk_lanes(), w2stats.p, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(ev1, st));
       usedBlocks = read1(used.p);
@@ -522,8 +547,9 @@ struct Engine {
     }
     if (w2stats.p) {
       static const char* names[32] = {"done", "next", "bs_text", "bs_sa", "bs_x", "fail_sa", "lce_sa", "lce",
-                                       "skip1", "gallop", "skipbs", "isa1", "con1", "con2", "adj", "lce_coop",
-                                       "kmer_text", "kmer_tab", "scan0", "scan1", "scan2", "scan3", "-", "-", "wave_steps",
+                                       "skip1", "gallop", "skipbs", "isa1", "con1", "con2", "adj", "kmer_text",
+                                       "kmer_tab", "ext_a", "ext_b", "lce_coop", "c_adj0", "c_adv", "c_post",
+                                       "c_char", "-", "-", "scan0", "scan1", "scan2", "scan3", "wave_steps",
                                        "coop_steps"};
       std::vector<unsigned long long> h(32);
       HIPCHK(hipMemcpy(h.data(), w2stats.p, 32 * 8, hipMemcpyDeviceToHost));
@@ -579,6 +605,8 @@ struct Engine {
     uint32_t C = 0, nch = 0;
     DBuf<Chunk> dch;
     DBuf<uint32_t> dLast, laneChunk;
+    DBuf<uint32_t> bandOrder, bandStart;  // uniform-step walk: chunks grouped by offset band
+    uint32_t nbands = 1;
   } plan;
 
   void build_plan(uint32_t C) {
@@ -620,6 +648,24 @@ struct Engine {
     HIPCHK(hipMemcpyAsync(plan.dLast.p, lastChunk.data(), ndocs * 4, hipMemcpyHostToDevice, st));
     plan.laneChunk.alloc(nch);
     HIPCHK(hipMemcpyAsync(plan.laneChunk.p, order.data(), nch * 4, hipMemcpyHostToDevice, st));
+    // Offset bands for the uniform-step walk: band = 8 * a / docLen, chunks of
+    // a band in document order.  Copies of the reference then keep an XCD's
+    // x / ISA / PLCP accesses inside one eighth of the reference.
+    const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(8, env_u32("CMSBWT_BANDS", 8)));
+    std::vector<uint32_t> bandCnt(nb + 1, 0), bandOf(nch);
+    for (uint32_t c = 0; c < nch; c++) {
+      const uint64_t L = hdoc[chunks[c].doc + 1] - hdoc[chunks[c].doc] - 1;
+      bandOf[c] = L ? (uint32_t)std::min<uint64_t>(nb - 1, (uint64_t)chunks[c].a * nb / L) : 0;
+      bandCnt[bandOf[c] + 1]++;
+    }
+    for (uint32_t k = 0; k < nb; k++) bandCnt[k + 1] += bandCnt[k];
+    std::vector<uint32_t> bandOrd(nch), fillp(bandCnt.begin(), bandCnt.end() - 1);
+    for (uint32_t c = 0; c < nch; c++) bandOrd[fillp[bandOf[c]]++] = c;
+    plan.bandOrder.alloc(nch);
+    HIPCHK(hipMemcpyAsync(plan.bandOrder.p, bandOrd.data(), nch * 4, hipMemcpyHostToDevice, st));
+    plan.bandStart.alloc(nb + 1);
+    HIPCHK(hipMemcpyAsync(plan.bandStart.p, bandCnt.data(), (nb + 1) * 4, hipMemcpyHostToDevice, st));
+    plan.nbands = nb;
     sync();
     plan.C = C;
     plan.nch = nch;

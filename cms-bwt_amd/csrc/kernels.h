@@ -42,10 +42,13 @@ void launch_chunk_with_end(const Chunk* chunks, const uint32_t* chunkCount, uint
 void launch_scatter_heads(const Pool& pool, uint32_t blocksUsed, const uint32_t* chunkCount,
                           const unsigned long long* chunkBase, const HeadsSoA& h, const Chunk* chunks,
                           const uint8_t* text, const uint64_t* docOff, hipStream_t st);
-// ms_walk2.hip: uniform-step walk; `lanes` resident lanes pull chunks from *nextChunk (zeroed)
+// ms_walk2.hip: uniform-step walk; `lanes` resident lanes pull chunks from
+// per-band queues: order[bandStart[k] ..) are band k's chunk ids, nextChunk[16k]
+// its (zeroed) counter
 void launch_ms_walk2(const DevRef& R, const uint8_t* text, const uint64_t* docOff, const Chunk* chunks,
-                     uint32_t nchunks, uint32_t* nextChunk, const Pool& pool, uint32_t* chunkCount,
-                     uint32_t lanes, unsigned long long* stats, hipStream_t st);
+                     uint32_t nchunks, const uint32_t* order, const uint32_t* bandStart, uint32_t nbands,
+                     uint32_t* nextChunk, const Pool& pool, uint32_t* chunkCount, uint32_t lanes,
+                     unsigned long long* stats, hipStream_t st);
 void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t ndocs,
                         const uint32_t* docLastChunk, const uint32_t* chunkCount,
                         const unsigned long long* chunkBase, uint32_t n, const HeadsSoA& h, uint32_t* docEndIdx,

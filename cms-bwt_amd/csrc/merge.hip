@@ -695,10 +695,11 @@ __global__ void k_count_distinct(const uint32_t* __restrict__ v, uint32_t K, uns
   __shared__ unsigned int acc;
   if (threadIdx.x == 0) acc = 0;
   __syncthreads();
-  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  bool first = q < K && (q == 0 || v[q] != v[q - 1]);
-  unsigned long long b = __ballot(first);
-  if ((threadIdx.x & 63) == 0 && b) atomicAdd(&acc, (unsigned int)__popcll(b));
+  uint32_t c = 0;  // grid-stride: one global atomic per block, few blocks
+  for (uint64_t q = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; q < K; q += (uint64_t)gridDim.x * blockDim.x)
+    c += (q == 0 || v[q] != v[q - 1]) ? 1u : 0u;
+  for (int o = 32; o > 0; o >>= 1) c += __shfl_xor(c, o);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(&acc, c);
   __syncthreads();
   if (threadIdx.x == 0 && acc) atomicAdd(out, (unsigned long long)acc);
 }
@@ -821,7 +822,7 @@ void mk_counter_win(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t
   else hipLaunchKernelGGL(k_counter_win<false>, dim3(nw), dim3(512), 0, st, A);
 }
 void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st) {
-  if (K) hipLaunchKernelGGL(k_count_distinct, g1(K), dim3(256), 0, st, v, K, out);
+  if (K) hipLaunchKernelGGL(k_count_distinct, dim3(std::min<unsigned>(2048, g1(K).x)), dim3(256), 0, st, v, K, out);
 }
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st) {
   hipLaunchKernelGGL(k_bucket, g1(n), dim3(256), 0, st, countIncl, hasHead, n, bucket);

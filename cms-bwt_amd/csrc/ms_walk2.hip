@@ -3,36 +3,40 @@
 // Same semantics as k_ms_walk (FN:45-149, FN:1151-1212, rmq_tree.h:184-225),
 // restructured for SIMT.  In the per-lane walk the nested loops (binary
 // searches, LCE, PLCP skip, PSV/NSV scans) make the 64 lanes of a wave issue
-// their dependent loads in separate, mostly-inactive instructions.  Here
-// every iteration each lane issues up to four 16-byte loads (slots 0/1 = the
-// aligned block holding address A and the next one, slots 2/3 the same for
-// address B; the LCE loads 16 unaligned bytes at A and B) and advances its own state machine by exactly one step, so one memory
-// latency moves every lane forward.  Lanes pull restart chunks from a global
-// queue (one atomic per wave) until it is empty.
+// their dependent loads in separate, mostly-inactive instructions.  Here each
+// iteration issues one round of loads for all lanes (a lane loads up to two
+// addresses A and B, as a byte, a dword or 16/32 bytes) and every lane advances
+// its own state machine by exactly one memory step; the work between two
+// loads (head record, contraction set-up, next character) runs as "compute
+// phases", each emitted once.  Lanes pull restart chunks from per-band queues.
 //
-//   phase     loads                          next
-//   BS_TEXT   t[j], SA[first probe]          BS_X          (FN:94-149)
-//   BS_SA     SA[m]                          BS_X
-//   BS_X      x[SA[m]+off]                   BS_SA / result
-//   FAIL_SA   SA[insertion point]            head record   (FN:65-76)
-//   LCE_SA    SA[lb]                         LCE           (FN:52-62)
-//   LCE       16 B of x and of the text      LCE_COOP / head record
-//   LCE_COOP  (no lane load) the whole wave compares 1 KiB per step of one
-//             lane's long extension with coalesced loads, lane by lane
-//   SKIP1     PLCP[pos+1], PLCP[T-7..T]      ISA1 / GALLOP (FN:1176-1185)
-//   GALLOP/SKIPBS  one PLCP probe            ISA1
-//   ISA1      ISA[pos+1]                     ADJ           (FN:1187)
-//   CON1/CON2 SA[lb],SA[rb] / ISA[..+1]      ADJ / root    (FN:34-43)
-//   ADJ       8 entries for PSV + 8 for NSV  ADJ / next position (FN:11-25)
+//   load phase  loads                          next
+//   BS_TEXT     t[j], SA[first probe]          BS_X          (FN:94-149)
+//   BS_SA       SA[m]                          BS_X
+//   BS_X        x[SA[m]+off]                   BS_SA / FAIL_SA / CHAR
+//   FAIL_SA     SA[insertion point]            POST          (FN:65-76)
+//   LCE_SA      SA[lb]                         LCE           (FN:52-62)
+//   LCE         16 B of x and of the text      POST / LCE_COOP
+//   LCE_COOP    (none) the whole wave compares 1 KiB per step of one lane's
+//               long extension with coalesced loads, lane by lane -> POST
+//   SKIP1       PLCP[pos+1], PLCP[T-7..T]      ISA1 / GALLOP (FN:1176-1185)
+//   GALLOP/SKIPBS  one PLCP probe              ISA1
+//   ISA1        ISA[pos+1]                     ADJ0          (FN:1187)
+//   CON1/CON2   SA[lb],SA[rb] / ISA[..+1]      ADJ0 / ADV    (FN:34-43)
+//   ADJ         8 LCP entries for PSV + 8 for NSV  ADJ / ADV (FN:11-25)
 //   KMER_TEXT/KMER_TAB  restart: K text bytes, then the K-mer's SA interval
-//             (= the state after K matched characters from the root)
+//               (= the state after K matched characters from the root)
+//   EXT_A/EXT_B one character over an interval of <= 8 suffixes without a
+//               binary search: its children at depth off start where LCP ==
+//               off, with first characters D (= x[SA[k]+LCP[k]]) and x[SA[lb]+off]
+//   compute phases (no load): ADJ0 (start adjustInterval), ADV (next
+//   position, FN:1195-1196), POST (head record FN:1154-1171 and the
+//   contraction choice FN:1175-1194), CHAR (next character, FN:45-62).
 //
-// Registers: the phase-local variables share ten 32-bit slots (u0..u9).
-// Cost model (measured): the walk is bound by per-lane divergent load
-// instructions (each a separate cache-line request), not by latency -- 5..7
-// waves per SIMD time the same, and widening each lane's window to 64 B with
-// more 16-B loads made it 2.6x slower.  Hence: few loads per step, and the
-// long extensions (about one per SNP, ~1000 bytes) moved to coalesced
+// Cost model (measured on the benchmark): neither latency (2..6 waves per
+// SIMD time the same) nor L2 locality (per-XCD offset bands change nothing)
+// bounds the walk; the issued instructions per step do.  Hence few, narrow
+// loads, compute written once, and long extensions moved to coalesced
 // wave-wide compares.
 #include "device_common.h"
 #include "kernels.h"
@@ -44,6 +48,7 @@ namespace {
 enum : uint32_t {
   PH_DONE = 0,
   PH_NEXT,  // needs a new chunk (no load)
+  // load phases
   PH_BS_TEXT,
   PH_BS_SA,
   PH_BS_X,
@@ -57,9 +62,17 @@ enum : uint32_t {
   PH_CON1,
   PH_CON2,
   PH_ADJ,
-  PH_LCE_COOP,  // long extension, served by the whole wave (no lane load)
-  PH_KMER_TEXT, // restart: K text bytes
-  PH_KMER_TAB,  // restart: SA interval of the K-mer
+  PH_KMER_TEXT,
+  PH_KMER_TAB,
+  PH_EXT_A,
+  PH_EXT_B,
+  PH_LCE_COOP,  // served by the whole wave (no lane load)
+  // compute phases
+  PC_ADJ0,
+  PC_ADV,
+  PC_POST,
+  PC_CHAR,
+  PH_COUNT
 };
 
 // Loads through global-address-space pointers (global_load_*, not flat), each
@@ -75,13 +88,14 @@ __device__ __forceinline__ uint4 ldu16(uintptr_t a) {
 }
 // slot loads of one step (`use` bits)
 enum : uint32_t {
-  U0B = 1,   // byte at A
-  U0D = 2,   // dword at A
-  U0Q = 4,   // 16 B at A
-  U1Q = 8,   // 16 B at A + 16
-  U2D = 16,  // dword at B
-  U2Q = 32,  // 16 B at B
-  U3Q = 64,  // 16 B at B + 16
+  U0B = 1,    // byte at A
+  U0D = 2,    // dword at A
+  U0Q = 4,    // 16 B at A
+  U1Q = 8,    // 16 B at A + 16
+  U2D = 16,   // dword at B
+  U2Q = 32,   // 16 B at B
+  U3Q = 64,   // 16 B at B + 16
+  U2B = 128,  // byte at B
 };
 // First differing byte of two 16-byte strings: 16 if equal.
 __device__ __forceinline__ uint32_t diff16(const uint4& x, const uint4& t, uint8_t& xc, uint8_t& tc) {
@@ -96,20 +110,14 @@ __device__ __forceinline__ uint32_t diff16(const uint4& x, const uint4& t, uint8
   return (d0 ? 0 : 8) + bit / 8;
 }
 
-__device__ __forceinline__ uint32_t lvl_len(const DevRef& R, uint32_t L) {
-  uint32_t v = R.lvlLen[0];
-#pragma unroll
-  for (uint32_t k = 1; k < (uint32_t)kMaxLevels; k++)
-    if (L == k) v = R.lvlLen[k];
-  return v;
-}
-__device__ __forceinline__ uint32_t lvl_off(const DevRef& R, uint32_t L) {
-  uint32_t v = R.lvlOff[0];
-#pragma unroll
-  for (uint32_t k = 1; k < (uint32_t)kMaxLevels; k++)
-    if (L == k) v = R.lvlOff[k];
-  return v;
-}
+// Level geometry of the LCP block minima, staged in LDS.
+struct Lv {
+  const uint32_t* len;  // lvlLen
+  const uint32_t* off;  // lvlOff (entries from lcp)
+  int nlvl;
+  int32_t n;
+  const int32_t* lcp;
+};
 
 // ---- PSV (UP=false) / NSV (UP=true) as a state machine over 8-entry windows
 // (rmq_tree.h:184-225).  State: cur/lim = remaining range of the current
@@ -125,17 +133,20 @@ __device__ __forceinline__ int32_t window_base(int32_t cur) {
 }
 
 template <bool UP>
-__device__ __forceinline__ uintptr_t scan_addr(const DevRef& R, int32_t cur, uint32_t ls) {
+__device__ __forceinline__ uintptr_t scan_addr(const Lv& V, int32_t cur, uint32_t ls) {
   const uint32_t stg = ls >> 4;
-  const uint32_t off = (stg == 0 || stg == 3) ? 0u : lvl_off(R, ls & 15);
-  return (uintptr_t)(R.lcp + off + (uint32_t)window_base<UP>(cur));
+  const uint32_t off = (stg == 0 || stg == 3) ? 0u : V.off[ls & 15];
+  return (uintptr_t)(V.lcp + off + (uint32_t)window_base<UP>(cur));
 }
 
-// Stage transitions that need no memory access.
+// Stage transitions that need no memory access.  At most two per call (the
+// usual case needs one); a range left empty is seen as exhausted by the next
+// scan_step, which settles again, so the walk stays correct with fewer
+// unrolled copies of this code.
 template <bool UP>
-__device__ __forceinline__ void scan_settle(const DevRef& R, int32_t& cur, int32_t& lim, int32_t& res,
-                                            int32_t& idx, uint32_t& ls) {
-  for (int guard = 0; guard < kMaxLevels + 2; guard++) {
+__device__ __forceinline__ void scan_settle(const Lv& V, int32_t& cur, int32_t& lim, int32_t& res, int32_t& idx,
+                                            uint32_t& ls) {
+  for (int guard = 0; guard < 2; guard++) {
     uint32_t stg = ls >> 4, L = ls & 15;
     if (stg == 4) return;
     if (UP ? (cur <= lim) : (cur >= lim)) return;  // range left: needs a load
@@ -143,17 +154,17 @@ __device__ __forceinline__ void scan_settle(const DevRef& R, int32_t& cur, int32
       stg = 1;
       L = 0;
     } else if (stg == 1) {
-      const int32_t len = (int32_t)lvl_len(R, L);
+      const int32_t len = (int32_t)V.len[L];
       const bool top = UP ? (min(idx | 63, len - 1) >= len - 1) : ((idx & ~63) == 0);
       idx >>= 6;
       L++;
-      if (top || (int)L >= R.nlvl) { res = -1; ls = kScanDone; return; }
+      if (top || (int)L >= V.nlvl) { res = -1; ls = kScanDone; return; }
     } else {  // a descent always finds (block minimum < ub); defensive
       res = -1;
       ls = kScanDone;
       return;
     }
-    const int32_t len = (int32_t)lvl_len(R, L);
+    const int32_t len = (int32_t)V.len[L];
     if (!UP) { cur = idx - 1; lim = idx & ~63; }
     else { cur = idx + 1; lim = min(idx | 63, len - 1); }
     ls = L | (stg << 4);
@@ -161,22 +172,20 @@ __device__ __forceinline__ void scan_settle(const DevRef& R, int32_t& cur, int32
 }
 
 template <bool UP>
-__device__ __forceinline__ void scan_start(const DevRef& R, int32_t i, int32_t& cur, int32_t& lim, int32_t& res,
+__device__ __forceinline__ void scan_start(const Lv& V, int32_t i, int32_t& cur, int32_t& lim, int32_t& res,
                                            int32_t& idx, uint32_t& ls) {
-  const int32_t n = (int32_t)R.n;
   res = -1;
-  if (UP && i >= n) { ls = kScanDone; return; }
+  if (UP && i >= V.n) { ls = kScanDone; return; }
   ls = 0;
   idx = i >> 6;
   cur = i;
-  lim = UP ? min(i | 63, n - 1) : (i & ~63);
-  scan_settle<UP>(R, cur, lim, res, idx, ls);
+  lim = UP ? min(i | 63, V.n - 1) : (i & ~63);
+  scan_settle<UP>(V, cur, lim, res, idx, ls);
 }
 
 template <bool UP>
-__device__ __forceinline__ void scan_step(const DevRef& R, const uint4& v0, const uint4& v1, int32_t ub,
-                                          int32_t& cur, int32_t& lim, int32_t& res, int32_t& idx, uint32_t& ls) {
-  const int32_t n = (int32_t)R.n;
+__device__ __forceinline__ void scan_step(const Lv& V, const uint4& v0, const uint4& v1, int32_t ub, int32_t& cur,
+                                          int32_t& lim, int32_t& res, int32_t& idx, uint32_t& ls) {
   const int32_t base = window_base<UP>(cur);
   const int32_t e[8] = {(int32_t)v0.x, (int32_t)v0.y, (int32_t)v0.z, (int32_t)v0.w,
                         (int32_t)v1.x, (int32_t)v1.y, (int32_t)v1.z, (int32_t)v1.w};
@@ -193,15 +202,15 @@ __device__ __forceinline__ void scan_step(const DevRef& R, const uint4& v0, cons
     // hit in a level array: descend into block k of the level below
     int32_t top;
     uint32_t nls;
-    if (L == 0) { top = n - 1; nls = 3u << 4; }
-    else { top = (int32_t)lvl_len(R, L - 1) - 1; nls = (L - 1) | (2u << 4); }
+    if (L == 0) { top = V.n - 1; nls = 3u << 4; }
+    else { top = (int32_t)V.len[L - 1] - 1; nls = (L - 1) | (2u << 4); }
     const int32_t lo = k * 64, hi = min(k * 64 + 63, top);
     if (UP) { cur = lo; lim = hi; } else { cur = hi; lim = lo; }
     ls = nls;
     return;
   }
   cur = UP ? base + 8 : base - 1;
-  scan_settle<UP>(R, cur, lim, res, idx, ls);
+  scan_settle<UP>(V, cur, lim, res, idx, ls);
 }
 
 }  // namespace
@@ -212,7 +221,10 @@ struct Walk2Args {
   const uint64_t* docOff;
   const Chunk* chunks;
   uint32_t nchunks;
-  uint32_t* nextChunk;
+  const uint32_t* order;      // chunk ids grouped by band
+  const uint32_t* bandStart;  // nbands + 1
+  uint32_t nbands;
+  uint32_t* nextChunk;        // one counter per band, 64 B apart (zeroed)
   Pool pool;
   uint32_t* chunkCount;
   unsigned long long* stats;  // STATS builds: per-phase lane-steps, wave-steps, ...
@@ -221,16 +233,24 @@ struct Walk2Args {
 #ifndef CMSBWT_W2_WAVES
 #define CMSBWT_W2_WAVES 6
 #endif
-// 6 waves/SIMD fit without spills (80 VGPRs); more waves spill (measured).
 template <bool STATS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CMSBWT_W2_WAVES, 8)))
 k_ms_walk2(Walk2Args A) {
   __shared__ unsigned long long sc[STATS ? 32 : 1];
   __shared__ uint8_t kmapL[256];
+  __shared__ uint32_t lvlL[2 * kMaxLevels];
   if (STATS && threadIdx.x < 32) sc[threadIdx.x] = 0;
   if (A.R.kmer) kmapL[threadIdx.x] = A.R.kmap[threadIdx.x];  // blockDim == 256
+  if (threadIdx.x == 0) {
+#pragma unroll
+    for (int k = 0; k < kMaxLevels; k++) {
+      lvlL[k] = A.R.lvlLen[k];
+      lvlL[kMaxLevels + k] = A.R.lvlOff[k];
+    }
+  }
   __syncthreads();
   const DevRef& R = A.R;
+  const Lv V{lvlL, lvlL + kMaxLevels, R.nlvl, (int32_t)R.n, R.lcp};
   const uint32_t n = R.n;
   const uintptr_t X = (uintptr_t)R.x;
   const uintptr_t SA = (uintptr_t)R.sa;
@@ -253,92 +273,21 @@ k_ms_walk2(Walk2Args A) {
   uint32_t u9 = 0;
   // binary search (BS_*): u0 = c | ansVal << 8 | ansSet << 16 | ubMode << 17,
   //   u1 = lo, u2 = hi (exclusive), u3 = probe, u5 = new lb while searching the right end
+  // EXT_*: u0 = the text character
   // skip (SKIP1/GALLOP/SKIPBS): u1 = lo, u2 = hi, u3 = probe, u4 = gallop step
-  // ADJ: PSV = (u0 cur, u1 lim, u2 res, u3 idx, u4 ls), NSV = (u5, u6, u7, u8, u9)
+  // ADJ0: u0 / u5 = the two ISA values;  ADJ: PSV = (u0 cur, u1 lim, u2 res,
+  //   u3 idx, u4 ls), NSV = (u5, u6, u7, u8, u9)
   // `len` doubles as `off` during an extension (FN:48: off starts at len).
 
-  auto begin_char = [&]() {  // next character of computeMSFactorAt at j = i + len
-    if (lb == rb) {
-      phase = PH_LCE_SA;
-      ad0 = SA + 4ull * (uint32_t)lb;
-      use = U0D;
-    } else {
-      phase = PH_BS_TEXT;
-      u1 = lb;
-      u2 = rb + 1;
-      u3 = (u1 + u2) >> 1;
-      u0 = 0;
-      ad0 = T + i + len;
-      ad2 = SA + 4ull * (uint32_t)u3;
-      use = U0B | U2D;
-    }
-  };
-  auto emit = [&]() {
-    if (fill == kPoolB) {
-      blk = atomicAdd(A.pool.used, 1u);
-      fill = 0;
-      if (blk < A.pool.capBlocks) { A.pool.blkChunk[blk] = cid; A.pool.blkSeq[blk] = seq; }
-      seq++;
-    }
-    if (blk < A.pool.capBlocks) {
-      HeadRec r;
-      r.start = i;
-      r.pos = pos;
-      r.len = len;
-      r.flags = smaller ? 1u : 0u;
-      A.pool.rec[(uint64_t)blk * kPoolB + fill] = r;
-    }
-    fill++;
-    count++;
-  };
-  auto advance = [&]() {
-    i++;
-    prevPos = pos;
-    if (i >= b) {
-      A.chunkCount[cid] = count;
-      phase = PH_NEXT;
-      use = 0;
-    } else {
-      begin_char();
-    }
-  };
-  auto adj_or_finish = [&]() {
-    if ((uint32_t)u4 == kScanDone && u9 == kScanDone) {
-      lb = u2 == -1 ? 0 : u2;
-      rb = u7 == -1 ? (int32_t)n - 1 : u7 - 1;
-      advance();
-    } else {
-      phase = PH_ADJ;
-      use = 0;
-      if ((uint32_t)u4 != kScanDone) { ad0 = scan_addr<false>(R, u0, (uint32_t)u4); use |= U0Q | U1Q; }
-      if (u9 != kScanDone) { ad2 = scan_addr<true>(R, u5, u9); use |= U2Q | U3Q; }
-    }
-  };
-  auto start_adj = [&](int32_t lo, int32_t hi) {  // adjustInterval (FN:11-25)
-    uint32_t ls0;
-    scan_start<false>(R, lo, u0, u1, u2, u3, ls0);
-    scan_start<true>(R, hi + 1, u5, u6, u7, u8, u9);
-    u4 = (int32_t)ls0;
-    adj_or_finish();
-  };
-  auto post_ext = [&]() {  // head test and record (FN:1154-1171), then contraction
-    if (i >= a && pos != prevPos + 1) emit();
-    len--;
-    if (lb == rb) {  // FN:1175-1189
-      phase = PH_SKIP1;
-      ad0 = P + 4ull * (pos + 1);
-      use = U0D;
-      if (len > 8) {
-        const uint64_t TT = (uint64_t)pos + 1 + len;
-        ad2 = P + 4ull * ((TT & ~3ull) - 4);
-        use = U0D | U2Q | U3Q;
-      }
-    } else {  // FN:1190-1194
-      phase = PH_CON1;
-      ad0 = SA + 4ull * (uint32_t)lb;
-      ad2 = SA + 4ull * (uint32_t)rb;
-      use = U0D | U2D;
-    }
+  auto begin_bs = [&]() {  // binary searches for the character at j = i + len
+    phase = PH_BS_TEXT;
+    u1 = lb;
+    u2 = rb + 1;
+    u3 = (u1 + u2) >> 1;
+    u0 = 0;
+    ad0 = T + i + len;
+    ad2 = SA + 4ull * (uint32_t)u3;
+    use = U0B | U2D;
   };
   auto skip_done = [&](uint32_t s) {
     i += s;
@@ -370,93 +319,152 @@ k_ms_walk2(Walk2Args A) {
       skip_done((uint32_t)u2);
     }
   };
-  // lower_bound / upper_bound driver: next probe or result
-  auto bs_next = [&]() {
-    while (true) {
-      if (u1 < u2) {
-        u3 = (u1 + u2) >> 1;
-        phase = PH_BS_SA;
-        ad0 = SA + 4ull * (uint32_t)u3;
-        use = U0D;
-        return;
-      }
-      const uint32_t f = (uint32_t)u0;
-      if (!(f & (1u << 17))) {  // lower bound done
-        if ((f & (1u << 16)) && ((f >> 8) & 0xff) == (f & 0xff)) {
-          u5 = u1;  // new lb; now the right end in [lb'+1, rb+1)
-          u0 = (int32_t)(f | (1u << 17));
-          u1 = u5 + 1;
-          u2 = rb + 1;
-          continue;
-        }
-        int32_t mm = u1;  // mismatch: insertion point (FN:65-76)
-        smaller = true;
-        if (mm == rb + 1) { mm = rb; smaller = false; }
-        phase = PH_FAIL_SA;
-        ad0 = SA + 4ull * (uint32_t)mm;
-        use = U0D;
-        return;
-      }
-      // upper bound done: interval [u5, u1 - 1], one more matched character
-      lb = u5;
-      rb = u1 - 1;
-      len++;
-      begin_char();
-      return;
+  auto set_adj_addr = [&]() {
+    use = 0;
+    if ((uint32_t)u4 != kScanDone) { ad0 = scan_addr<false>(V, u0, (uint32_t)u4); use |= U0Q | U1Q; }
+    if (u9 != kScanDone) { ad2 = scan_addr<true>(V, u5, u9); use |= U2Q | U3Q; }
+  };
+  auto adj_or_finish = [&]() {
+    if ((uint32_t)u4 == kScanDone && u9 == kScanDone) {
+      lb = u2 == -1 ? 0 : u2;
+      rb = u7 == -1 ? (int32_t)n - 1 : u7 - 1;
+      phase = PC_ADV;
+      use = 0;
+    } else {
+      phase = PH_ADJ;
+      set_adj_addr();
     }
   };
 
   while (true) {
-    // ---- refill lanes from the chunk queue (one atomic per wave)
-    const uint64_t need = __ballot(phase == PH_NEXT);
-    if (need) {
+    // ---- refill lanes from the chunk queues (one atomic per wave and band).
+    // Chunks are banded by their offset inside the document; blocks that
+    // share an XCD (equal blockIdx % 8 under round-robin placement) start on
+    // the same band.  Exhausted bands are stolen from in turn.
+    uint64_t need = __ballot(phase == PH_NEXT);
+    for (uint32_t s2 = 0; need && s2 < A.nbands; s2++) {
+      const uint32_t band = (blockIdx.x + s2) % A.nbands;
       const uint32_t first = (uint32_t)__builtin_ctzll(need);
+      const uint32_t bs0 = A.bandStart[band], bsz = A.bandStart[band + 1] - bs0;
       uint32_t base = 0;
-      if (lane == first) base = atomicAdd(A.nextChunk, (uint32_t)__popcll(need));
+      if (lane == first) base = atomicAdd(&A.nextChunk[16 * band], (uint32_t)__popcll(need));
       base = __shfl(base, first);
-      if (phase == PH_NEXT) {
-        const uint32_t my = base + (uint32_t)__popcll(need & ((1ull << lane) - 1));
-        if (my >= A.nchunks) {
-          phase = PH_DONE;
-          use = 0;
+      const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1));
+      const bool mine = phase == PH_NEXT && base < bsz && rank < bsz - base;
+      need &= ~__ballot(mine);
+      if (mine) {
+        cid = A.order[bs0 + base + rank];
+        const Chunk ch = A.chunks[cid];
+        T = (uintptr_t)(A.text + A.docOff[ch.doc]);
+        a = ch.a;
+        b = ch.b;
+        count = 0;
+        fill = kPoolB;
+        seq = 0;
+        i = a > 0 ? a - 1 : 0;
+        if (i >= b) {
+          A.chunkCount[cid] = 0;  // empty document: refills next iteration
         } else {
-          cid = my;
-          const Chunk ch = A.chunks[cid];
-          T = (uintptr_t)(A.text + A.docOff[ch.doc]);
-          a = ch.a;
-          b = ch.b;
-          count = 0;
-          fill = kPoolB;
-          seq = 0;
-          i = a > 0 ? a - 1 : 0;
-          if (i >= b) {
-            A.chunkCount[cid] = 0;  // empty document: stays PH_NEXT
+          len = 0;
+          pos = n - 1;
+          lb = 0;
+          rb = (int32_t)n - 1;
+          prevPos = 0xfffffffeu;  // prevPos + 1 never equals a position
+          smaller = false;
+          if (R.kmer) {
+            phase = PH_KMER_TEXT;
+            ad0 = T + i;
+            use = U0Q;
           } else {
-            len = 0;
-            pos = n - 1;
-            lb = 0;
-            rb = (int32_t)n - 1;
-            prevPos = 0xfffffffeu;  // prevPos + 1 never equals a position
-            smaller = false;
-            if (R.kmer) {
-              phase = PH_KMER_TEXT;
-              ad0 = T + i;
-              use = U0Q;
-            } else {
-              begin_char();
-            }
+            phase = PC_CHAR;
           }
         }
       }
     }
+    if (need && phase == PH_NEXT && ((need >> lane) & 1)) {  // every band is empty
+      phase = PH_DONE;
+      use = 0;
+    }
+
+    // ---- compute phases, in chain order (ADJ0 -> ADV -> CHAR; POST is terminal)
+    if (phase == PC_ADJ0) {  // adjustInterval(lo = u0, hi = u5, len) (FN:11-25)
+      const int32_t lo = u0, hi = u5;
+      uint32_t ls0;
+      scan_start<false>(V, lo, u0, u1, u2, u3, ls0);
+      scan_start<true>(V, hi + 1, u5, u6, u7, u8, u9);
+      u4 = (int32_t)ls0;
+      adj_or_finish();
+    }
+    if (phase == PC_ADV) {  // FN:1195-1196
+      i++;
+      prevPos = pos;
+      if (i >= b) {
+        A.chunkCount[cid] = count;
+        phase = PH_NEXT;
+        use = 0;
+      } else {
+        phase = PC_CHAR;
+      }
+    }
+    if (phase == PC_POST) {  // head test and record (FN:1154-1171), then contraction
+      if (i >= a && pos != prevPos + 1) {
+        if (fill == kPoolB) {
+          blk = atomicAdd(A.pool.used, 1u);
+          fill = 0;
+          if (blk < A.pool.capBlocks) { A.pool.blkChunk[blk] = cid; A.pool.blkSeq[blk] = seq; }
+          seq++;
+        }
+        if (blk < A.pool.capBlocks) {
+          HeadRec r;
+          r.start = i;
+          r.pos = pos;
+          r.len = len;
+          r.flags = smaller ? 1u : 0u;
+          A.pool.rec[(uint64_t)blk * kPoolB + fill] = r;
+        }
+        fill++;
+        count++;
+      }
+      len--;
+      if (lb == rb) {  // FN:1175-1189: skip, then adjustInterval(ISA[pos+1])
+        phase = PH_SKIP1;
+        ad0 = P + 4ull * (pos + 1);
+        use = U0D;
+        if (len > 8) {
+          const uint64_t TT = (uint64_t)pos + 1 + len;
+          ad2 = P + 4ull * ((TT & ~3ull) - 4);
+          use = U0D | U2Q | U3Q;
+        }
+      } else {  // FN:1190-1194: contractLeft
+        phase = PH_CON1;
+        ad0 = SA + 4ull * (uint32_t)lb;
+        ad2 = SA + 4ull * (uint32_t)rb;
+        use = U0D | U2D;
+      }
+    }
+    if (phase == PC_CHAR) {  // next character of computeMSFactorAt at j = i + len
+      if (lb == rb) {
+        phase = PH_LCE_SA;
+        ad0 = SA + 4ull * (uint32_t)lb;
+        use = U0D;
+      } else if (R.ld && rb - lb < 8 && len < 0xffffffu) {
+        phase = PH_EXT_A;
+        ad0 = SA + 4ull * (uint32_t)lb;
+        ad2 = T + i + len;
+        use = U0D | U2B;
+      } else {
+        begin_bs();
+      }
+    }
+
     if (!__ballot(phase != PH_DONE)) break;
     if (STATS) {
       if (phase != PH_DONE) atomicAdd(&sc[phase], 1ull);
       if (phase == PH_ADJ) {
-        if ((uint32_t)u4 != kScanDone) atomicAdd(&sc[18 + ((uint32_t)u4 >> 4)], 1ull);
-        if (u9 != kScanDone) atomicAdd(&sc[18 + (u9 >> 4)], 1ull);
+        if ((uint32_t)u4 != kScanDone) atomicAdd(&sc[26 + ((uint32_t)u4 >> 4)], 1ull);
+        if (u9 != kScanDone) atomicAdd(&sc[26 + (u9 >> 4)], 1ull);
       }
-      if (lane == 0) atomicAdd(&sc[24], 1ull);
+      if (lane == 0) atomicAdd(&sc[30], 1ull);
     }
     // ---- one memory step
     uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0, v2 = v0, v3 = v0;
@@ -465,9 +473,10 @@ k_ms_walk2(Walk2Args A) {
     if (use & U0Q) v0 = ldu16(ad0);
     if (use & U1Q) v1 = ldu16(ad0 + 16);
     if (use & U2D) v2.x = ld4(ad2);
+    if (use & U2B) v2.x = ld1(ad2);
     if (use & U2Q) v2 = ldu16(ad2);
     if (use & U3Q) v3 = ldu16(ad2 + 16);
-    // ---- one state-machine step
+    // ---- one state-machine step (load phases)
     switch (phase) {
       case PH_BS_TEXT: {  // c = t[j]; the first probe's SA value is in slot 2
         u0 = (int32_t)v0.x;
@@ -492,12 +501,45 @@ k_ms_walk2(Walk2Args A) {
           if (v <= c) u1 = u3 + 1;
           else u2 = u3;
         }
-        bs_next();
+        // lower_bound / upper_bound driver: next probe or result
+        for (int g = 0; g < 2; g++) {
+          if (u1 < u2) {
+            u3 = (u1 + u2) >> 1;
+            phase = PH_BS_SA;
+            ad0 = SA + 4ull * (uint32_t)u3;
+            use = U0D;
+            break;
+          }
+          const uint32_t f2 = (uint32_t)u0;
+          if (!(f2 & (1u << 17))) {  // lower bound done
+            if ((f2 & (1u << 16)) && ((f2 >> 8) & 0xff) == (f2 & 0xff)) {
+              u5 = u1;  // new lb; now the right end in [lb'+1, rb+1)
+              u0 = (int32_t)(f2 | (1u << 17));
+              u1 = u5 + 1;
+              u2 = rb + 1;
+              continue;
+            }
+            int32_t mm = u1;  // mismatch: insertion point (FN:65-76)
+            smaller = true;
+            if (mm == rb + 1) { mm = rb; smaller = false; }
+            phase = PH_FAIL_SA;
+            ad0 = SA + 4ull * (uint32_t)mm;
+            use = U0D;
+            break;
+          }
+          // upper bound done: interval [u5, u1 - 1], one more matched character
+          lb = u5;
+          rb = u1 - 1;
+          len++;
+          phase = PC_CHAR;
+          use = 0;
+          break;
+        }
         break;
       }
       case PH_FAIL_SA: {
         pos = v0.x;
-        post_ext();
+        phase = PC_POST;
         break;
       }
       case PH_LCE_SA: {
@@ -514,14 +556,14 @@ k_ms_walk2(Walk2Args A) {
         if (m < 16) {
           len += m;
           smaller = (int8_t)xc > (int8_t)tc;  // FN:55, char compare
-          post_ext();
+          phase = PC_POST;
         } else {  // long extension: hand it to the wave
           len += 16;
           ad0 += 16;
           ad2 += 16;
           phase = PH_LCE_COOP;
-          use = 0;
         }
+        use = 0;
         break;
       }
       case PH_SKIP1: {
@@ -566,8 +608,9 @@ k_ms_walk2(Walk2Args A) {
         break;
       }
       case PH_ISA1: {
-        const int32_t v = (int32_t)v0.x;
-        start_adj(v, v);
+        u0 = u5 = (int32_t)v0.x;
+        phase = PC_ADJ0;
+        use = 0;
         break;
       }
       case PH_CON1: {
@@ -575,7 +618,8 @@ k_ms_walk2(Walk2Args A) {
         if (sl == n - 1 || sh == n - 1) {  // root (FN:37-39)
           lb = 0;
           rb = (int32_t)n - 1;
-          advance();
+          phase = PC_ADV;
+          use = 0;
         } else {
           phase = PH_CON2;
           ad0 = (uintptr_t)(R.isa + sl + 1);
@@ -585,7 +629,69 @@ k_ms_walk2(Walk2Args A) {
         break;
       }
       case PH_CON2: {
-        start_adj((int32_t)v0.x, (int32_t)v2.x);
+        u0 = (int32_t)v0.x;
+        u5 = (int32_t)v2.x;
+        phase = PC_ADJ0;
+        use = 0;
+        break;
+      }
+      case PH_ADJ: {
+        uint32_t ls0 = (uint32_t)u4;
+        if (ls0 != kScanDone) scan_step<false>(V, v0, v1, (int32_t)len, u0, u1, u2, u3, ls0);
+        u4 = (int32_t)ls0;
+        if (u9 != kScanDone) scan_step<true>(V, v2, v3, (int32_t)len, u5, u6, u7, u8, u9);
+        adj_or_finish();
+        break;
+      }
+      case PH_EXT_A: {
+        u0 = (int32_t)v2.x;  // the text character
+        phase = PH_EXT_B;
+        ad0 = (uintptr_t)(R.ld + lb + 1);
+        ad2 = X + v0.x + len;
+        use = U0Q | U1Q | U2B;
+        break;
+      }
+      case PH_EXT_B: {
+        // children of [lb, rb] at depth off = len, in character order: the
+        // first starts at lb with character x[SA[lb]+off], the others at each
+        // k with LCP[k] == off with character D[k]
+        const uint32_t c = (uint32_t)u0;
+        const uint32_t e[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        const int32_t S1 = rb - lb;
+        bool valid = true;
+        int32_t lo = -1, hi = -1, mm = rb + 1;
+        uint32_t curChar = v2.x & 0xff;
+        int32_t curStart = lb;
+#pragma unroll
+        for (int k = 0; k < 7; k++) {
+          if (k < S1) {
+            const uint32_t l = e[k] >> 8;
+            if (l < len) valid = false;
+            if (l == len) {
+              if (curChar == c) { lo = curStart; hi = lb + k; }
+              if (curChar > c && mm == rb + 1) mm = curStart;
+              curChar = e[k] & 0xff;
+              curStart = lb + 1 + k;
+            }
+          }
+        }
+        if (curChar == c) { lo = curStart; hi = rb; }
+        if (curChar > c && mm == rb + 1) mm = curStart;
+        if (!valid) {  // not an lcp-interval of depth off (root after contraction)
+          begin_bs();
+        } else if (lo >= 0) {  // FN:79-84: one more matched character
+          lb = lo;
+          rb = hi;
+          len++;
+          phase = PC_CHAR;
+          use = 0;
+        } else {  // FN:65-76: insertion point of c
+          smaller = true;
+          if (mm == rb + 1) { mm = rb; smaller = false; }
+          phase = PH_FAIL_SA;
+          ad0 = SA + 4ull * (uint32_t)mm;
+          use = U0D;
+        }
         break;
       }
       case PH_KMER_TEXT: {
@@ -606,7 +712,8 @@ k_ms_walk2(Walk2Args A) {
           ad0 = (uintptr_t)(R.kmer + code);
           use = U0Q;
         } else {
-          begin_char();  // from the root
+          phase = PC_CHAR;  // from the root
+          use = 0;
         }
         break;
       }
@@ -616,15 +723,8 @@ k_ms_walk2(Walk2Args A) {
           rb = (int32_t)v0.y;
           len = R.kmerK;
         }
-        begin_char();
-        break;
-      }
-      case PH_ADJ: {
-        uint32_t ls0 = (uint32_t)u4;
-        if (ls0 != kScanDone) scan_step<false>(R, v0, v1, (int32_t)len, u0, u1, u2, u3, ls0);
-        u4 = (int32_t)ls0;
-        if (u9 != kScanDone) scan_step<true>(R, v2, v3, (int32_t)len, u5, u6, u7, u8, u9);
-        adj_or_finish();
+        phase = PC_CHAR;
+        use = 0;
         break;
       }
       default:
@@ -644,7 +744,7 @@ k_ms_walk2(Walk2Args A) {
         const uint4 xv = ldu16(xa + run + 16 * lane), tv = ldu16(ta + run + 16 * lane);
         const uint32_t m = diff16(xv, tv, xc, tc);
         const uint64_t mis = __ballot(m < 16);
-        if (STATS && lane == 0) atomicAdd(&sc[25], 1ull);
+        if (STATS && lane == 0) atomicAdd(&sc[31], 1ull);
         if (mis) {
           const uint32_t f = (uint32_t)__builtin_ctzll(mis);
           const uint32_t mm = (uint32_t)__shfl((int)m, f);
@@ -652,7 +752,7 @@ k_ms_walk2(Walk2Args A) {
           if (lane == L) {
             len += run + 16 * f + mm;
             smaller = (int8_t)(uint8_t)cc > (int8_t)(uint8_t)(cc >> 8);  // FN:55
-            post_ext();
+            phase = PC_POST;
           }
           break;
         }
@@ -667,10 +767,11 @@ k_ms_walk2(Walk2Args A) {
 }
 
 void launch_ms_walk2(const DevRef& R, const uint8_t* text, const uint64_t* docOff, const Chunk* chunks,
-                     uint32_t nchunks, uint32_t* nextChunk, const Pool& pool, uint32_t* chunkCount,
-                     uint32_t lanes, unsigned long long* stats, hipStream_t st) {
+                     uint32_t nchunks, const uint32_t* order, const uint32_t* bandStart, uint32_t nbands,
+                     uint32_t* nextChunk, const Pool& pool, uint32_t* chunkCount, uint32_t lanes,
+                     unsigned long long* stats, hipStream_t st) {
   if (!nchunks) return;
-  Walk2Args A{R, text, docOff, chunks, nchunks, nextChunk, pool, chunkCount, stats};
+  Walk2Args A{R, text, docOff, chunks, nchunks, order, bandStart, nbands, nextChunk, pool, chunkCount, stats};
   const uint32_t blocks = (std::min<uint32_t>(lanes, nchunks) + 255) / 256;
   if (stats) hipLaunchKernelGGL(k_ms_walk2<true>, dim3(blocks), dim3(256), 0, st, A);
   else hipLaunchKernelGGL(k_ms_walk2<false>, dim3(blocks), dim3(256), 0, st, A);
