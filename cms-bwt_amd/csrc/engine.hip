@@ -892,6 +892,9 @@ struct Engine {
     unsigned long long cs[8];
     HIPCHK(hipMemcpyAsync(cs, cstats.p, sizeof(cs), hipMemcpyDeviceToHost, st));
     sync();
+    if (env_u32("CMSBWT_COUNTER_STATS", 0))
+      fprintf(stderr, "[counter] bad %llu good %llu nothing %llu windows %u crossings %u\n", cs[0], cs[1], cs[2],
+              windows, crossings);
     stats.counter_bad = cs[0];
     stats.counter_good = cs[1];
     stats.counter_nothing = cs[2];

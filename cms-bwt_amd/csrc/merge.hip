@@ -318,8 +318,8 @@ struct CounterArgs {
   uint32_t slotCap;          // windows with more slots use global atomics
 };
 
-struct QueryStats {
-  unsigned long long bad = 0, good = 0, nothing = 0, viol = 0;
+struct QueryStats {  // per lane; a lane serves far fewer than 2^32 queries per window
+  uint32_t bad = 0, good = 0, nothing = 0, viol = 0;
 };
 
 __device__ __forceinline__ uint32_t d_upper_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t v) {
@@ -494,24 +494,26 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
       const uint32_t ql = __builtin_amdgcn_readlane(bl, e), qi = __builtin_amdgcn_readlane(bi, e);
       const uint32_t cq = __builtin_amdgcn_readlane(bc, e), slq = __builtin_amdgcn_readlane(bs, e);
       const bool S = __builtin_amdgcn_readlane(bS, e) != 0;
-      const uint64_t lo = max((uint64_t)p + 1, (uint64_t)T0);
-      const uint64_t hi = min((uint64_t)p + u, (uint64_t)T1 - 1);
-      for (uint64_t t0 = lo; t0 <= hi; t0 += 64) {
-        const uint64_t t = t0 + lane;
-        if (t > hi) break;
-        const uint32_t k = (uint32_t)(t - p - 1);
-        if (lds) d_counter_query<CHECK>(LV, ql, qi, S, cq, slq, k, (uint32_t)t, qs, addLds);
-        else d_counter_query<CHECK>(GV, ql, qi, S, cq, slq, k, (uint32_t)t, qs, addGlb);
+      // targets p+1 .. p+u inside [T0, T1) (positions < 2^31: 32-bit is exact)
+      const uint32_t lo = max(p + 1, T0);
+      const uint32_t hi = (uint32_t)min((uint64_t)p + u, (uint64_t)T1 - 1);
+      for (uint32_t t0 = lo; t0 <= hi; t0 += 64) {
+        const uint32_t t = t0 + lane;
+        if (t <= hi) {
+          const uint32_t k = t - p - 1;
+          if (lds) d_counter_query<CHECK>(LV, ql, qi, S, cq, slq, k, t, qs, addLds);
+          else d_counter_query<CHECK>(GV, ql, qi, S, cq, slq, k, t, qs, addGlb);
+        }
       }
     }
   }
   __syncthreads();
   if (lds)
     for (uint32_t i = threadIdx.x; i < nslot; i += blockDim.x) A.counter[sb + i] = cnt[i];
-  if (qs.bad) atomicAdd(&red[0], qs.bad);
-  if (qs.good) atomicAdd(&red[1], qs.good);
-  if (qs.nothing) atomicAdd(&red[2], qs.nothing);
-  if (qs.viol) atomicAdd(&red[3], qs.viol);
+  if (qs.bad) atomicAdd(&red[0], (unsigned long long)qs.bad);
+  if (qs.good) atomicAdd(&red[1], (unsigned long long)qs.good);
+  if (qs.nothing) atomicAdd(&red[2], (unsigned long long)qs.nothing);
+  if (qs.viol) atomicAdd(&red[3], (unsigned long long)qs.viol);
   __syncthreads();
   if (threadIdx.x < 4 && red[threadIdx.x]) atomicAdd(&A.stats[threadIdx.x], red[threadIdx.x]);
 }
