@@ -62,6 +62,24 @@ def cpu_baseline(ref_len, copies, p, seed):
             "seconds": round(t_coll, 3)}
 
 
+def pmc_traffic(args):
+    """Beyond-L2 bytes per launch of the walk kernel from the committed PMC
+    summary (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate passes, KiB
+    units; tools/gpu_prof.sh), for the default workload only.  FETCH_SIZE is
+    TCC_EA0_RDREQ x 64 B and includes Infinity-Cache hits; the walk's reads
+    are scattered 1..16-byte loads, so no streaming-read correction applies."""
+    default = (args.ref_len, args.copies, args.p, args.seed) == (10_000_000, 1000, 0.001, 4)
+    path = os.path.join(ROOT, "profiles", "r01_pmc.json")
+    if not default or not os.path.exists(path):
+        return None, None
+    try:
+        d = json.load(open(path))["k_ms_walk2"]
+        b = (d["FETCH_SIZE"]["per_launch"] + d["WRITE_SIZE"]["per_launch"]) * 1024.0
+        return int(b), "profiles/r01_pmc.json (FETCH_SIZE+WRITE_SIZE per launch)"
+    except (KeyError, ValueError):
+        return None, None
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -135,6 +153,7 @@ def main():
     b_ms = 22 * n_local + 24 * heads_local
     t_ms = st.ms_walk_kernel_ms / 1e3
     achieved = b_ms / t_ms / 1e9 if t_ms > 0 else 0.0
+    traffic, traffic_src = pmc_traffic(args) if world == 1 else (None, None)
     out = {
         "metric": "collection MB/s to .rl_bwt (10 MB ref + 1000 copies @0.1% SNP)",
         "value": round(value, 3), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
@@ -146,9 +165,10 @@ def main():
                    "collection_bytes": chars_total, "heads": st.heads, "keys": st.keys, "runs": st.runs,
                    "parallelism": (f"documents sharded over {world} GPUs, heads gathered to rank 0 over RCCL, merge on rank 0"
                                    if world > 1 else "1 GPU")},
-        "roofline": {"bound": "hbm", "kernel": "k_ms_walk", "achieved": round(achieved, 1),
+        "roofline": {"bound": "hbm", "kernel": "k_ms_walk2", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "algorithmic_bytes": b_ms, "kernel_ms": round(st.ms_walk_kernel_ms, 3),
+                     "traffic": traffic, "traffic_source": traffic_src,
+                     "algorithmic_bytes": b_ms, "kernel_ms": round(st.ms_walk_kernel_ms, 3),
                      "bytes_model": "22 B/char + 24 B/head (SURVEY.md §8d)"},
         "stages_ms": {"ms_walk": round(st.t_ms_walk_s * 1e3, 2), "merge": round(st.t_merge_s * 1e3, 2),
                       "ms_walk_kernel": round(st.ms_walk_kernel_ms, 2),
