@@ -34,6 +34,12 @@
 
 namespace cmsbwt {
 
+struct IsActive {  // an unresolved member's sa position (0xffffffff = resolved)
+  __host__ __device__ bool operator()(uint32_t v) const { return v != 0xffffffffu; }
+};
+struct LastNonEmpty {  // scan operator: the later non-empty unit's (has, last, first) wins
+  __host__ __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return (b >> 16) ? b : a; }
+};
 struct WidenU64 {
   __host__ __device__ uint64_t operator()(uint32_t v) const { return (uint64_t)v; }
 };
@@ -225,6 +231,13 @@ struct Engine {
   }
 
   // ---- rocPRIM helpers
+  template <class In, class Out, class Init, class Op>
+  void exscan(In in, Out out, Init init, uint64_t n, Op op) {
+    if (!n) return;
+    size_t b = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, b, in, out, init, (size_t)n, op, st));
+    HIPCHK(rocprim::exclusive_scan(scratch(b), b, in, out, init, (size_t)n, op, st));
+  }
   template <class In, class Out, class Init>
   void exscan(In in, Out out, Init init, uint64_t n) {
     if (!n) return;
@@ -252,6 +265,16 @@ struct Engine {
     size_t b = 0;
     HIPCHK(rocprim::radix_sort_keys(nullptr, b, kin, kout, (size_t)n, 0u, (unsigned)bits, st));
     HIPCHK(rocprim::radix_sort_keys(scratch(b), b, kin, kout, (size_t)n, 0u, (unsigned)bits, st));
+  }
+  uint32_t select_flagged_u64(const unsigned long long* in, const uint32_t* flags, unsigned long long* out,
+                              uint32_t n) {
+    if (!n) return 0;
+    DBuf<uint32_t> cnt;
+    cnt.alloc(1);
+    size_t b = 0;
+    HIPCHK(rocprim::select(nullptr, b, in, flags, out, cnt.p, (size_t)n, st));
+    HIPCHK(rocprim::select(scratch(b), b, in, flags, out, cnt.p, (size_t)n, st));
+    return read1(cnt.p);
   }
   uint32_t max_u32(const uint32_t* in, uint64_t n) {
     if (!n) return 0;
@@ -571,11 +594,13 @@ struct Engine {
     hSmall.alloc(H); hChar.alloc(H); hNext.alloc(H);
     HeadsSoA h = heads();
     Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
-    launch_scatter_heads(pool, usedBlocks, chunkCount.p, chunkBase.p, h, plan.dch.p, dtext.p, ddoc.p, st);
+    DBuf<uint32_t> hDoc;  // document of each head (finalize)
+    hDoc.alloc(H);
+    launch_scatter_heads(pool, usedBlocks, chunkCount.p, chunkBase.p, h, plan.dch.p, dtext.p, ddoc.p, hDoc.p, st);
     DBuf<uint32_t> docEnd;
     docEnd.alloc(ndocs);
     launch_end_phrases(dtext.p, ddoc.p, (uint32_t)ndocs, plan.dLast.p, chunkCount.p, chunkBase.p, R.n, h, docEnd.p,
-                       st);
+                       hDoc.p, st);
     diff.alloc((uint64_t)R.n + 1);
     diff.zero(st);
     hasHead.alloc(R.n);
@@ -583,7 +608,7 @@ struct Engine {
     DBuf<uint32_t> errf;
     errf.alloc(1);
     errf.zero(st);
-    launch_finalize(R, h, H, docEnd.p, (uint32_t)ndocs, dtext.p, ddoc.p, diff.p, hasHead.p, errf.p, st);
+    launch_finalize(R, h, H, docEnd.p, (uint32_t)ndocs, dtext.p, ddoc.p, diff.p, hasHead.p, errf.p, hDoc.p, st);
     HIPCHK(hipGetLastError());
     uint32_t ef = read1(errf.p);
     orderInvariant = (ef & 8u) == 0;
@@ -778,33 +803,54 @@ struct Engine {
       HIPCHK(hipMemcpyAsync(saT.p, &hh, 4, hipMemcpyHostToDevice, st));
       HIPCHK(hipMemcpyAsync(grp.p + H, &zz, 4, hipMemcpyHostToDevice, st));
     }
-    mk_ranks(S, K, P.p, posBegin.p, disa.p, itemRankBase.p, headBase.p, n, E, T.p, saT.p, grp.p, st);
+    // slot-major members: item of each slot and member idx of each slot
+    DBuf<uint32_t> itemOfSlot, Pm;
+    itemOfSlot.alloc(H);
+    Pm.alloc(H);
+    {
+      DBuf<uint32_t> mark;
+      mark.alloc(H);
+      mark.zero(st);
+      mk_slot_mark(sSlot.p, K, mark.p, st);
+      inscan(mark.p, itemOfSlot.p, H, rocprim::plus<uint32_t>());
+    }
+    mk_slot_members(S, itemOfSlot.p, P.p, H, Pm.p, st);
+    DBuf<uint32_t> actv;
+    actv.alloc(H);
+    {
+      DBuf<uint32_t> rankBase, gBase;
+      rankBase.alloc(n);
+      gBase.alloc(n);
+      mk_pos_rank_base(posBegin.p, sSlot.p, disa.p, itemRankBase.p, headBase.p, n, E, rankBase.p, gBase.p, st);
+      mk_ranks_slot(S, itemOfSlot.p, Pm.p, H, rankBase.p, gBase.p, n, T.p, saT.p, grp.p, actv.p, st);
+    }
     itemRankBase.release();
     stats.rank = (uint64_t)E + 2 + (uint64_t)(K - 1);
-    sync();
 
     // ---- suffix sort of the head string (libsais_int, FN:1455-1459)
     {
-      DBuf<uint32_t> ac, acOff;
-      ac.alloc(K);
-      acOff.alloc(K);
-      mk_active_count(S, K, n, ac.p, st);
-      exscan(ac.p, acOff.p, 0u, K);
+      const int bH = bits_for(H);
+      // unresolved members' sa positions (resolved ones are 0xffffffff and
+      // sort to the end); U of them
+      DBuf<uint32_t> act, act2, val, val2, lab, labMax, keep;
+      act.alloc(H); act2.alloc(H);
       uint32_t U = 0;
       {
-        uint32_t lastOff = read1(acOff.p + (K - 1)), lastC = read1(ac.p + (K - 1));
-        U = lastOff + lastC;
+        DBuf<uint32_t> cntU;
+        cntU.alloc(1);
+        size_t bb = 0;
+        HIPCHK(rocprim::select(nullptr, bb, actv.p, act2.p, cntU.p, (size_t)H, IsActive(), st));
+        HIPCHK(rocprim::select(scratch(bb), bb, actv.p, act2.p, cntU.p, (size_t)H, IsActive(), st));
+        U = read1(cntU.p);
       }
-      DBuf<uint32_t> act, act2, val, val2, lab, labMax, keep;
+      actv.release();
+      sort_keys(act2.p, act.p, U, bH);
       DBuf<uint64_t> k64, k64b;
-      act.alloc(U); act2.alloc(U); val.alloc(U); val2.alloc(U); lab.alloc(U); labMax.alloc(U); keep.alloc(U);
+      val.alloc(U); val2.alloc(U); lab.alloc(U); labMax.alloc(U); keep.alloc(U);
       k64.alloc(U); k64b.alloc(U);
-      mk_active_init(S, K, n, disa.p, posBegin.p, headBase.p, acOff.p, act.p, st);
-      const int bH = bits_for(H);
-      // groups must be visited in suffix-array order (k_dbl_apply writes the
-      // u-th smallest key to the u-th smallest active sa position)
-      sort_keys(act.p, act2.p, U, bH);
-      std::swap(act.p, act2.p);
+      // groups are visited in suffix-array order (k_dbl_apply writes the
+      // u-th smallest key to the u-th smallest active sa position): act is
+      // sorted above
       for (uint64_t hstep = 1; U > 0; hstep <<= 1) {
         if (hstep > H) throw InputError{CMSBWT_EINPUT, "internal: head-string suffix sort did not converge"};
         mk_dbl_keys(act.p, saT.p, grp.p, (uint32_t)hstep, U, k64.p, val.p, st);
@@ -822,17 +868,35 @@ struct Engine {
     bwtHeads.alloc(H);
     mk_head_ranks(saT.p, hChar.p, H, headRank.p, bwtHeads.p, st);
 
-    // ---- next-head ranks, sorted per item (FN:1480-1494)
+    // ---- next-head ranks, sorted per item (FN:1480-1494): small items by an
+    // in-place insertion sort, large ones by one global (item, nhr) sort
     DBuf<uint32_t> nhr;
     nhr.alloc(H);
     {
-      DBuf<uint64_t> nk, nk2;
-      nk.alloc(H); nk2.alloc(H);
-      mk_nhr_keys(S, K, P.p, headRank.p, hNext.p, nk.p, st);
-      sort_keys(nk.p, nk2.p, H, 32 + bits_for(K));
-      mk_low32(nk2.p, nhr.p, H, st);
+      mk_nhr_slot(Pm.p, headRank.p, hNext.p, H, nhr.p, st);
+      DBuf<uint32_t> bigItem;
+      bigItem.alloc(K);
+      mk_nhr_sort_small(S, K, nhr.p, bigItem.p, st);
+      DBuf<unsigned long long> bk, bk2, bsel;
+      DBuf<uint32_t> bflag, bslots, iotaS;
+      bk.alloc(H); bflag.alloc(H);
+      mk_nhr_big_keys(itemOfSlot.p, bigItem.p, nhr.p, H, bk.p, bflag.p, st);
+      bsel.alloc(H);
+      const uint32_t B = select_flagged_u64(bk.p, bflag.p, bsel.p, H);
+      if (B) {
+        iotaS.alloc(H);
+        mk_iota(iotaS.p, H, st);
+        bslots.alloc(B);
+        const uint32_t B2 = select_flagged(iotaS.p, bflag.p, bslots.p, H);
+        if (B2 != B) throw InputError{CMSBWT_EINPUT, "internal: large-item selection mismatch"};
+        bk2.alloc(B);
+        sort_keys(bsel.p, bk2.p, B, 32 + bits_for(K));
+        mk_nhr_big_back(bk2.p, bslots.p, B, nhr.p, st);
+      }
     }
     headRank.release();
+    Pm.release();
+    itemOfSlot.release();
 
     // ---- counterSmallerThanHead (FN:1523-1603)
     counter.alloc((uint64_t)H + 1);
@@ -920,31 +984,28 @@ struct Engine {
     // ---- writer (FN:1631-1777) as segments + run-length merge
     WriterIn wi{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, sCount.p, headBase.p, bwtHeads.p, counter.p,
                 n, E, rle};
-    DBuf<unsigned long long> segN, segOff;
-    segN.alloc(n);
-    segOff.alloc(n);
-    mk_seg_count(wi, segN.p, st);
-    exscan(segN.p, segOff.p, 0ull, n);
-    uint64_t S_ = (uint64_t)E + read1(segOff.p + (n - 1)) + read1(segN.p + (n - 1));
-    segN.release();
-    DBuf<uint8_t> sc;
-    DBuf<unsigned long long> sn_, flag, runId, cum;
-    sc.alloc(S_); sn_.alloc(S_);
-    mk_seg_emit(wi, segOff.p, sc.p, sn_.p, st);
-    segOff.release();
-    flag.alloc(S_); runId.alloc(S_); cum.alloc(S_);
-    mk_run_flags(sc.p, S_, flag.p, st);
-    inscan(flag.p, runId.p, S_, rocprim::plus<unsigned long long>());
-    inscan(sn_.p, cum.p, S_, rocprim::plus<unsigned long long>());
-    uint64_t Rn = read1(runId.p + (S_ - 1));
-    uint64_t symbols = read1(cum.p + (S_ - 1));
-    flag.release();
-    DBuf<unsigned long long> runEnd;
+    // units: the E end phrases, then SA ranks 1..n-1; runs counted per unit,
+    // joined across unit boundaries, emitted as (start, char) and packed
+    const uint64_t U64 = (uint64_t)E + n - 1;
+    if (U64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer units"};
+    const uint32_t Uw = (uint32_t)U64;
+    DBuf<uint32_t> wruns, whl, wprev;
+    DBuf<unsigned long long> wsym, wrunOff, wsymOff;
+    wruns.alloc(Uw); whl.alloc(Uw); wprev.alloc(Uw); wsym.alloc(Uw); wrunOff.alloc(Uw); wsymOff.alloc(Uw);
+    mk_wr_count(wi, Uw, wruns.p, wsym.p, whl.p, st);
+    exscan(whl.p, wprev.p, 0u, Uw, LastNonEmpty());
+    mk_wr_adjust(whl.p, wprev.p, Uw, wruns.p, st);
+    auto runs64 = rocprim::make_transform_iterator(wruns.p, WidenU64());
+    exscan(runs64, wrunOff.p, 0ull, Uw);
+    exscan(wsym.p, wsymOff.p, 0ull, Uw);
+    const uint64_t Rn = read1(wrunOff.p + (Uw - 1)) + read1(wruns.p + (Uw - 1));
+    const uint64_t symbols = read1(wsymOff.p + (Uw - 1)) + read1(wsym.p + (Uw - 1));
+    DBuf<unsigned long long> runStart;
     DBuf<uint8_t> runChar;
-    runEnd.alloc(Rn); runChar.alloc(Rn);
-    mk_run_pack(sc.p, runId.p, cum.p, S_, runEnd.p, runChar.p, st);
+    runStart.alloc(std::max<uint64_t>(Rn, 1)); runChar.alloc(std::max<uint64_t>(Rn, 1));
+    mk_wr_emit(wi, Uw, wrunOff.p, wsymOff.p, wprev.p, runStart.p, runChar.p, st);
     runs.alloc(Rn * 9);
-    mk_run_records(runEnd.p, runChar.p, Rn, runs.p, st);
+    mk_wr_records(runStart.p, runChar.p, Rn, symbols, runs.p, st);
     HIPCHK(hipGetLastError());
     sync();
     nruns = Rn;

@@ -41,7 +41,7 @@ void launch_chunk_with_end(const Chunk* chunks, const uint32_t* chunkCount, uint
                            hipStream_t st);
 void launch_scatter_heads(const Pool& pool, uint32_t blocksUsed, const uint32_t* chunkCount,
                           const unsigned long long* chunkBase, const HeadsSoA& h, const Chunk* chunks,
-                          const uint8_t* text, const uint64_t* docOff, hipStream_t st);
+                          const uint8_t* text, const uint64_t* docOff, uint32_t* hdoc, hipStream_t st);
 // ms_walk2.hip: uniform-step walk; `lanes` resident lanes pull chunks from
 // per-band queues: order[bandStart[k] ..) are band k's chunk ids, nextChunk[16k]
 // its (zeroed) counter
@@ -52,10 +52,10 @@ void launch_ms_walk2(const DevRef& R, const uint8_t* text, const uint64_t* docOf
 void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t ndocs,
                         const uint32_t* docLastChunk, const uint32_t* chunkCount,
                         const unsigned long long* chunkBase, uint32_t n, const HeadsSoA& h, uint32_t* docEndIdx,
-                        hipStream_t st);
+                        uint32_t* hdoc, hipStream_t st);
 void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint32_t* docEndIdx,
                      uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, int32_t* diff, uint8_t* hasHead,
-                     uint32_t* errFlags, hipStream_t st);
+                     uint32_t* errFlags, const uint32_t* hdoc, hipStream_t st);
 
 // synth.hip
 void launch_synth_collection(uint8_t* text, uint64_t L, uint64_t seed, uint64_t copy_begin, uint64_t ncopies,

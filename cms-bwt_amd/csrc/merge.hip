@@ -280,6 +280,100 @@ __global__ void k_nhr_keys(const ItemsSoA it, uint32_t K, const uint32_t* __rest
   }
 }
 
+// ---- slot-major members (one thread per head, no per-item loops)
+// mark[slot[q]] = 1 for q >= 1; its inclusive scan is the item of each slot
+__global__ void k_slot_mark(const uint32_t* __restrict__ slot, uint32_t K, uint32_t* __restrict__ mark) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= 1 && q < K) mark[slot[q]] = 1;
+}
+// Pm[s] = idx of the member of slot s (members of an item in idx order)
+__global__ void k_slot_members(const ItemsSoA it, const uint32_t* __restrict__ itemOfSlot,
+                               const uint32_t* __restrict__ perm, uint32_t H, uint32_t* __restrict__ Pm) {
+  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= H) return;
+  const uint32_t q = itemOfSlot[s];
+  Pm[s] = perm[it.first[q] + (s - it.slot[q])];
+}
+// Ranks of FN:1432-1453 and the initial (first-symbol) order of the head
+// string for the suffix sort (FN:1455-1459), one thread per member.
+// Per position (mod 2^32): rank(q) = rankBase[p] + q, group g(q) = gBase[p] +
+// slot[q] for the items q of p (their SA-rank prefix sums, FN:1436-1449).
+__global__ void k_pos_rank_base(const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ slot,
+                                const uint32_t* __restrict__ isaRef, const uint32_t* __restrict__ itemRankBase,
+                                const uint32_t* __restrict__ headBase, uint32_t n, uint32_t E,
+                                uint32_t* __restrict__ rankBase, uint32_t* __restrict__ gBase) {
+  uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t b = posBegin[p];
+  if (b == posBegin[p + 1]) return;  // no items here
+  const uint32_t r = isaRef[p];
+  rankBase[p] = E + 2 + itemRankBase[r] - b;
+  gBase[p] = 1 + headBase[r] - slot[b];
+}
+__global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ itemOfSlot,
+                             const uint32_t* __restrict__ Pm, uint32_t H, const uint32_t* __restrict__ rankBase,
+                             const uint32_t* __restrict__ gBase, uint32_t n, int32_t* __restrict__ T,
+                             uint32_t* __restrict__ sa, uint32_t* __restrict__ grp, uint32_t* __restrict__ actv) {
+  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= H) return;
+  const uint32_t q = itemOfSlot[s], idx = Pm[s];
+  const uint32_t sq = it.slot[q], m = s - sq, p = it.pos[q];
+  if (p == n - 1) {  // end phrases: one rank each, in document order
+    T[idx] = (int32_t)(1 + m);
+    sa[1 + m] = idx;
+    grp[idx] = 1 + m;
+    actv[s] = 0xffffffffu;
+    return;
+  }
+  const uint32_t g = gBase[p] + sq;
+  T[idx] = (int32_t)(rankBase[p] + q);
+  sa[g + m] = idx;
+  grp[idx] = g;
+  // unresolved members (items with >= 2 heads): their sa positions
+  actv[s] = it.count[q] >= 2 ? g + m : 0xffffffffu;
+}
+// next-head rank of each member, in slot order (FN:1480-1494)
+__global__ void k_nhr_slot(const uint32_t* __restrict__ Pm, const uint32_t* __restrict__ headRank,
+                           const uint16_t* __restrict__ nexthead, uint32_t H, uint32_t* __restrict__ nhr) {
+  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= H) return;
+  const uint32_t idx = Pm[s];
+  nhr[s] = headRank[idx + nexthead[idx]];
+}
+// Sort each item's nhr segment: insertion sort in place for <= kSmallSeg
+// members; larger items are flagged (slot-wise) for one global sort.
+constexpr uint32_t kSmallSeg = 32;
+__global__ void k_nhr_sort_small(const ItemsSoA it, uint32_t K, uint32_t* __restrict__ nhr,
+                                 uint32_t* __restrict__ bigItem) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= K) return;
+  const uint32_t c = it.count[q];
+  bigItem[q] = c > kSmallSeg ? 1u : 0u;
+  if (c < 2 || c > kSmallSeg) return;
+  uint32_t* a = nhr + it.slot[q];
+  for (uint32_t x = 1; x < c; x++) {
+    const uint32_t v = a[x];
+    uint32_t y = x;
+    while (y > 0 && a[y - 1] > v) { a[y] = a[y - 1]; y--; }
+    a[y] = v;
+  }
+}
+// keys (item, nhr) and slots of the members of large items
+__global__ void k_nhr_big_keys(const uint32_t* __restrict__ itemOfSlot, const uint32_t* __restrict__ bigItem,
+                               const uint32_t* __restrict__ nhr, uint32_t H, unsigned long long* __restrict__ key,
+                               uint32_t* __restrict__ flag) {
+  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= H) return;
+  const uint32_t q = itemOfSlot[s];
+  flag[s] = bigItem[q];
+  key[s] = ((unsigned long long)q << 32) | nhr[s];
+}
+__global__ void k_nhr_big_back(const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ slots,
+                               uint32_t B, uint32_t* __restrict__ nhr) {
+  uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < B) nhr[slots[u]] = (uint32_t)sorted[u];
+}
+
 __global__ void k_low32(const uint64_t* __restrict__ key, uint32_t* __restrict__ out, uint64_t n) {
   uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) out[i] = (uint32_t)key[i];
@@ -645,6 +739,94 @@ __device__ __forceinline__ uint64_t d_segments(const WriterArgs& A, uint32_t r, 
   return ns;
 }
 
+// Segments of one writer unit, in output order, to f(char, count): units
+// [0, E) are the end phrases' BWT characters (rank 0's heads), unit E + r - 1
+// is SA rank r >= 1 (the same walk as d_segments).
+template <class F>
+__device__ __forceinline__ void d_unit_segments(const WriterArgs& A, uint32_t u, F&& f) {
+  if (u < A.E) { f(A.bwtHeads[u], 1ull); return; }
+  const uint32_t r = u - A.E + 1;
+  const uint32_t p = (uint32_t)A.sa[r];
+  const uint8_t c = A.bwt[r];
+  const int64_t b = A.bucket[p];
+  if (b > 0) { f(c, (unsigned long long)b); return; }
+  if (b == 0) return;
+  int64_t acc = b;
+  const uint32_t i0 = A.posBegin[p], i1 = A.posBegin[p + 1];
+  const uint32_t s0 = A.slot[i0];
+  const uint32_t hb = A.headBase[r];
+  for (uint32_t q = i0; q < i1; q++) {
+    const uint32_t sb = A.slot[q], se = sb + A.count[q];
+    for (uint32_t s = sb; s < se; s++) {
+      const unsigned long long cs = A.counter[s];
+      if (cs) { f(c, cs); acc += (int64_t)cs; }
+      f(A.bwtHeads[hb + (s - s0)], 1ull);
+      acc++;
+    }
+    if (A.rle && acc != 0) f(c, (unsigned long long)(-acc));  // FN:1761-1770 quirk
+  }
+  if (!A.rle && acc < 0) f(c, (unsigned long long)(-acc));
+}
+
+// Run writer, pass 1: per unit its run starts (counting its first segment),
+// symbols, first and last character.  hl = has << 16 | last << 8 | first.
+__global__ void k_wr_count(WriterArgs A, uint32_t U, uint32_t* __restrict__ runs, unsigned long long* __restrict__ sym,
+                           uint32_t* __restrict__ hl) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  int prev = -1, first = -1;
+  uint32_t nr = 0;
+  unsigned long long ns = 0;
+  d_unit_segments(A, u, [&](uint8_t c, unsigned long long cnt) {
+    if (first < 0) first = c;
+    if ((int)c != prev) nr++;
+    prev = c;
+    ns += cnt;
+  });
+  runs[u] = nr;
+  sym[u] = ns;
+  hl[u] = first < 0 ? 0u : (1u << 16) | ((uint32_t)prev << 8) | (uint32_t)first;
+}
+// pass 2: a unit's first segment continues the previous non-empty unit's run
+// when the characters match (prevHL = exclusive "last non-empty" scan of hl)
+__global__ void k_wr_adjust(const uint32_t* __restrict__ hl, const uint32_t* __restrict__ prevHL, uint32_t U,
+                            uint32_t* __restrict__ runs) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  const uint32_t a = hl[u], pv = prevHL[u];
+  if ((a >> 16) && (pv >> 16) && (a & 0xff) == ((pv >> 8) & 0xff)) runs[u]--;
+}
+// pass 3: emit run starts (symbol offsets) and characters
+__global__ void k_wr_emit(WriterArgs A, uint32_t U, const unsigned long long* __restrict__ runOff,
+                          const unsigned long long* __restrict__ symOff, const uint32_t* __restrict__ prevHL,
+                          unsigned long long* __restrict__ runStart, uint8_t* __restrict__ runChar) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  const uint32_t pv = prevHL[u];
+  int prev = (pv >> 16) ? (int)((pv >> 8) & 0xff) : -1;
+  unsigned long long j = runOff[u], pos = symOff[u];
+  d_unit_segments(A, u, [&](uint8_t c, unsigned long long cnt) {
+    if ((int)c != prev) {
+      runStart[j] = pos;
+      runChar[j] = c;
+      j++;
+    }
+    prev = c;
+    pos += cnt;
+  });
+}
+// pass 4: 9-byte little-endian records (length u64, char)
+__global__ void k_wr_records(const unsigned long long* __restrict__ runStart, const uint8_t* __restrict__ runChar,
+                             uint64_t R, unsigned long long total, uint8_t* __restrict__ out) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= R) return;
+  const unsigned long long len = (j + 1 < R ? runStart[j + 1] : total) - runStart[j];
+  uint8_t* o = out + 9 * j;
+#pragma unroll
+  for (int b = 0; b < 8; b++) o[b] = (uint8_t)(len >> (8 * b));
+  o[8] = runChar[j];
+}
+
 __global__ void k_seg_count(WriterArgs A, unsigned long long* __restrict__ segN) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= A.n) return;
@@ -733,6 +915,42 @@ void mk_item_flags64(const unsigned long long* key, uint32_t* flag, uint64_t H, 
 void mk_item_fill64(const unsigned long long* key, const uint32_t* perm, const uint32_t* flag, const uint32_t* incl,
                     const HeadsSoA& h, uint64_t H, int bN, int bL, const ItemsSoA& it, hipStream_t st) {
   if (H) hipLaunchKernelGGL(k_item_fill64, g1(H), dim3(256), 0, st, key, perm, flag, incl, h, H, bN, bL, it);
+}
+void mk_slot_mark(const uint32_t* slot, uint32_t K, uint32_t* mark, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_slot_mark, g1(K), dim3(256), 0, st, slot, K, mark);
+}
+void mk_slot_members(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* perm, uint32_t H, uint32_t* Pm,
+                     hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_slot_members, g1(H), dim3(256), 0, st, it, itemOfSlot, perm, H, Pm);
+}
+void mk_pos_rank_base(const uint32_t* posBegin, const uint32_t* slot, const uint32_t* isaRef,
+                      const uint32_t* itemRankBase, const uint32_t* headBase, uint32_t n, uint32_t E,
+                      uint32_t* rankBase, uint32_t* gBase, hipStream_t st) {
+  if (n)
+    hipLaunchKernelGGL(k_pos_rank_base, g1(n), dim3(256), 0, st, posBegin, slot, isaRef, itemRankBase, headBase, n, E,
+                       rankBase, gBase);
+}
+void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
+                   const uint32_t* rankBase, const uint32_t* gBase, uint32_t n, int32_t* T, uint32_t* sa,
+                   uint32_t* grp, uint32_t* actv, hipStream_t st) {
+  if (H)
+    hipLaunchKernelGGL(k_ranks_slot, g1(H), dim3(256), 0, st, it, itemOfSlot, Pm, H, rankBase, gBase, n, T, sa, grp,
+                       actv);
+}
+void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, const uint16_t* nexthead, uint32_t H, uint32_t* nhr,
+                 hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_nhr_slot, g1(H), dim3(256), 0, st, Pm, headRank, nexthead, H, nhr);
+}
+void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigItem, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_nhr_sort_small, g1(K), dim3(256), 0, st, it, K, nhr, bigItem);
+}
+void mk_nhr_big_keys(const uint32_t* itemOfSlot, const uint32_t* bigItem, const uint32_t* nhr, uint32_t H,
+                     unsigned long long* key, uint32_t* flag, hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_nhr_big_keys, g1(H), dim3(256), 0, st, itemOfSlot, bigItem, nhr, H, key, flag);
+}
+void mk_nhr_big_back(const unsigned long long* sorted, const uint32_t* slots, uint32_t B, uint32_t* nhr,
+                     hipStream_t st) {
+  if (B) hipLaunchKernelGGL(k_nhr_big_back, g1(B), dim3(256), 0, st, sorted, slots, B, nhr);
 }
 void mk_item_count(const uint32_t* first, uint32_t* count, uint32_t K, uint32_t H, hipStream_t st) {
   if (K) hipLaunchKernelGGL(k_item_count, g1(K), dim3(256), 0, st, first, count, K, H);
@@ -839,6 +1057,25 @@ void mk_seg_emit(const WriterIn& w, const unsigned long long* segOff, uint8_t* s
   WriterArgs A{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.count, w.headBase, w.bwtHeads, w.counter,
                w.n, w.E, w.rle};
   hipLaunchKernelGGL(k_seg_emit, g1(w.n), dim3(256), 0, st, A, segOff, sc, sn);
+}
+static WriterArgs writer_args(const WriterIn& w) {
+  return WriterArgs{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.count, w.headBase, w.bwtHeads, w.counter,
+                    w.n, w.E, w.rle};
+}
+void mk_wr_count(const WriterIn& w, uint32_t U, uint32_t* runs, unsigned long long* sym, uint32_t* hl, hipStream_t st) {
+  if (U) hipLaunchKernelGGL(k_wr_count, g1(U), dim3(256), 0, st, writer_args(w), U, runs, sym, hl);
+}
+void mk_wr_adjust(const uint32_t* hl, const uint32_t* prevHL, uint32_t U, uint32_t* runs, hipStream_t st) {
+  if (U) hipLaunchKernelGGL(k_wr_adjust, g1(U), dim3(256), 0, st, hl, prevHL, U, runs);
+}
+void mk_wr_emit(const WriterIn& w, uint32_t U, const unsigned long long* runOff, const unsigned long long* symOff,
+                const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st) {
+  if (U) hipLaunchKernelGGL(k_wr_emit, g1(U), dim3(256), 0, st, writer_args(w), U, runOff, symOff, prevHL, runStart,
+                            runChar);
+}
+void mk_wr_records(const unsigned long long* runStart, const uint8_t* runChar, uint64_t R, unsigned long long total,
+                   uint8_t* out, hipStream_t st) {
+  if (R) hipLaunchKernelGGL(k_wr_records, g1(R), dim3(256), 0, st, runStart, runChar, R, total, out);
 }
 void mk_run_flags(const uint8_t* sc, uint64_t S, unsigned long long* flag, hipStream_t st) {
   if (S) hipLaunchKernelGGL(k_run_flags, g1(S), dim3(256), 0, st, sc, S, flag);

@@ -33,6 +33,24 @@ void mk_item_fill64(const unsigned long long* key, const uint32_t* perm, const u
 void mk_item_fill(const uint32_t* perm, const uint32_t* flag, const uint32_t* incl, const HeadsSoA& h,
                   uint64_t H, const ItemsSoA& it, hipStream_t st);
 void mk_item_count(const uint32_t* first, uint32_t* count, uint32_t K, uint32_t H, hipStream_t st);
+// slot-major members: item of each slot, member idx of each slot, ranks and
+// unresolved sa positions (0xffffffff = resolved), next-head ranks
+void mk_slot_mark(const uint32_t* slot, uint32_t K, uint32_t* mark, hipStream_t st);
+void mk_slot_members(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* perm, uint32_t H, uint32_t* Pm,
+                     hipStream_t st);
+void mk_pos_rank_base(const uint32_t* posBegin, const uint32_t* slot, const uint32_t* isaRef,
+                      const uint32_t* itemRankBase, const uint32_t* headBase, uint32_t n, uint32_t E,
+                      uint32_t* rankBase, uint32_t* gBase, hipStream_t st);
+void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
+                   const uint32_t* rankBase, const uint32_t* gBase, uint32_t n, int32_t* T, uint32_t* sa,
+                   uint32_t* grp, uint32_t* actv, hipStream_t st);
+void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, const uint16_t* nexthead, uint32_t H, uint32_t* nhr,
+                 hipStream_t st);
+void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigItem, hipStream_t st);
+void mk_nhr_big_keys(const uint32_t* itemOfSlot, const uint32_t* bigItem, const uint32_t* nhr, uint32_t H,
+                     unsigned long long* key, uint32_t* flag, hipStream_t st);
+void mk_nhr_big_back(const unsigned long long* sorted, const uint32_t* slots, uint32_t B, uint32_t* nhr,
+                     hipStream_t st);
 void mk_item_permute(const ItemsSoA& in, const uint32_t* order, const ItemsSoA& out, uint32_t K, hipStream_t st);
 void mk_pos_begin(const uint32_t* ipos, uint32_t K, uint32_t n, uint32_t* posBegin, hipStream_t st);
 void mk_pos_f(const uint32_t* ipos, const uint8_t* ism, const uint32_t* posBegin, uint32_t K, uint32_t n,
@@ -73,6 +91,13 @@ void mk_counter_win(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t
                     hipStream_t st);
 void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st);
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st);
+// run writer: units = E end phrases + SA ranks 1..n-1
+void mk_wr_count(const WriterIn& w, uint32_t U, uint32_t* runs, unsigned long long* sym, uint32_t* hl, hipStream_t st);
+void mk_wr_adjust(const uint32_t* hl, const uint32_t* prevHL, uint32_t U, uint32_t* runs, hipStream_t st);
+void mk_wr_emit(const WriterIn& w, uint32_t U, const unsigned long long* runOff, const unsigned long long* symOff,
+                const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st);
+void mk_wr_records(const unsigned long long* runStart, const uint8_t* runChar, uint64_t R, unsigned long long total,
+                   uint8_t* out, hipStream_t st);
 void mk_seg_count(const WriterIn& w, unsigned long long* segN, hipStream_t st);
 void mk_seg_emit(const WriterIn& w, const unsigned long long* segOff, uint8_t* sc, unsigned long long* sn,
                  hipStream_t st);

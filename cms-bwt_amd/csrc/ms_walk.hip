@@ -283,7 +283,7 @@ __global__ void k_chunk_with_end(const Chunk* __restrict__ chunks, const uint32_
 __global__ void k_scatter_heads(Pool pool, uint32_t blocksUsed, const uint32_t* __restrict__ chunkCount,
                                 const unsigned long long* __restrict__ chunkBase, HeadsSoA h,
                                 const Chunk* __restrict__ chunks, const uint8_t* __restrict__ text,
-                                const uint64_t* __restrict__ docOff) {
+                                const uint64_t* __restrict__ docOff, uint32_t* __restrict__ hdoc) {
   uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t blk = slot / kPoolB;
   if (blk >= blocksUsed) return;
@@ -297,7 +297,9 @@ __global__ void k_scatter_heads(Pool pool, uint32_t blocksUsed, const uint32_t* 
   h.len[idx] = r.len;
   h.smaller[idx] = (uint8_t)(r.flags & 1u);
   // BWT character of the phrase: the text byte before it, 0x02 at a document start
-  h.lchar[idx] = r.start == 0 ? (uint8_t)kSep : text[docOff[chunks[cid].doc] + r.start - 1];
+  const uint32_t d = chunks[cid].doc;
+  h.lchar[idx] = r.start == 0 ? (uint8_t)kSep : text[docOff[d] + r.start - 1];
+  hdoc[idx] = d;
 }
 
 // End-of-document phrase (FN:1198-1212): (docLen, n-1, 0, false), char =
@@ -306,7 +308,7 @@ __global__ void k_end_phrases(const uint8_t* __restrict__ text, const uint64_t* 
                               uint32_t ndocs, const uint32_t* __restrict__ docLastChunk,
                               const uint32_t* __restrict__ chunkCount,
                               const unsigned long long* __restrict__ chunkBase, uint32_t n, HeadsSoA h,
-                              uint32_t* __restrict__ docEndIdx) {
+                              uint32_t* __restrict__ docEndIdx, uint32_t* __restrict__ hdoc) {
   uint32_t d = blockIdx.x * blockDim.x + threadIdx.x;
   if (d >= ndocs) return;
   uint32_t c = docLastChunk[d];
@@ -318,6 +320,7 @@ __global__ void k_end_phrases(const uint8_t* __restrict__ text, const uint64_t* 
   h.smaller[idx] = 0;
   h.lchar[idx] = len ? text[docOff[d] + len - 1] : kSep;
   docEndIdx[d] = idx;
+  hdoc[idx] = d;
 }
 
 // ------------------------------------------------------------ j-scan (FN:1359-1385)
@@ -329,7 +332,7 @@ __global__ void k_end_phrases(const uint8_t* __restrict__ text, const uint64_t* 
 __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __restrict__ docEndIdx,
                            uint32_t ndocs, const uint8_t* __restrict__ text, const uint64_t* __restrict__ docOff,
                            int32_t* __restrict__ diff, uint8_t* __restrict__ hasHead,
-                           uint32_t* __restrict__ errFlags) {
+                           uint32_t* __restrict__ errFlags, const uint32_t* __restrict__ hdoc) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= H) return;
   const uint32_t leni = h.len[i];
@@ -342,12 +345,7 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
     hasHead[R.n - 1] = 1;
     return;
   }
-  // document of i: first docEnd >= i
-  uint32_t lo = 0, hi = ndocs - 1;
-  while (lo < hi) {
-    uint32_t m = (lo + hi) >> 1;
-    if (docEndIdx[m] >= i) hi = m; else lo = m + 1;
-  }
+  const uint32_t lo = hdoc[i];  // document of i (written by the scatter)
   const uint32_t de = docEndIdx[lo];
   const uint32_t si = h.start[i];
   const uint32_t ei = si + leni;
@@ -404,28 +402,28 @@ void launch_chunk_with_end(const Chunk* chunks, const uint32_t* chunkCount, uint
 
 void launch_scatter_heads(const Pool& pool, uint32_t blocksUsed, const uint32_t* chunkCount,
                           const unsigned long long* chunkBase, const HeadsSoA& h, const Chunk* chunks,
-                          const uint8_t* text, const uint64_t* docOff, hipStream_t st) {
+                          const uint8_t* text, const uint64_t* docOff, uint32_t* hdoc, hipStream_t st) {
   uint64_t slots = (uint64_t)blocksUsed * kPoolB;
   if (!slots) return;
   hipLaunchKernelGGL(k_scatter_heads, dim3((unsigned)((slots + 255) / 256)), dim3(256), 0, st, pool,
-                     blocksUsed, chunkCount, chunkBase, h, chunks, text, docOff);
+                     blocksUsed, chunkCount, chunkBase, h, chunks, text, docOff, hdoc);
 }
 
 void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t ndocs,
                         const uint32_t* docLastChunk, const uint32_t* chunkCount,
                         const unsigned long long* chunkBase, uint32_t n, const HeadsSoA& h, uint32_t* docEndIdx,
-                        hipStream_t st) {
+                        uint32_t* hdoc, hipStream_t st) {
   if (!ndocs) return;
   hipLaunchKernelGGL(k_end_phrases, dim3((ndocs + 255) / 256), dim3(256), 0, st, text, docOff, ndocs,
-                     docLastChunk, chunkCount, chunkBase, n, h, docEndIdx);
+                     docLastChunk, chunkCount, chunkBase, n, h, docEndIdx, hdoc);
 }
 
 void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint32_t* docEndIdx,
                      uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, int32_t* diff, uint8_t* hasHead,
-                     uint32_t* errFlags, hipStream_t st) {
+                     uint32_t* errFlags, const uint32_t* hdoc, hipStream_t st) {
   if (!H) return;
   hipLaunchKernelGGL(k_finalize, dim3((H + 255) / 256), dim3(256), 0, st, R, h, H, docEndIdx, ndocs, text, docOff,
-                     diff, hasHead, errFlags);
+                     diff, hasHead, errFlags, hdoc);
 }
 
 }  // namespace cmsbwt
