@@ -570,9 +570,9 @@ struct Engine {
     }
     if (w2stats.p) {
       static const char* names[32] = {"done", "next", "bs_text", "bs_sa", "bs_x", "fail_sa", "lce_sa", "lce",
-                                       "skip1", "gallop", "skipbs", "isa1", "con1", "con2", "adj", "kmer_text",
-                                       "kmer_tab", "ext_a", "ext_b", "lce_coop", "c_adj0", "c_adv", "c_post",
-                                       "c_char", "-", "-", "scan0", "scan1", "scan2", "scan3", "wave_steps",
+                                       "skip1", "skip0", "gallop", "skipbs", "isa1", "con1", "con2", "adj",
+                                       "kmer_text", "kmer_tab", "ext_a", "ext_b", "lce_coop", "c_adj0", "c_adv",
+                                       "c_post", "c_char", "-", "scan0", "scan1", "scan2", "scan3", "wave_steps",
                                        "coop_steps"};
       std::vector<unsigned long long> h(32);
       HIPCHK(hipMemcpy(h.data(), w2stats.p, 32 * 8, hipMemcpyDeviceToHost));

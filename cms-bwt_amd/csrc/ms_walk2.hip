@@ -19,14 +19,15 @@
 //   LCE         16 B of x and of the text      POST / LCE_COOP
 //   LCE_COOP    (none) the whole wave compares 1 KiB per step of one lane's
 //               long extension with coalesced loads, lane by lane -> POST
-//   SKIP1       PLCP[pos+1], PLCP[T-7..T]      ISA1 / GALLOP (FN:1176-1185)
+//   SKIP1       PLCP[T-16..T-1]                ISA1 / SKIP0 (FN:1176-1185)
+//   SKIP0       PLCP[pos+1]                    ISA1 / GALLOP
 //   GALLOP/SKIPBS  one PLCP probe              ISA1
 //   ISA1        ISA[pos+1]                     ADJ0          (FN:1187)
 //   CON1/CON2   SA[lb],SA[rb] / ISA[..+1]      ADJ0 / ADV    (FN:34-43)
 //   ADJ         8 LCP entries for PSV + 8 for NSV  ADJ / ADV (FN:11-25)
 //   KMER_TEXT/KMER_TAB  restart: K text bytes, then the K-mer's SA interval
 //               (= the state after K matched characters from the root)
-//   EXT_A/EXT_B one character over an interval of <= 8 suffixes without a
+//   EXT_A/EXT_B one character over an interval of <= 16 suffixes without a
 //               binary search: its children at depth off start where LCP ==
 //               off, with first characters D (= x[SA[k]+LCP[k]]) and x[SA[lb]+off]
 //   compute phases (no load): ADJ0 (start adjustInterval), ADV (next
@@ -56,6 +57,7 @@ enum : uint32_t {
   PH_LCE_SA,
   PH_LCE,
   PH_SKIP1,
+  PH_SKIP0,
   PH_GALLOP,
   PH_SKIPBS,
   PH_ISA1,
@@ -96,6 +98,8 @@ enum : uint32_t {
   U2Q = 32,   // 16 B at B
   U3Q = 64,   // 16 B at B + 16
   U2B = 128,  // byte at B
+  U4Q = 256,  // 16 B at A + 32
+  U5Q = 512,  // 16 B at A + 48
 };
 // First differing byte of two 16-byte strings: 16 if equal.
 __device__ __forceinline__ uint32_t diff16(const uint4& x, const uint4& t, uint8_t& xc, uint8_t& tc) {
@@ -297,18 +301,18 @@ k_ms_walk2(Walk2Args A) {
     ad0 = (uintptr_t)(R.isa + pos + 1);
     use = U0D;
   };
-  // gallop (u4 = step, u1 = lo) then binary search on (u1, u2]
+  // gallop (u4 = step, u1 = lo, below the cap u2 where the predicate holds)
+  // then binary search on (u1, u2]
   auto skip_probe = [&](bool galloping) {
     if (galloping) {
       const uint64_t t = (uint64_t)(uint32_t)u1 + (uint32_t)u4;
-      if (t < len) {
+      if (t < (uint32_t)u2) {
         u3 = (int32_t)t;
         phase = PH_GALLOP;
         ad0 = P + 4ull * (pos + 1 + (uint32_t)u3);
         use = U0D;
         return;
       }
-      u2 = (int32_t)len;
     }
     if ((uint32_t)u2 - (uint32_t)u1 > 1) {
       u3 = (int32_t)((uint32_t)u1 + (((uint32_t)u2 - (uint32_t)u1) >> 1));
@@ -427,14 +431,13 @@ k_ms_walk2(Walk2Args A) {
       }
       len--;
       if (lb == rb) {  // FN:1175-1189: skip, then adjustInterval(ISA[pos+1])
+        // the exit is the first q >= pos+1 with PLCP[q] + q >= T = pos+1+len;
+        // PLCP of a random-like text is ~log4 n, so it lies ~12 below T:
+        // probe the 16 entries below T first
         phase = PH_SKIP1;
-        ad0 = P + 4ull * (pos + 1);
-        use = U0D;
-        if (len > 8) {
-          const uint64_t TT = (uint64_t)pos + 1 + len;
-          ad2 = P + 4ull * ((TT & ~3ull) - 4);
-          use = U0D | U2Q | U3Q;
-        }
+        const uint64_t TT = (uint64_t)pos + 1 + len;
+        ad0 = P + 4ull * (TT >= 16 ? TT - 16 : 0);
+        use = U0Q | U1Q | U4Q | U5Q;
       } else {  // FN:1190-1194: contractLeft
         phase = PH_CON1;
         ad0 = SA + 4ull * (uint32_t)lb;
@@ -447,7 +450,7 @@ k_ms_walk2(Walk2Args A) {
         phase = PH_LCE_SA;
         ad0 = SA + 4ull * (uint32_t)lb;
         use = U0D;
-      } else if (R.ld && rb - lb < 8 && len < 0xffffffu) {
+      } else if (R.ld && rb - lb < 16 && len < 0xffffffu) {
         phase = PH_EXT_A;
         ad0 = SA + 4ull * (uint32_t)lb;
         ad2 = T + i + len;
@@ -467,7 +470,7 @@ k_ms_walk2(Walk2Args A) {
       if (lane == 0) atomicAdd(&sc[30], 1ull);
     }
     // ---- one memory step
-    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0, v2 = v0, v3 = v0;
+    uint4 v0 = make_uint4(0, 0, 0, 0), v1 = v0, v2 = v0, v3 = v0, v4 = v0, v5 = v0;
     if (use & U0B) v0.x = ld1(ad0);
     if (use & U0D) v0.x = ld4(ad0);
     if (use & U0Q) v0 = ldu16(ad0);
@@ -476,6 +479,8 @@ k_ms_walk2(Walk2Args A) {
     if (use & U2B) v2.x = ld1(ad2);
     if (use & U2Q) v2 = ldu16(ad2);
     if (use & U3Q) v3 = ldu16(ad2 + 16);
+    if (use & U4Q) v4 = ldu16(ad0 + 32);
+    if (use & U5Q) v5 = ldu16(ad0 + 48);
     // ---- one state-machine step (load phases)
     switch (phase) {
       case PH_BS_TEXT: {  // c = t[j]; the first probe's SA value is in slot 2
@@ -567,23 +572,30 @@ k_ms_walk2(Walk2Args A) {
         break;
       }
       case PH_SKIP1: {
-        const int64_t p0 = (int32_t)v0.x;
-        if ((int64_t)len <= p0) { skip_done(0); break; }
-        if (len > 8) {
-          // entries B..B+7 around TT (TT - B in [4, 7]); PLCP[q] + q is
-          // non-decreasing, so if B is below TT every crossing lies in (B, TT]
-          const int64_t TT = (int64_t)pos + 1 + len;
-          const int64_t B = (TT & ~3ll) - 4;
-          const int32_t e[8] = {(int32_t)v2.x, (int32_t)v2.y, (int32_t)v2.z, (int32_t)v2.w,
-                                (int32_t)v3.x, (int32_t)v3.y, (int32_t)v3.z, (int32_t)v3.w};
-          if ((int64_t)e[0] + B < TT) {
-            uint32_t cc = 0;
+        // entries Wb..Wb+15 below TT; PLCP[q] + q is non-decreasing, so the
+        // window decides when it starts at or below pos+1 or below the exit
+        const int64_t TT = (int64_t)pos + 1 + len, q0 = (int64_t)pos + 1;
+        const int64_t Wb = TT >= 16 ? TT - 16 : 0;
+        const uint32_t e[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                                v4.x, v4.y, v4.z, v4.w, v5.x, v5.y, v5.z, v5.w};
+        if (Wb <= q0 || (int64_t)(int32_t)e[0] + Wb < TT) {
+          int64_t qc = TT;  // first crossing (TT itself always crosses)
 #pragma unroll
-            for (int k = 1; k < 8; k++) cc += (B + k < TT && (int64_t)e[k] + B + k < TT) ? 1u : 0u;
-            skip_done((uint32_t)(B + 1 + cc - ((int64_t)pos + 1)));
-            break;
+          for (int k = 15; k >= 0; k--) {
+            const int64_t q = Wb + k;
+            if (q >= q0 && q < TT && (int64_t)(int32_t)e[k] + q >= TT) qc = q;
           }
+          skip_done((uint32_t)(qc - q0));
+        } else {  // exit at or below Wb: PLCP[pos+1] first, then gallop
+          phase = PH_SKIP0;
+          ad0 = P + 4ull * (pos + 1);
+          use = U0D;
+          u2 = (int32_t)(Wb - q0);  // the predicate holds at s = Wb - (pos+1)
         }
+        break;
+      }
+      case PH_SKIP0: {
+        if ((int64_t)len <= (int64_t)(int32_t)v0.x) { skip_done(0); break; }
         u1 = 0;
         u4 = 1;
         skip_probe(true);
@@ -648,7 +660,7 @@ k_ms_walk2(Walk2Args A) {
         phase = PH_EXT_B;
         ad0 = (uintptr_t)(R.ld + lb + 1);
         ad2 = X + v0.x + len;
-        use = U0Q | U1Q | U2B;
+        use = U0Q | U1Q | U4Q | U5Q | U2B;
         break;
       }
       case PH_EXT_B: {
@@ -656,14 +668,15 @@ k_ms_walk2(Walk2Args A) {
         // first starts at lb with character x[SA[lb]+off], the others at each
         // k with LCP[k] == off with character D[k]
         const uint32_t c = (uint32_t)u0;
-        const uint32_t e[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+        const uint32_t e[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                                v4.x, v4.y, v4.z, v4.w, v5.x, v5.y, v5.z, v5.w};
         const int32_t S1 = rb - lb;
         bool valid = true;
         int32_t lo = -1, hi = -1, mm = rb + 1;
         uint32_t curChar = v2.x & 0xff;
         int32_t curStart = lb;
 #pragma unroll
-        for (int k = 0; k < 7; k++) {
+        for (int k = 0; k < 15; k++) {
           if (k < S1) {
             const uint32_t l = e[k] >> 8;
             if (l < len) valid = false;
