@@ -3,8 +3,8 @@
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH ?= gfx950
 SRC := cms-bwt_amd/csrc
-OUT := cms-bwt_amd/build
-HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-function
+OUT ?= cms-bwt_amd/build
+HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-function $(XFLAGS)
 HOSTFLAGS := -O3 -std=c++17 -fPIC -Wall
 
 OBJS := $(OUT)/engine.o $(OUT)/ms_walk.o $(OUT)/ms_walk2.o $(OUT)/merge.o $(OUT)/synth.o $(OUT)/host_index.o $(OUT)/host_reader.o

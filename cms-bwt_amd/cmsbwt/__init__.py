@@ -22,7 +22,8 @@ from dataclasses import dataclass, field
 from typing import Optional
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-_LIB_PATH = os.path.join(os.path.dirname(_HERE), "build", "libcmsbwt.so")
+# CMSBWT_LIB selects another build of the same library (A/B experiments)
+_LIB_PATH = os.environ.get("CMSBWT_LIB") or os.path.join(os.path.dirname(_HERE), "build", "libcmsbwt.so")
 
 CMSBWT_OK = 0
 CMSBWT_EIO = 1
