@@ -112,12 +112,16 @@ def main():
     c0, c1 = cdist.shard_range(args.copies, world, rank)
     eng.load_synth(args.seed, 1 + c0, c1 - c0, args.p, leading_empty_doc=(rank == 0))
     device = f"cuda:{local}"
+    gather = os.environ.get("CMSBWT_DIST", "sharded") == "gather"
+    xfer = cdist.Transport(device) if world > 1 else None
 
     def step():
         if world == 1:
             eng.step(rle=True)
-        else:
-            cdist.sharded_step(eng, device, rle=True)
+        elif gather:  # all heads to rank 0, single-GPU merge there
+            cdist.gather_step(eng, device, rle=True)
+        else:         # merge sharded by reference position (dist_merge.hip)
+            cdist.sharded_step(eng, device, rle=True, xfer=xfer)
 
     def barrier():
         torch.cuda.synchronize(local)
@@ -163,7 +167,10 @@ def main():
         "config": {"workload": f"{args.ref_len // 10**6} MB ref + {args.copies} copies @{args.p * 100:g}% SNP, -r",
                    "ref_len": args.ref_len, "copies": args.copies, "snp": args.p, "seed": args.seed,
                    "collection_bytes": chars_total, "heads": st.heads, "keys": st.keys, "runs": st.runs,
-                   "parallelism": (f"documents sharded over {world} GPUs, heads gathered to rank 0 over RCCL, merge on rank 0"
+                   "parallelism": ((f"documents sharded over {world} GPUs, heads gathered to rank 0 over RCCL, merge on rank 0"
+                                    if gather else
+                                    f"walk: documents sharded over {world} GPUs; merge: reference positions sharded, "
+                                    "all-to-all/all-reduce over RCCL, runs gathered to rank 0")
                                    if world > 1 else "1 GPU")},
         "roofline": {"bound": "hbm", "kernel": "k_ms_walk2", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),

@@ -81,6 +81,14 @@ def load_library() -> ctypes.CDLL:
         return _lib
     if not os.path.exists(_LIB_PATH):
         raise CmsBwtError(CMSBWT_EDEVICE, f"{_LIB_PATH} not built (run `make lib` or __graft_entry__.build())")
+    # One HIP runtime per process: PyTorch ships its own libamdhip64.so.7 /
+    # libhsa-runtime64.so.1 with the same sonames as /opt/rocm's.  Whichever
+    # loads first serves both, and torch cannot initialise the GPU on a
+    # runtime other than its own, so torch (when installed) goes first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = ctypes.CDLL(_LIB_PATH)
     P, U64, I32, VP = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p
     sig = {
@@ -105,6 +113,26 @@ def load_library() -> ctypes.CDLL:
                                               ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "cmsbwt_host_suffix_array": (I32, [VP, U64, VP]),
         "cmsbwt_walk_import": (I32, [P, U64, U64, U64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+        # position-sharded merge (device pointers; cmsbwt.dist drives the transport)
+        "cmsbwt_dm_begin": (I32, [P, ctypes.c_uint32, ctypes.c_uint32, U64, U64, ctypes.c_uint32, VP, VP, I32]),
+        "cmsbwt_dm_route_heads": (I32, [P, VP]),
+        "cmsbwt_dm_pack_heads": (I32, [P, VP]),
+        "cmsbwt_dm_group": (I32, [P, VP, U64, VP]),
+        "cmsbwt_dm_labels": (I32, [P, VP, VP]),
+        "cmsbwt_dm_dbl_init": (I32, [P, VP, ctypes.POINTER(U64)]),
+        "cmsbwt_dm_dbl_route": (I32, [P, U64, VP]),
+        "cmsbwt_dm_dbl_pack": (I32, [P, VP]),
+        "cmsbwt_dm_dbl_sort": (I32, [P, VP, U64, VP]),
+        "cmsbwt_dm_dbl_apply": (I32, [P, VP, ctypes.POINTER(U64)]),
+        "cmsbwt_dm_pack_ranks": (I32, [P, VP]),
+        "cmsbwt_dm_load_ranks": (I32, [P, VP]),
+        "cmsbwt_dm_route_halo": (I32, [P, VP, VP]),
+        "cmsbwt_dm_pack_halo": (I32, [P, VP, VP]),
+        "cmsbwt_dm_counter": (I32, [P, VP, U64, VP, U64, VP]),
+        "cmsbwt_dm_units": (I32, [P, VP]),
+        "cmsbwt_dm_emit": (I32, [P, VP, ctypes.POINTER(U64)]),
+        "cmsbwt_dm_copy_stream": (I32, [P, VP, VP]),
+        "cmsbwt_dm_finish": (I32, [P, ctypes.POINTER(VP), ctypes.POINTER(VP), VP, VP]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -120,6 +148,10 @@ EXPORTED = [
     "cmsbwt_load_collection", "cmsbwt_load_collection_synth", "cmsbwt_ms_walk", "cmsbwt_merge",
     "cmsbwt_step", "cmsbwt_get_stats", "cmsbwt_num_runs", "cmsbwt_copy_runs", "cmsbwt_write_output",
     "cmsbwt_copy_array", "cmsbwt_host_read_collection", "cmsbwt_host_suffix_array", "cmsbwt_walk_import",
+    "cmsbwt_dm_begin", "cmsbwt_dm_route_heads", "cmsbwt_dm_pack_heads", "cmsbwt_dm_group", "cmsbwt_dm_labels",
+    "cmsbwt_dm_dbl_init", "cmsbwt_dm_dbl_route", "cmsbwt_dm_dbl_pack", "cmsbwt_dm_dbl_sort", "cmsbwt_dm_dbl_apply",
+    "cmsbwt_dm_pack_ranks", "cmsbwt_dm_load_ranks", "cmsbwt_dm_route_halo", "cmsbwt_dm_pack_halo",
+    "cmsbwt_dm_counter", "cmsbwt_dm_units", "cmsbwt_dm_emit", "cmsbwt_dm_copy_stream", "cmsbwt_dm_finish",
 ]
 
 
@@ -248,6 +280,92 @@ class Engine:
         """Install merged walk results (pointers in WALK_ARRAYS order, host or device)."""
         arr = (ctypes.c_void_p * len(WALK_ARRAYS))(*[ctypes.c_void_p(p) for p in ptrs])
         self._chk(self._lib.cmsbwt_walk_import(self._ctx, heads, ndocs, chars, 1 if order_invariant else 0, arr))
+
+    # ---- position-sharded merge: thin wrappers, pointers are device addresses
+    # (ints, e.g. torch.Tensor.data_ptr()); see include/cmsbwt.h for the order
+    def _u64s(self, k):
+        return (ctypes.c_uint64 * k)()
+
+    def dm_begin(self, world, rank, heads_total, docs_total, order_invariant, diff_ptr, hashead_ptr, rle=True):
+        self._chk(self._lib.cmsbwt_dm_begin(self._ctx, world, rank, heads_total, docs_total,
+                                            1 if order_invariant else 0, ctypes.c_void_p(diff_ptr),
+                                            ctypes.c_void_p(hashead_ptr), 1 if rle else 0))
+
+    def dm_route_heads(self, world):
+        c = self._u64s(world)
+        self._chk(self._lib.cmsbwt_dm_route_heads(self._ctx, c))
+        return list(c)
+
+    def dm_pack_heads(self, out_ptr):
+        self._chk(self._lib.cmsbwt_dm_pack_heads(self._ctx, ctypes.c_void_p(out_ptr)))
+
+    def dm_group(self, recv_ptr, nrecv, sa_counts_ptr):
+        self._chk(self._lib.cmsbwt_dm_group(self._ctx, ctypes.c_void_p(recv_ptr), nrecv,
+                                            ctypes.c_void_p(sa_counts_ptr)))
+
+    def dm_labels(self, sa_counts_ptr, back_ptr):
+        self._chk(self._lib.cmsbwt_dm_labels(self._ctx, ctypes.c_void_p(sa_counts_ptr), ctypes.c_void_p(back_ptr)))
+
+    def dm_dbl_init(self, labels_ptr):
+        a = ctypes.c_uint64()
+        self._chk(self._lib.cmsbwt_dm_dbl_init(self._ctx, ctypes.c_void_p(labels_ptr), ctypes.byref(a)))
+        return a.value
+
+    def dm_dbl_route(self, h, world):
+        c = self._u64s(world)
+        self._chk(self._lib.cmsbwt_dm_dbl_route(self._ctx, h, c))
+        return list(c)
+
+    def dm_dbl_pack(self, out_ptr):
+        self._chk(self._lib.cmsbwt_dm_dbl_pack(self._ctx, ctypes.c_void_p(out_ptr)))
+
+    def dm_dbl_sort(self, recv_ptr, nrecv, res_ptr):
+        self._chk(self._lib.cmsbwt_dm_dbl_sort(self._ctx, ctypes.c_void_p(recv_ptr), nrecv, ctypes.c_void_p(res_ptr)))
+
+    def dm_dbl_apply(self, back_ptr):
+        a = ctypes.c_uint64()
+        self._chk(self._lib.cmsbwt_dm_dbl_apply(self._ctx, ctypes.c_void_p(back_ptr), ctypes.byref(a)))
+        return a.value
+
+    def dm_pack_ranks(self, out_ptr):
+        self._chk(self._lib.cmsbwt_dm_pack_ranks(self._ctx, ctypes.c_void_p(out_ptr)))
+
+    def dm_load_ranks(self, recv_ptr):
+        self._chk(self._lib.cmsbwt_dm_load_ranks(self._ctx, ctypes.c_void_p(recv_ptr)))
+
+    def dm_route_halo(self, world):
+        ic, wc = self._u64s(world), self._u64s(world)
+        self._chk(self._lib.cmsbwt_dm_route_halo(self._ctx, ic, wc))
+        return list(ic), list(wc)
+
+    def dm_pack_halo(self, hdr_ptr, words_ptr):
+        self._chk(self._lib.cmsbwt_dm_pack_halo(self._ctx, ctypes.c_void_p(hdr_ptr), ctypes.c_void_p(words_ptr)))
+
+    def dm_counter(self, hdr_ptr, nitems, words_ptr, nwords):
+        """-> [bad, good, nothing, violations, errors, items] of this rank."""
+        out = self._u64s(6)
+        self._chk(self._lib.cmsbwt_dm_counter(self._ctx, ctypes.c_void_p(hdr_ptr), nitems, ctypes.c_void_p(words_ptr),
+                                              nwords, out))
+        return list(out)
+
+    def dm_units(self, units_ptr):
+        self._chk(self._lib.cmsbwt_dm_units(self._ctx, ctypes.c_void_p(units_ptr)))
+
+    def dm_emit(self, units_ptr):
+        a = ctypes.c_uint64()
+        self._chk(self._lib.cmsbwt_dm_emit(self._ctx, ctypes.c_void_p(units_ptr), ctypes.byref(a)))
+        return a.value
+
+    def dm_copy_stream(self, starts_ptr, chars_ptr):
+        self._chk(self._lib.cmsbwt_dm_copy_stream(self._ctx, ctypes.c_void_p(starts_ptr), ctypes.c_void_p(chars_ptr)))
+
+    def dm_finish(self, start_ptrs, char_ptrs, counts, gstats):
+        k = len(counts)
+        sp = (ctypes.c_void_p * k)(*[ctypes.c_void_p(p) for p in start_ptrs])
+        cp = (ctypes.c_void_p * k)(*[ctypes.c_void_p(p) for p in char_ptrs])
+        cn = (ctypes.c_uint64 * k)(*counts)
+        gs = (ctypes.c_uint64 * len(gstats))(*gstats)
+        self._chk(self._lib.cmsbwt_dm_finish(self._ctx, sp, cp, cn, gs))
 
     def write_output(self, outname: str, rle: bool = True):
         self._chk(self._lib.cmsbwt_write_output(self._ctx, outname.encode(), 1 if rle else 0))

@@ -1,13 +1,22 @@
-"""Document-sharded multi-GPU execution.
+"""Multi-GPU execution.
 
 The MS walk and the j-scan are document-local (positions are per document,
 FN:1149; the j-scan stops at the end-of-document phrase, FN:1367-1370), so
 documents are sharded by contiguous ranges, one process per GPU.  The merge
-is global: rank 0 gathers every shard's head records in document order
-(= global idx order, because shards are contiguous and ordered), reduces the
-per-position difference arrays (sum) and head flags (max), imports them and
-runs the merge.  Transport is torch.distributed: RCCL ("nccl") over xGMI on
-MI355X, gloo for the CPU tests.
+is global; two ways to run it:
+
+* :func:`sharded_step` (default) — the merge sharded by reference position
+  (dist_merge.hip): heads go to the owner of their position (all-to-all), the
+  head-string suffix sort runs as distributed prefix doubling, counters and
+  writer units are computed per position range, and rank 0 only places the
+  runs every rank emitted and packs the records.
+* :func:`gather_step` — rank 0 gathers every shard's head records in document
+  order (= global idx order, shards being contiguous and ordered), reduces the
+  per-position difference arrays (sum) and head flags (max), imports them and
+  runs the single-GPU merge.
+
+Transport is torch.distributed: RCCL ("nccl") over xGMI on MI355X, gloo (host
+staging) for the CPU tests and for several ranks sharing one test GPU.
 """
 from __future__ import annotations
 
@@ -88,7 +97,7 @@ def import_walk(eng, combined: dict, totals):
     eng.walk_import(totals[0], totals[1], totals[2], ptrs, order_invariant=bool(totals[3]))
 
 
-def sharded_step(eng, device, rle: bool = True, root: int = 0):
+def gather_step(eng, device, rle: bool = True, root: int = 0):
     """One distributed step: local walk, gather, merge on root."""
     eng.ms_walk()
     st = eng.stats()
@@ -98,3 +107,179 @@ def sharded_step(eng, device, rle: bool = True, root: int = 0):
         import_walk(eng, combined, totals)
         eng.merge(rle)
     return totals
+
+
+# ---------------------------------------------------------------- sharded merge
+class Transport:
+    """Collectives on 1-D/2-D device tensors (dim-0 splits).  With gloo and
+    device tensors the data is staged through host memory; world == 1 needs no
+    process group (identity exchange)."""
+
+    def __init__(self, device, world=None, rank=None):
+        self.device = torch.device(device)
+        if world is None:
+            world, rank = (dist.get_world_size(), dist.get_rank()) if dist.is_initialized() else (1, 0)
+        self.world, self.rank = world, rank
+        self.staged = self.world > 1 and dist.get_backend() == "gloo" and self.device.type != "cpu"
+
+    def sync(self):
+        if self.device.type == "cuda":
+            torch.cuda.synchronize(self.device)
+
+    def empty(self, shape, dtype):
+        return torch.empty(shape, dtype=dtype, device=self.device)
+
+    def counts(self, send_counts):
+        """Per-destination counts -> per-source counts."""
+        if self.world == 1:
+            return list(send_counts)
+        t = torch.tensor(send_counts, dtype=torch.int64)
+        out = torch.empty_like(t)
+        if not self.staged and self.device.type != "cpu":
+            t, out = t.to(self.device), out.to(self.device)
+        dist.all_to_all_single(out, t)
+        return [int(x) for x in out.tolist()]
+
+    def a2a(self, send, send_counts, recv_counts):
+        if self.world == 1:
+            return send
+        shape = (sum(recv_counts),) + tuple(send.shape[1:])
+        if self.staged:
+            out = torch.empty(shape, dtype=send.dtype)
+            dist.all_to_all_single(out, send.cpu(), list(recv_counts), list(send_counts))
+            out = out.to(self.device)
+        else:
+            out = torch.empty(shape, dtype=send.dtype, device=send.device)
+            dist.all_to_all_single(out, send, list(recv_counts), list(send_counts))
+        self.sync()
+        return out
+
+    def allreduce(self, t, op="sum"):
+        if self.world == 1:
+            return t
+        rop = {"sum": dist.ReduceOp.SUM, "max": dist.ReduceOp.MAX}[op]
+        if self.staged:
+            c = t.cpu()
+            dist.all_reduce(c, op=rop)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, op=rop)
+        self.sync()
+        return t
+
+    def allgather_ints(self, vals):
+        """[per-rank list of ints] for a list of ints of equal length."""
+        if self.world == 1:
+            return [list(vals)]
+        t = torch.tensor(vals, dtype=torch.int64)
+        if not self.staged and self.device.type != "cpu":
+            t = t.to(self.device)
+        outs = [torch.empty_like(t) for _ in range(self.world)]
+        dist.all_gather(outs, t)
+        return [[int(x) for x in o.tolist()] for o in outs]
+
+
+def sharded_step(eng, device, rle: bool = True, xfer: Transport = None):
+    """One distributed step with the position-sharded merge (see module doc and
+    include/cmsbwt.h "Multi-GPU merge").  The runs end up on rank 0."""
+    eng.ms_walk()
+    return sharded_merge(eng, xfer or Transport(device), rle)
+
+
+def sharded_merge(eng, x: Transport, rle: bool = True):
+    from . import CMSBWT_EINPUT, CMSBWT_EORDER, CmsBwtError
+    world, rank = x.world, x.rank
+    st = eng.stats()
+    H, n = int(st.heads), int(st.n)
+    meta = x.allgather_ints([H, int(st.ndocs), int(st.chars), int(st.order_invariant)])
+    Htot = sum(m[0] for m in meta)
+    E = sum(m[1] for m in meta)
+    chars = sum(m[2] for m in meta)
+    inv = all(m[3] for m in meta)
+    i32, i64 = torch.int32, torch.int64
+    diff = x.empty(n + 1, i32)
+    hh = x.empty(n, torch.uint8)
+    x.sync()
+    eng.array_into("diff", diff.data_ptr())
+    eng.array_into("hashead", hh.data_ptr())
+    x.allreduce(diff, "sum")
+    x.allreduce(hh, "max")
+    eng.dm_begin(world, rank, Htot, E, inv, diff.data_ptr(), hh.data_ptr(), rle)
+    del diff, hh
+    # 1-2. heads to position owners; items; initial group labels
+    hc = eng.dm_route_heads(world)
+    send = x.empty((H, 5), i32)
+    eng.dm_pack_heads(send.data_ptr())
+    rc = x.counts(hc)
+    recv = x.a2a(send, hc, rc)
+    del send
+    Hp = sum(rc)
+    sa = x.empty(2 * n, i32)
+    eng.dm_group(recv.data_ptr(), Hp, sa.data_ptr())
+    del recv
+    x.allreduce(sa, "sum")
+    back = x.empty(Hp, i32)
+    eng.dm_labels(sa.data_ptr(), back.data_ptr())
+    del sa
+    labels = x.a2a(back, rc, hc)
+    U = eng.dm_dbl_init(labels.data_ptr())
+    del back, labels
+    # 3. prefix doubling of the head string
+    h = 1
+    while True:
+        tot = x.allgather_ints([U])
+        if sum(t[0] for t in tot) == 0:
+            break
+        c = eng.dm_dbl_route(h, world)
+        send = x.empty((U, 2), i32)
+        eng.dm_dbl_pack(send.data_ptr())
+        r = x.counts(c)
+        recv = x.a2a(send, c, r)
+        res = x.empty(sum(r), i32)
+        eng.dm_dbl_sort(recv.data_ptr(), sum(r), res.data_ptr())
+        back = x.a2a(res, r, c)
+        U = eng.dm_dbl_apply(back.data_ptr())
+        h *= 2
+    # 4. head ranks / next-head ranks to the position owners
+    ranks = x.empty((H, 2), i32)
+    eng.dm_pack_ranks(ranks.data_ptr())
+    rr = x.a2a(ranks, hc, rc)
+    eng.dm_load_ranks(rr.data_ptr())
+    del ranks, rr
+    # 5. counters with the halo of items reaching in from earlier ranks
+    ic, wc = eng.dm_route_halo(world)
+    hdr = x.empty((sum(ic), 6), i32)
+    words = x.empty(sum(wc), i32)
+    eng.dm_pack_halo(hdr.data_ptr(), words.data_ptr())
+    ric, rwc = x.counts(ic), x.counts(wc)
+    hin = x.a2a(hdr, ic, ric)
+    win = x.a2a(words, wc, rwc)
+    c6 = eng.dm_counter(hin.data_ptr(), sum(ric), win.data_ptr(), sum(rwc))
+    del hdr, words, hin, win
+    g = x.allgather_ints(c6)
+    bad, good, nothing, viol, errs, keys = [sum(v[k] for v in g) for k in range(6)]
+    if errs:
+        raise CmsBwtError(CMSBWT_EINPUT, "counter target beyond the reference (reference UB)")
+    if viol:
+        raise CmsBwtError(CMSBWT_EORDER, f"MatchInSet comparator is not a strict weak order on this input ({viol})")
+    # 6. writer units, emission, gather to rank 0
+    Uw = E + n - 1
+    units = x.empty(2 * Uw, i64)
+    eng.dm_units(units.data_ptr())
+    x.allreduce(units, "sum")
+    nloc = eng.dm_emit(units.data_ptr())
+    del units
+    starts = x.empty(nloc, i64)
+    chs = x.empty(nloc, torch.uint8)
+    eng.dm_copy_stream(starts.data_ptr(), chs.data_ptr())
+    counts = [v[0] for v in x.allgather_ints([nloc])]
+    sc = [nloc if k == 0 else 0 for k in range(world)]
+    rcv = counts if rank == 0 else [0] * world
+    gst = x.a2a(starts, sc, rcv)
+    gch = x.a2a(chs, sc, rcv)
+    if rank == 0:
+        offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        sp = [gst.data_ptr() + 8 * int(offs[k]) for k in range(world)]
+        cp = [gch.data_ptr() + int(offs[k]) for k in range(world)]
+        eng.dm_finish(sp, cp, counts, [Htot, keys, E, chars, bad, good, nothing, viol])
+    return Htot, E, chars

@@ -1,1145 +1,5 @@
-// engine.hip — host orchestration of the CMS-BWT hot path on one MI355X, and
-// the C ABI of include/cmsbwt.h.
-//
-// Stage map (reference = CMS-BWT-functions.cpp, "FN"):
-//   load_reference ... FN:151-310  (host SA-IS + LCP, staged into HBM)
-//   load_collection .. FN:1138-1275 (reader) -> text + doc offsets in HBM
-//   ms_walk .......... FN:1151-1212 walk (k_ms_walk), FN:1359-1385 j-scan
-//   merge ............ FN:1387-1416 grouping (radix sorts), FN:1432-1494 ranks
-//                      + suffix sort of the head string (prefix doubling),
-//                      FN:1504-1603 counters, FN:1618-1777 inversion + runs
-#include <stdarg.h>
-#include <stdio.h>
-#include <string.h>
-#include <cstring>
-
-#include <hip/hip_runtime.h>
-#include <rocprim/rocprim.hpp>
-
-#include <algorithm>
-#include <chrono>
-#include <fstream>
-#include <map>
-#include <string>
-#include <unordered_map>
-#include <vector>
-
-#include "../../include/cmsbwt.h"
-#include "device_common.h"
-#include "host_index.h"
-#include "host_reader.h"
-#include "kernels.h"
-#include "merge_kernels.h"
-#include "synth.h"
-
-namespace cmsbwt {
-
-struct IsActive {  // an unresolved member's sa position (0xffffffff = resolved)
-  __host__ __device__ bool operator()(uint32_t v) const { return v != 0xffffffffu; }
-};
-struct LastNonEmpty {  // scan operator: the later non-empty unit's (has, last, first) wins
-  __host__ __device__ uint32_t operator()(uint32_t a, uint32_t b) const { return (b >> 16) ? b : a; }
-};
-struct WidenU64 {
-  __host__ __device__ uint64_t operator()(uint32_t v) const { return (uint64_t)v; }
-};
-
-struct HipError {
-  std::string msg;
-};
-
-#define HIPCHK(x)                                                                              \
-  do {                                                                                         \
-    hipError_t e_ = (x);                                                                       \
-    if (e_ != hipSuccess)                                                                      \
-      throw HipError{std::string(#x) + " -> " + hipGetErrorString(e_) + " @" + std::to_string(__LINE__)}; \
-  } while (0)
-
-struct InputError {
-  int code;
-  std::string msg;
-};
-
-// Caching device allocator: the step allocates the same sequence of buffers
-// every time, so blocks are kept after release and handed back on the next
-// request of a similar size (all work runs on one stream, so stream order
-// makes reuse safe).  hipMalloc/hipFree of multi-GB buffers otherwise cost
-// tens of milliseconds per step.
-struct DevAlloc {
-  std::multimap<uint64_t, void*> freeBlocks;
-  std::unordered_map<void*, uint64_t> sizes;
-  uint64_t cached = 0;
-  uint64_t limit = 96ull << 30;
-  void* get(uint64_t bytes) {
-    bytes = (std::max<uint64_t>(bytes, 64) + 255) & ~255ull;
-    auto it = freeBlocks.lower_bound(bytes);
-    if (it != freeBlocks.end() && it->first <= bytes + bytes / 4 + (4u << 20)) {
-      void* p = it->second;
-      cached -= it->first;
-      freeBlocks.erase(it);
-      return p;
-    }
-    void* p = nullptr;
-    if (hipMalloc(&p, bytes) != hipSuccess) {
-      (void)hipGetLastError();
-      trim();
-      HIPCHK(hipMalloc(&p, bytes));
-    }
-    sizes[p] = bytes;
-    return p;
-  }
-  void put(void* p) {
-    auto s = sizes.find(p);
-    if (s == sizes.end()) { (void)hipFree(p); return; }
-    freeBlocks.emplace(s->second, p);
-    cached += s->second;
-    if (cached > limit) trim();
-  }
-  void trim() {
-    (void)hipDeviceSynchronize();
-    for (auto& kv : freeBlocks) {
-      sizes.erase(kv.second);
-      (void)hipFree(kv.second);
-    }
-    freeBlocks.clear();
-    cached = 0;
-  }
-  ~DevAlloc() {
-    trim();
-    for (auto& kv : sizes) (void)hipFree(kv.first);
-  }
-};
-static thread_local DevAlloc* g_alloc = nullptr;
-
-template <class T>
-struct DBuf {
-  T* p = nullptr;
-  uint64_t n = 0;
-  DevAlloc* owner = nullptr;
-  DBuf() = default;
-  DBuf(const DBuf&) = delete;
-  DBuf& operator=(const DBuf&) = delete;
-  ~DBuf() { release(); }
-  void alloc(uint64_t k) {
-    release();
-    n = k;
-    if (!k) return;
-    owner = g_alloc;
-    if (owner) p = (T*)owner->get(k * sizeof(T));
-    else HIPCHK(hipMalloc((void**)&p, std::max<uint64_t>(k * sizeof(T), 64)));
-  }
-  void zero(hipStream_t st) { if (n) HIPCHK(hipMemsetAsync(p, 0, n * sizeof(T), st)); }
-  void release() {
-    if (p) {
-      if (owner) owner->put(p);
-      else (void)hipFree(p);
-    }
-    p = nullptr;
-    n = 0;
-    owner = nullptr;
-  }
-  uint64_t bytes() const { return n * sizeof(T); }
-};
-
-static uint32_t env_u32(const char* name, uint32_t dflt) {
-  const char* v = getenv(name);
-  return v ? (uint32_t)strtoul(v, nullptr, 10) : dflt;
-}
-
-static int bits_for(uint64_t v) {  // bits to represent values in [0, v]
-  int b = 1;
-  while (b < 64 && (v >> b)) b++;
-  return b;
-}
-
-struct Engine {
-  DevAlloc alloc;  // first member: destroyed last
-  int device = 0;
-  hipStream_t st = nullptr;
-  std::string err;
-  cmsbwt_stats stats{};
-
-  // ---- reference
-  bool refLoaded = false;
-  HostIndex hix;
-  DBuf<uint8_t> dx, dbwt;
-  DBuf<int32_t> dsa, dlcp, dplcp;
-  DBuf<uint32_t> disa;
-  DBuf<int2> dkmer;
-  DBuf<uint32_t> dld;
-  DBuf<uint8_t> dkmap;
-  DevRef R{};
-
-  // ---- collection
-  bool collLoaded = false;
-  DBuf<uint8_t> dtext;
-  DBuf<uint64_t> ddoc;
-  std::vector<uint64_t> hdoc;  // doc offsets (ndocs+1), doc k = [hdoc[k], hdoc[k+1]-1)
-  uint64_t ndocs = 0, chars = 0, sn = 0;
-  uint64_t collChars = 0;  // chars of the loaded collection (ms_walk input)
-
-  // ---- walk outputs
-  bool walked = false;
-  uint32_t H = 0;
-  DBuf<uint32_t> hStart, hPos, hLen, hIsa, hTonext;
-  DBuf<uint8_t> hSmall, hChar;
-  DBuf<uint16_t> hNext;
-  DBuf<int32_t> diff;
-  DBuf<uint8_t> hasHead;
-
-  // ---- merge outputs (kept for parity copies)
-  bool merged = false;
-  uint32_t K = 0;
-  DBuf<int32_t> T;
-  DBuf<uint32_t> saT;
-  DBuf<uint8_t> bwtHeads;
-  DBuf<unsigned long long> counter;
-  DBuf<int64_t> bucket;
-  DBuf<uint8_t> runs;
-  uint64_t nruns = 0;
-  int lastRle = 1;
-  DBuf<uint8_t> tmp;  // rocPRIM scratch
-
-  hipEvent_t ev0 = nullptr, ev1 = nullptr;
-
-  explicit Engine(int dev) : device(dev) {
-    g_alloc = &alloc;
-    HIPCHK(hipSetDevice(dev));
-    HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-    HIPCHK(hipEventCreate(&ev0));
-    HIPCHK(hipEventCreate(&ev1));
-  }
-  ~Engine() {
-    g_alloc = &alloc;
-    if (ev0) (void)hipEventDestroy(ev0);
-    if (ev1) (void)hipEventDestroy(ev1);
-    if (st) (void)hipStreamDestroy(st);
-  }
-
-  void* scratch(size_t bytes) {
-    if (tmp.n < bytes) tmp.alloc(bytes + (bytes >> 3) + 256);
-    return tmp.p;
-  }
-  void sync() { HIPCHK(hipStreamSynchronize(st)); }
-
-  template <class T_>
-  T_ read1(const T_* d) {
-    T_ v;
-    HIPCHK(hipMemcpyAsync(&v, d, sizeof(T_), hipMemcpyDeviceToHost, st));
-    sync();
-    return v;
-  }
-
-  // ---- rocPRIM helpers
-  template <class In, class Out, class Init, class Op>
-  void exscan(In in, Out out, Init init, uint64_t n, Op op) {
-    if (!n) return;
-    size_t b = 0;
-    HIPCHK(rocprim::exclusive_scan(nullptr, b, in, out, init, (size_t)n, op, st));
-    HIPCHK(rocprim::exclusive_scan(scratch(b), b, in, out, init, (size_t)n, op, st));
-  }
-  template <class In, class Out, class Init>
-  void exscan(In in, Out out, Init init, uint64_t n) {
-    if (!n) return;
-    size_t b = 0;
-    HIPCHK(rocprim::exclusive_scan(nullptr, b, in, out, init, (size_t)n, rocprim::plus<Init>(), st));
-    HIPCHK(rocprim::exclusive_scan(scratch(b), b, in, out, init, (size_t)n, rocprim::plus<Init>(), st));
-  }
-  template <class In, class Out, class Op>
-  void inscan(In in, Out out, uint64_t n, Op op) {
-    if (!n) return;
-    size_t b = 0;
-    HIPCHK(rocprim::inclusive_scan(nullptr, b, in, out, (size_t)n, op, st));
-    HIPCHK(rocprim::inclusive_scan(scratch(b), b, in, out, (size_t)n, op, st));
-  }
-  template <class Kt, class Vt>
-  void sort_pairs(const Kt* kin, Kt* kout, const Vt* vin, Vt* vout, uint64_t n, int bits) {
-    if (!n) return;
-    size_t b = 0;
-    HIPCHK(rocprim::radix_sort_pairs(nullptr, b, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, st));
-    HIPCHK(rocprim::radix_sort_pairs(scratch(b), b, kin, kout, vin, vout, (size_t)n, 0u, (unsigned)bits, st));
-  }
-  template <class Kt>
-  void sort_keys(const Kt* kin, Kt* kout, uint64_t n, int bits) {
-    if (!n) return;
-    size_t b = 0;
-    HIPCHK(rocprim::radix_sort_keys(nullptr, b, kin, kout, (size_t)n, 0u, (unsigned)bits, st));
-    HIPCHK(rocprim::radix_sort_keys(scratch(b), b, kin, kout, (size_t)n, 0u, (unsigned)bits, st));
-  }
-  uint32_t select_flagged_u64(const unsigned long long* in, const uint32_t* flags, unsigned long long* out,
-                              uint32_t n) {
-    if (!n) return 0;
-    DBuf<uint32_t> cnt;
-    cnt.alloc(1);
-    size_t b = 0;
-    HIPCHK(rocprim::select(nullptr, b, in, flags, out, cnt.p, (size_t)n, st));
-    HIPCHK(rocprim::select(scratch(b), b, in, flags, out, cnt.p, (size_t)n, st));
-    return read1(cnt.p);
-  }
-  uint32_t max_u32(const uint32_t* in, uint64_t n) {
-    if (!n) return 0;
-    DBuf<uint32_t> out;
-    out.alloc(1);
-    size_t b = 0;
-    HIPCHK(rocprim::reduce(nullptr, b, in, out.p, 0u, (size_t)n, rocprim::maximum<uint32_t>(), st));
-    HIPCHK(rocprim::reduce(scratch(b), b, in, out.p, 0u, (size_t)n, rocprim::maximum<uint32_t>(), st));
-    return read1(out.p);
-  }
-  uint32_t select_flagged(const uint32_t* in, const uint32_t* flags, uint32_t* out, uint32_t n) {
-    if (!n) return 0;
-    DBuf<uint32_t> cnt;
-    cnt.alloc(1);
-    size_t b = 0;
-    HIPCHK(rocprim::select(nullptr, b, in, flags, out, cnt.p, (size_t)n, st));
-    HIPCHK(rocprim::select(scratch(b), b, in, flags, out, cnt.p, (size_t)n, st));
-    return read1(cnt.p);
-  }
-
-  // =====================================================================
-  // reference (FN:151-310)
-  void load_reference_bytes(const std::string& trimmed) {
-    auto t0 = std::chrono::steady_clock::now();
-    for (unsigned char c : trimmed)
-      if (c == 2) throw InputError{CMSBWT_EINPUT, "reference contains byte 0x02 (the document separator)"};
-    if (trimmed.size() + 130 >= (1ull << 31)) throw InputError{CMSBWT_ELIMIT, "reference longer than 2^31 (int32 SA)"};
-    build_index(trimmed, hix);
-    const uint32_t n = hix.n;
-    // Skip-search precondition: PLCP[q] + q non-decreasing.
-    for (uint32_t q = 0; q + 1 < n; q++)
-      if ((int64_t)hix.plcp[q + 1] + 1 < (int64_t)hix.plcp[q])
-        throw InputError{CMSBWT_EINPUT, "internal: PLCP monotonicity violated"};
-    dx.alloc((uint64_t)n + kTextPad);
-    HIPCHK(hipMemsetAsync(dx.p, 0, n + kTextPad, st));
-    HIPCHK(hipMemcpyAsync(dx.p, hix.x.data(), n, hipMemcpyHostToDevice, st));
-    // +16 entries: the uniform-step walk loads whole aligned 16-B blocks (and
-    // 8-entry windows) around an index, so arrays carry a readable tail
-    dsa.alloc((uint64_t)n + 16);
-    HIPCHK(hipMemcpyAsync(dsa.p, hix.sa.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
-    disa.alloc((uint64_t)n + 16);
-    HIPCHK(hipMemcpyAsync(disa.p, hix.isa.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
-    dplcp.alloc((uint64_t)n + 17);
-    HIPCHK(hipMemcpyAsync(dplcp.p, hix.plcp.data(), (size_t)n * 4, hipMemcpyHostToDevice, st));
-    dbwt.alloc(n);
-    HIPCHK(hipMemcpyAsync(dbwt.p, hix.bwt.data(), n, hipMemcpyHostToDevice, st));
-    // LCP and its block-minima levels in one buffer: [lcp | lvl0 | lvl1 ...],
-    // each part 16-B aligned with >= 16 readable entries of tail
-    memset(&R, 0, sizeof(R));
-    std::vector<std::vector<int32_t>> levels;
-    {
-      std::vector<int32_t> prev(hix.lcp.begin(), hix.lcp.begin() + n), cur;
-      do {
-        cur.assign((prev.size() + 63) / 64, INT32_MAX);
-        for (size_t i = 0; i < prev.size(); i++) cur[i / 64] = std::min(cur[i / 64], prev[i]);
-        levels.push_back(cur);
-        prev.swap(cur);
-      } while (prev.size() > 64 && (int)levels.size() < kMaxLevels);
-    }
-    auto pad = [](uint64_t k) { return (k + 16 + 3) & ~3ull; };
-    uint64_t total = pad((uint64_t)n + 1);
-    for (auto& v : levels) total += pad(v.size());
-    dlcp.alloc(total);
-    HIPCHK(hipMemcpyAsync(dlcp.p, hix.lcp.data(), ((size_t)n + 1) * 4, hipMemcpyHostToDevice, st));
-    uint64_t off = pad((uint64_t)n + 1);
-    int L = 0;
-    for (auto& v : levels) {
-      HIPCHK(hipMemcpyAsync(dlcp.p + off, v.data(), v.size() * 4, hipMemcpyHostToDevice, st));
-      R.lvl[L] = dlcp.p + off;
-      R.lvlOff[L] = (uint32_t)off;
-      R.lvlLen[L] = (uint32_t)v.size();
-      off += pad(v.size());
-      L++;
-    }
-    sync();  // `levels` is pageable host memory
-    R.nlvl = L;
-    R.x = dx.p;
-    R.sa = dsa.p;
-    R.isa = disa.p;
-    R.lcp = dlcp.p;
-    R.plcp = dplcp.p;
-    R.bwt = dbwt.p;
-    R.n = n;
-    build_kmer_table();
-    build_child_table();
-    sync();
-    refLoaded = true;
-    stats.n = n;
-    stats.t_index_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  }
-
-  // Restart table of the uniform-step walk: a chunk restart at the SA root
-  // (K extensions by binary search, ~2 K log n dependent loads) becomes one
-  // table lookup when the K text bytes are all reference bytes and the K-mer
-  // occurs.  The table is exactly the SA range of each K-prefix, i.e. the
-  // state computeMSFactorAt (FN:45-88) reaches after K matched characters.
-  void build_kmer_table() {
-    R.kmer = nullptr;
-    R.kmap = nullptr;
-    R.kmerK = R.kmerB = 0;
-    if (!env_u32("CMSBWT_KMER", 1)) return;
-    const uint32_t n = hix.n;
-    uint64_t cnt[256] = {0};
-    for (uint64_t k = 0; k < hix.ref_len; k++) cnt[(uint8_t)hix.x[k]]++;
-    std::vector<uint8_t> map(256, 0xff);
-    uint32_t sigma = 0;
-    for (int c = 0; c < 256; c++)
-      if (cnt[c]) map[c] = (uint8_t)sigma++;
-    if (sigma < 2 || sigma > 64) return;
-    uint32_t B = 1;
-    while ((1u << B) < sigma) B++;
-    uint32_t lg = 1;
-    while ((1ull << lg) < n) lg++;
-    const uint32_t maxBits = std::min<uint32_t>(env_u32("CMSBWT_KMER_BITS", 24), std::max<uint32_t>(lg + 1, 12));
-    const uint32_t K = std::min<uint32_t>(maxBits / B, 16);
-    if (K < 3) return;
-    const uint64_t entries = 1ull << (B * K);
-    std::vector<int2> tab(entries + 2, make_int2(1, 0));
-    for (uint32_t i = 0; i < n; i++) {
-      const uint32_t s0 = (uint32_t)hix.sa[i];
-      if ((uint64_t)s0 + K > n) continue;
-      uint64_t code = 0;
-      bool ok = true;
-      for (uint32_t d = 0; d < K && ok; d++) {
-        const uint8_t m = map[(uint8_t)hix.x[s0 + d]];
-        ok = m != 0xff;
-        code = (code << B) | m;
-      }
-      if (!ok) continue;
-      int2& e = tab[code];
-      if (e.x > e.y) e = make_int2((int)i, (int)i);
-      else e.y = (int)i;  // SA order: ranges of one K-prefix are contiguous
-    }
-    dkmer.alloc(entries + 2);
-    HIPCHK(hipMemcpyAsync(dkmer.p, tab.data(), (entries + 2) * sizeof(int2), hipMemcpyHostToDevice, st));
-    dkmap.alloc(256);
-    HIPCHK(hipMemcpyAsync(dkmap.p, map.data(), 256, hipMemcpyHostToDevice, st));
-    sync();  // `tab` and `map` are pageable
-    R.kmer = dkmer.p;
-    R.kmap = dkmap.p;
-    R.kmerK = K;
-    R.kmerB = B;
-  }
-
-  // Child table of the uniform-step walk: ld[k] packs LCP[k] (clipped to 24
-  // bits) with D[k] = x[SA[k] + LCP[k]], the first character in which suffix
-  // SA[k] differs from SA[k-1].  Inside an lcp-interval of depth off, the
-  // children start at lb and at every k with LCP[k] == off, and D[k] is the
-  // child's character, so one character of computeMSFactorAt over a small
-  // interval needs one window of ld instead of two binary searches.
-  void build_child_table() {
-    R.ld = nullptr;
-    if (!env_u32("CMSBWT_EXT8", 1)) return;
-    const uint32_t n = hix.n;
-    std::vector<uint32_t> ld((size_t)n + 16, 0);
-    for (uint32_t k = 1; k < n; k++) {
-      const uint32_t l = (uint32_t)std::max<int32_t>(hix.lcp[k], 0);
-      const uint64_t at = (uint64_t)(uint32_t)hix.sa[k] + l;
-      const uint8_t d = at < n ? (uint8_t)hix.x[at] : 0;
-      ld[k] = (std::min<uint32_t>(l, 0xffffffu) << 8) | d;
-    }
-    dld.alloc((uint64_t)n + 16);
-    HIPCHK(hipMemcpyAsync(dld.p, ld.data(), ((size_t)n + 16) * 4, hipMemcpyHostToDevice, st));
-    sync();  // `ld` is pageable
-    R.ld = dld.p;
-  }
-
-  // =====================================================================
-  // collection
-  void check_bytes(const uint8_t* p, uint64_t len) {
-    for (uint64_t i = 0; i < len; i++)
-      if (!hix.present[p[i]])
-        throw InputError{CMSBWT_EINPUT, "collection byte " + std::to_string((int)p[i]) +
-                                            " does not occur in the reference (reference behaviour undefined)"};
-  }
-  void reset_collection() {
-    collLoaded = walked = merged = false;
-    plan.valid = false;
-    H = K = 0;
-  }
-  void upload_collection(const Collection& c) {
-    if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
-    auto t0 = std::chrono::steady_clock::now();
-    reset_collection();
-    for (uint64_t d = 0; d < c.ndocs(); d++) {
-      uint64_t len = c.off[d + 1] - c.off[d] - 1;
-      if (len >= (1ull << 32) - 1) throw InputError{CMSBWT_ELIMIT, "document longer than 2^32 (uint32 positions)"};
-      check_bytes(c.text.data() + c.off[d], len);
-    }
-    dtext.alloc(c.text.size() + kTextPad);
-    HIPCHK(hipMemsetAsync(dtext.p + c.text.size(), kSep, kTextPad, st));
-    if (!c.text.empty()) HIPCHK(hipMemcpyAsync(dtext.p, c.text.data(), c.text.size(), hipMemcpyHostToDevice, st));
-    hdoc = c.off;
-    ddoc.alloc(hdoc.size());
-    HIPCHK(hipMemcpyAsync(ddoc.p, hdoc.data(), hdoc.size() * 8, hipMemcpyHostToDevice, st));
-    sync();
-    ndocs = c.ndocs();
-    chars = collChars = c.chars;
-    sn = c.sn;
-    collLoaded = true;
-    stats.t_upload_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  }
-  void load_synth(uint64_t seed, uint64_t copy_begin, uint64_t ncopies, double p, int leadingEmpty) {
-    if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
-    reset_collection();
-    // the reference must be the synthetic reference of the same seed: its
-    // trimmed length is n - (augmentation) ; recover L from the stored x.
-    const uint64_t L = hix.ref_len;
-    for (uint64_t k = 0; k < std::min<uint64_t>(L, 4096); k++)
-      if ((uint8_t)hix.x[k] != (uint8_t)synth_acgt(synth_base_code(seed, k)))
-        throw InputError{CMSBWT_EARG, "loaded reference is not the synthetic reference of this seed"};
-    uint64_t base = leadingEmpty ? 1 : 0;
-    uint64_t total = base + ncopies * (L + 1);
-    dtext.alloc(total + kTextPad);
-    HIPCHK(hipMemsetAsync(dtext.p, kSep, total + kTextPad, st));
-    launch_synth_collection(dtext.p, L, seed, copy_begin, ncopies, synth_threshold(p), base, st);
-    HIPCHK(hipGetLastError());
-    hdoc.clear();
-    hdoc.push_back(0);
-    if (leadingEmpty) hdoc.push_back(1);
-    for (uint64_t d = 0; d < ncopies; d++) hdoc.push_back(base + (d + 1) * (L + 1));
-    ddoc.alloc(hdoc.size());
-    HIPCHK(hipMemcpyAsync(ddoc.p, hdoc.data(), hdoc.size() * 8, hipMemcpyHostToDevice, st));
-    sync();
-    ndocs = hdoc.size() - 1;
-    chars = collChars = ncopies * L;
-    sn = total;
-    collLoaded = true;
-  }
-
-  // =====================================================================
-  // MS walk + head finalisation
-  // CMSBWT_WALK=1 selects the per-lane walk (k_ms_walk); default is the
-  // uniform-step walk (k_ms_walk2) over a chunk queue.
-  static bool walk_v1() { return env_u32("CMSBWT_WALK", 2) == 1; }
-  static uint32_t walk_lanes() { return std::max<uint32_t>(256, env_u32("CMSBWT_WALK_LANES", 256u * 32 * 64)); }
-
-  uint32_t chunk_size() const {
-    if (const char* e = getenv("CMSBWT_CHUNK")) return (uint32_t)std::max(64L, atol(e));
-    if (!walk_v1()) {  // queue-fed: ~1 chunk per lane (restarts cost; measured best at 16 K)
-      uint64_t c = chars / (uint64_t)walk_lanes();
-      return (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(16384, c));
-    }
-    uint64_t c = chars / (256ull * 64 * 64);
-    c = std::max<uint64_t>(2048, std::min<uint64_t>(32768, c));
-    return (uint32_t)c;
-  }
-
-  void ms_walk() {
-    if (!collLoaded) throw InputError{CMSBWT_EARG, "load a collection first"};
-    auto t0 = std::chrono::steady_clock::now();
-    walked = merged = false;
-    ndocs = hdoc.size() - 1;  // walk_import may have replaced these with merged totals
-    chars = collChars;
-    const uint32_t C = chunk_size();
-    if (!plan.valid || plan.C != C) build_plan(C);
-    const uint32_t nch = plan.nch;
-    DBuf<uint32_t> chunkCount, used, nextChunk;
-    chunkCount.alloc(nch);
-    used.alloc(1);
-    nextChunk.alloc(16 * 8);
-    const bool v1 = walk_v1();
-    DBuf<unsigned long long> w2stats;  // CMSBWT_W2_STATS=1: step counts of the uniform-step walk
-    if (!v1 && env_u32("CMSBWT_W2_STATS", 0)) {
-      w2stats.alloc(32);
-      w2stats.zero(st);
-    }
-    // pool sized for ~3% heads + one partial block per chunk; grown on overflow
-    uint64_t cap = (uint64_t)nch + chars / 32 / kPoolB + 1024;
-    DBuf<HeadRec> rec;
-    DBuf<uint32_t> blkChunk, blkSeq;
-    uint32_t usedBlocks = 0;
-    while (true) {
-      if (cap > 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "head pool exceeds 2^32 blocks"};
-      rec.alloc(cap * kPoolB);
-      blkChunk.alloc(cap);
-      blkSeq.alloc(cap);
-      used.zero(st);
-      nextChunk.zero(st);
-      Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
-      HIPCHK(hipEventRecord(ev0, st));
-      if (v1) launch_ms_walk(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.laneChunk.p, pool, chunkCount.p, st);
-      else launch_ms_walk2(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.bandOrder.p, plan.bandStart.p, plan.nbands,
-                           nextChunk.p, pool, chunkCount.p, walk_lanes(), w2stats.p, st);
-      HIPCHK(hipGetLastError());
-      HIPCHK(hipEventRecord(ev1, st));
-      usedBlocks = read1(used.p);
-      float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, ev0, ev1));
-      stats.ms_walk_kernel_ms = ms;
-      if (usedBlocks <= cap) break;
-      cap = (uint64_t)usedBlocks + (uint64_t)nch + 1024;
-    }
-    if (w2stats.p) {
-      static const char* names[32] = {"done", "next", "bs_text", "bs_sa", "bs_x", "fail_sa", "lce_sa", "lce",
-                                       "skip1", "skip0", "gallop", "skipbs", "isa1", "con1", "con2", "adj",
-                                       "kmer_text", "kmer_tab", "ext_a", "ext_b", "lce_coop", "c_adj0", "c_adv",
-                                       "c_post", "c_char", "-", "scan0", "scan1", "scan2", "scan3", "wave_steps",
-                                       "coop_steps"};
-      std::vector<unsigned long long> h(32);
-      HIPCHK(hipMemcpy(h.data(), w2stats.p, 32 * 8, hipMemcpyDeviceToHost));
-      for (int k = 0; k < 32; k++)
-        if (h[k]) fprintf(stderr, "[w2stats] %-10s %llu\n", names[k] ? names[k] : "?", h[k]);
-    }
-    // chunk bases (end phrase counted in the last chunk of each document)
-    DBuf<unsigned long long> withEnd, chunkBase;
-    withEnd.alloc(nch);
-    chunkBase.alloc(nch);
-    launch_chunk_with_end(plan.dch.p, chunkCount.p, nch, withEnd.p, st);
-    exscan(withEnd.p, chunkBase.p, 0ull, nch);
-    {
-      const unsigned long long tot = read1(chunkBase.p + (nch - 1)) + read1(withEnd.p + (nch - 1));
-      if (tot >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^31-1 heads (int32 ranks, FN:1436)"};
-      H = (uint32_t)tot;
-    }
-    hStart.alloc(H); hPos.alloc(H); hLen.alloc(H); hIsa.alloc(H); hTonext.alloc(H);
-    hSmall.alloc(H); hChar.alloc(H); hNext.alloc(H);
-    HeadsSoA h = heads();
-    Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
-    DBuf<uint32_t> hDoc;  // document of each head (finalize)
-    hDoc.alloc(H);
-    launch_scatter_heads(pool, usedBlocks, chunkCount.p, chunkBase.p, h, plan.dch.p, dtext.p, ddoc.p, hDoc.p, st);
-    DBuf<uint32_t> docEnd;
-    docEnd.alloc(ndocs);
-    launch_end_phrases(dtext.p, ddoc.p, (uint32_t)ndocs, plan.dLast.p, chunkCount.p, chunkBase.p, R.n, h, docEnd.p,
-                       hDoc.p, st);
-    diff.alloc((uint64_t)R.n + 1);
-    diff.zero(st);
-    hasHead.alloc(R.n);
-    hasHead.zero(st);
-    DBuf<uint32_t> errf;
-    errf.alloc(1);
-    errf.zero(st);
-    launch_finalize(R, h, H, docEnd.p, (uint32_t)ndocs, dtext.p, ddoc.p, diff.p, hasHead.p, errf.p, hDoc.p, st);
-    HIPCHK(hipGetLastError());
-    uint32_t ef = read1(errf.p);
-    orderInvariant = (ef & 8u) == 0;
-    if (ef & 1) throw InputError{CMSBWT_EINPUT, "internal: match ends not monotone inside a document"};
-    if (ef & 6) throw InputError{CMSBWT_EINPUT, "isaNext/run index outside the reference (reference UB)"};
-    walked = true;
-    stats.order_invariant = orderInvariant ? 1 : 0;
-    stats.heads = H;
-    stats.ndocs = ndocs;
-    stats.chars = chars;
-    stats.sn = sn;
-    stats.t_ms_walk_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  }
-
-  // Restart chunks of the loaded collection; rebuilt when the collection or
-  // the chunk size changes.
-  struct ChunkPlan {
-    bool valid = false;
-    uint32_t C = 0, nch = 0;
-    DBuf<Chunk> dch;
-    DBuf<uint32_t> dLast, laneChunk;
-    DBuf<uint32_t> bandOrder, bandStart;  // uniform-step walk: chunks grouped by offset band
-    uint32_t nbands = 1;
-  } plan;
-
-  void build_plan(uint32_t C) {
-    std::vector<Chunk> chunks;
-    std::vector<uint32_t> lastChunk(ndocs), firstChunk(ndocs);
-    uint32_t maxc = 0;
-    for (uint64_t d = 0; d < ndocs; d++) {
-      uint64_t L = hdoc[d + 1] - hdoc[d] - 1;
-      uint64_t nc = std::max<uint64_t>(1, (L + C - 1) / C);
-      firstChunk[d] = (uint32_t)chunks.size();
-      for (uint64_t k = 0; k < nc; k++) {
-        Chunk ch;
-        ch.doc = (uint32_t)d;
-        ch.a = (uint32_t)(k * C);
-        ch.b = (uint32_t)std::min<uint64_t>(L, (k + 1) * C);
-        ch.last = k + 1 == nc;
-        chunks.push_back(ch);
-      }
-      lastChunk[d] = (uint32_t)chunks.size() - 1;
-      maxc = std::max<uint32_t>(maxc, (uint32_t)nc);
-    }
-    const uint32_t nch = (uint32_t)chunks.size();
-    // Lane order: document-major by default.  CMSBWT_OFFSET_MAJOR=1 puts the
-    // same offset of consecutive documents in one wave (shared reference
-    // lines, but same-offset text of equal-length copies collides in memory
-    // channels; measured slower on the benchmark).
-    std::vector<uint32_t> order(nch);
-    if (!env_u32("CMSBWT_OFFSET_MAJOR", 0)) {
-      for (uint32_t c = 0; c < nch; c++) order[c] = c;
-    } else {
-      uint32_t o = 0;
-      for (uint32_t k = 0; k < maxc; k++)
-        for (uint64_t d = 0; d < ndocs; d++)
-          if (firstChunk[d] + k <= lastChunk[d]) order[o++] = firstChunk[d] + k;
-    }
-    plan.dch.alloc(nch);
-    HIPCHK(hipMemcpyAsync(plan.dch.p, chunks.data(), nch * sizeof(Chunk), hipMemcpyHostToDevice, st));
-    plan.dLast.alloc(ndocs);
-    HIPCHK(hipMemcpyAsync(plan.dLast.p, lastChunk.data(), ndocs * 4, hipMemcpyHostToDevice, st));
-    plan.laneChunk.alloc(nch);
-    HIPCHK(hipMemcpyAsync(plan.laneChunk.p, order.data(), nch * 4, hipMemcpyHostToDevice, st));
-    // Offset bands for the uniform-step walk: band = 8 * a / docLen, chunks of
-    // a band in document order.  Copies of the reference then keep an XCD's
-    // x / ISA / PLCP accesses inside one eighth of the reference.
-    const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(8, env_u32("CMSBWT_BANDS", 8)));
-    std::vector<uint32_t> bandCnt(nb + 1, 0), bandOf(nch);
-    for (uint32_t c = 0; c < nch; c++) {
-      const uint64_t L = hdoc[chunks[c].doc + 1] - hdoc[chunks[c].doc] - 1;
-      bandOf[c] = L ? (uint32_t)std::min<uint64_t>(nb - 1, (uint64_t)chunks[c].a * nb / L) : 0;
-      bandCnt[bandOf[c] + 1]++;
-    }
-    for (uint32_t k = 0; k < nb; k++) bandCnt[k + 1] += bandCnt[k];
-    std::vector<uint32_t> bandOrd(nch), fillp(bandCnt.begin(), bandCnt.end() - 1);
-    for (uint32_t c = 0; c < nch; c++) bandOrd[fillp[bandOf[c]]++] = c;
-    plan.bandOrder.alloc(nch);
-    HIPCHK(hipMemcpyAsync(plan.bandOrder.p, bandOrd.data(), nch * 4, hipMemcpyHostToDevice, st));
-    plan.bandStart.alloc(nb + 1);
-    HIPCHK(hipMemcpyAsync(plan.bandStart.p, bandCnt.data(), (nb + 1) * 4, hipMemcpyHostToDevice, st));
-    plan.nbands = nb;
-    sync();
-    plan.C = C;
-    plan.nch = nch;
-    plan.valid = true;
-  }
-
-  HeadsSoA heads() {
-    return HeadsSoA{hStart.p, hPos.p, hLen.p, hSmall.p, hChar.p, hIsa.p, hTonext.p, hNext.p};
-  }
-
-  // =====================================================================
-  // merge
-  void merge(int rle) {
-    if (!walked) throw InputError{CMSBWT_EARG, "run ms_walk first"};
-    auto t0 = std::chrono::steady_clock::now();
-    const uint32_t n = R.n;
-    const uint32_t E = (uint32_t)ndocs;
-    const int bN = bits_for(n);
-    HeadsSoA h = heads();
-
-    // ---- grouping: perm sorted by (pos, len, isaNext, idx)   FN:1387-1416
-    const int bL = bits_for(max_u32(hLen.p, H));
-    const bool packed = 2 * bN + bL <= 64 && !env_u32("CMSBWT_GROUP3", 0);
-    DBuf<uint32_t> perm, perm2, key, key2;
-    perm.alloc(H); perm2.alloc(H); key.alloc(H); key2.alloc(H);
-    DBuf<unsigned long long> gk, gk2;
-    mk_iota(perm.p, H, st);
-    if (packed) {  // one sort on the composite key
-      gk.alloc(H); gk2.alloc(H);
-      mk_group_key(h, H, bN, bL, gk.p, st);
-      sort_pairs(gk.p, gk2.p, perm.p, perm2.p, H, 2 * bN + bL);
-      gk.release();
-    } else {       // LSD: isaNext, len, pos
-      mk_gather(hIsa.p, perm.p, key.p, H, st);
-      sort_pairs(key.p, key2.p, perm.p, perm2.p, H, bN);
-      mk_gather(hLen.p, perm2.p, key.p, H, st);
-      sort_pairs(key.p, key2.p, perm2.p, perm.p, H, bL);
-      mk_gather(hPos.p, perm.p, key.p, H, st);
-      sort_pairs(key.p, key2.p, perm.p, perm2.p, H, bN);
-    }
-    perm.release();
-    DBuf<uint32_t>& P = perm2;  // sorted members
-    // items
-    if (packed) mk_item_flags64(gk2.p, key.p, H, st);
-    else mk_item_flags(P.p, h, key.p, H, st);
-    inscan(key.p, key2.p, H, rocprim::plus<uint32_t>());
-    K = read1(key2.p + (H - 1));
-    DBuf<uint32_t> aPos, aLen, aIsa, aUntil, aCount, aFirst, aSlot;
-    DBuf<uint8_t> aSmall;
-    aPos.alloc(K); aLen.alloc(K); aIsa.alloc(K); aUntil.alloc(K); aCount.alloc(K); aFirst.alloc(K);
-    aSmall.alloc(K);
-    ItemsSoA A0{aPos.p, aLen.p, aIsa.p, aSmall.p, aUntil.p, aCount.p, aFirst.p, nullptr, nullptr, nullptr};
-    if (packed) mk_item_fill64(gk2.p, P.p, key.p, key2.p, h, H, bN, bL, A0, st);
-    else mk_item_fill(P.p, key.p, key2.p, h, H, A0, st);
-    gk2.release();
-    mk_item_count(aFirst.p, aCount.p, K, H, st);
-    key.release();
-    key2.release();
-    // map order inside each position (match.h:27-33): stable sort by class/len, then by pos
-    DBuf<uint32_t> io, io2, ik, ik2;
-    io.alloc(K); io2.alloc(K); ik.alloc(K); ik2.alloc(K);
-    mk_iota(io.p, K, st);
-    mk_item_key(aLen.p, aSmall.p, io.p, ik.p, K, st);
-    sort_pairs(ik.p, ik2.p, io.p, io2.p, K, 32);
-    mk_gather(aPos.p, io2.p, ik.p, K, st);
-    sort_pairs(ik.p, ik2.p, io2.p, io.p, K, bN);
-    ik.release(); ik2.release(); io2.release();
-    DBuf<uint32_t> sPos, sLen, sIsa, sUntil, sCount, sFirst, sSlot;
-    DBuf<uint8_t> sSmall;
-    DBuf<unsigned long long> sKey;
-    sPos.alloc(K); sLen.alloc(K); sIsa.alloc(K); sUntil.alloc(K); sCount.alloc(K); sFirst.alloc(K);
-    sSlot.alloc((uint64_t)K + 1); sSmall.alloc(K); sKey.alloc(K);
-    ItemsSoA S{sPos.p, sLen.p, sIsa.p, sSmall.p, sUntil.p, sCount.p, sFirst.p, sSlot.p, nullptr, sKey.p};
-    mk_item_permute(A0, io.p, S, K, st);
-    mk_item_sk(S, K, st);
-    io.release();
-    aPos.release(); aLen.release(); aIsa.release(); aUntil.release(); aCount.release(); aFirst.release();
-    aSmall.release();
-    // slots = prefixSumForPositions (FN:1504-1515)
-    exscan(sCount.p, sSlot.p, 0u, K);
-    {
-      uint32_t hh = H;
-      HIPCHK(hipMemcpyAsync(sSlot.p + K, &hh, 4, hipMemcpyHostToDevice, st));
-    }
-    DBuf<uint32_t> posBegin, posF;
-    posBegin.alloc((uint64_t)n + 1);
-    posF.alloc(n);
-    mk_pos_begin(sPos.p, K, n, posBegin.p, st);
-    mk_pos_f(sPos.p, sSmall.p, posBegin.p, K, n, posF.p, st);
-    DBuf<unsigned long long> cstats;
-    cstats.alloc(8);
-    cstats.zero(st);
-    if (!orderInvariant || env_u32("CMSBWT_FORCE_CHECK", 0)) mk_check_items(S, posBegin.p, posF.p, K, cstats.p + 3, st);
-
-    // ---- ranks (FN:1432-1453)
-    DBuf<uint32_t> itemsSA, headsSA, itemRankBase, headBase;
-    itemsSA.alloc(n); headsSA.alloc(n); itemRankBase.alloc(n); headBase.alloc(n);
-    mk_sa_counts(dsa.p, posBegin.p, sSlot.p, n, E, itemsSA.p, headsSA.p, st);
-    exscan(itemsSA.p, itemRankBase.p, 0u, n);
-    exscan(headsSA.p, headBase.p, 0u, n);
-    itemsSA.release(); headsSA.release();
-    T.alloc((uint64_t)H + 1);
-    saT.alloc((uint64_t)H + 1);
-    DBuf<uint32_t> grp;
-    grp.alloc((uint64_t)H + 1);
-    {
-      int32_t z = 0;
-      uint32_t hh = H, zz = 0;
-      HIPCHK(hipMemcpyAsync(T.p + H, &z, 4, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(saT.p, &hh, 4, hipMemcpyHostToDevice, st));
-      HIPCHK(hipMemcpyAsync(grp.p + H, &zz, 4, hipMemcpyHostToDevice, st));
-    }
-    // slot-major members: item of each slot and member idx of each slot
-    DBuf<uint32_t> itemOfSlot, Pm;
-    itemOfSlot.alloc(H);
-    Pm.alloc(H);
-    {
-      DBuf<uint32_t> mark;
-      mark.alloc(H);
-      mark.zero(st);
-      mk_slot_mark(sSlot.p, K, mark.p, st);
-      inscan(mark.p, itemOfSlot.p, H, rocprim::plus<uint32_t>());
-    }
-    mk_slot_members(S, itemOfSlot.p, P.p, H, Pm.p, st);
-    DBuf<uint32_t> actv;
-    actv.alloc(H);
-    {
-      DBuf<uint32_t> rankBase, gBase;
-      rankBase.alloc(n);
-      gBase.alloc(n);
-      mk_pos_rank_base(posBegin.p, sSlot.p, disa.p, itemRankBase.p, headBase.p, n, E, rankBase.p, gBase.p, st);
-      mk_ranks_slot(S, itemOfSlot.p, Pm.p, H, rankBase.p, gBase.p, n, T.p, saT.p, grp.p, actv.p, st);
-    }
-    itemRankBase.release();
-    stats.rank = (uint64_t)E + 2 + (uint64_t)(K - 1);
-
-    // ---- suffix sort of the head string (libsais_int, FN:1455-1459)
-    {
-      const int bH = bits_for(H);
-      // unresolved members' sa positions (resolved ones are 0xffffffff and
-      // sort to the end); U of them
-      DBuf<uint32_t> act, act2, val, val2, lab, labMax, keep;
-      act.alloc(H); act2.alloc(H);
-      uint32_t U = 0;
-      {
-        DBuf<uint32_t> cntU;
-        cntU.alloc(1);
-        size_t bb = 0;
-        HIPCHK(rocprim::select(nullptr, bb, actv.p, act2.p, cntU.p, (size_t)H, IsActive(), st));
-        HIPCHK(rocprim::select(scratch(bb), bb, actv.p, act2.p, cntU.p, (size_t)H, IsActive(), st));
-        U = read1(cntU.p);
-      }
-      actv.release();
-      sort_keys(act2.p, act.p, U, bH);
-      DBuf<uint64_t> k64, k64b;
-      val.alloc(U); val2.alloc(U); lab.alloc(U); labMax.alloc(U); keep.alloc(U);
-      k64.alloc(U); k64b.alloc(U);
-      // groups are visited in suffix-array order (k_dbl_apply writes the
-      // u-th smallest key to the u-th smallest active sa position): act is
-      // sorted above
-      for (uint64_t hstep = 1; U > 0; hstep <<= 1) {
-        if (hstep > H) throw InputError{CMSBWT_EINPUT, "internal: head-string suffix sort did not converge"};
-        mk_dbl_keys(act.p, saT.p, grp.p, (uint32_t)hstep, U, k64.p, val.p, st);
-        sort_pairs(k64.p, k64b.p, val.p, val2.p, U, 32 + bH);
-        mk_dbl_apply(act.p, k64b.p, val2.p, U, saT.p, lab.p, st);
-        inscan(lab.p, labMax.p, U, rocprim::maximum<uint32_t>());
-        mk_dbl_groups(act.p, k64b.p, val2.p, labMax.p, U, grp.p, keep.p, st);
-        U = select_flagged(act.p, keep.p, act2.p, U);
-        std::swap(act.p, act2.p);
-      }
-    }
-    grp.release();
-    DBuf<uint32_t> headRank;
-    headRank.alloc(H);
-    bwtHeads.alloc(H);
-    mk_head_ranks(saT.p, hChar.p, H, headRank.p, bwtHeads.p, st);
-
-    // ---- next-head ranks, sorted per item (FN:1480-1494): small items by an
-    // in-place insertion sort, large ones by one global (item, nhr) sort
-    DBuf<uint32_t> nhr;
-    nhr.alloc(H);
-    {
-      mk_nhr_slot(Pm.p, headRank.p, hNext.p, H, nhr.p, st);
-      DBuf<uint32_t> bigItem;
-      bigItem.alloc(K);
-      mk_nhr_sort_small(S, K, nhr.p, bigItem.p, st);
-      DBuf<unsigned long long> bk, bk2, bsel;
-      DBuf<uint32_t> bflag, bslots, iotaS;
-      bk.alloc(H); bflag.alloc(H);
-      mk_nhr_big_keys(itemOfSlot.p, bigItem.p, nhr.p, H, bk.p, bflag.p, st);
-      bsel.alloc(H);
-      const uint32_t B = select_flagged_u64(bk.p, bflag.p, bsel.p, H);
-      if (B) {
-        iotaS.alloc(H);
-        mk_iota(iotaS.p, H, st);
-        bslots.alloc(B);
-        const uint32_t B2 = select_flagged(iotaS.p, bflag.p, bslots.p, H);
-        if (B2 != B) throw InputError{CMSBWT_EINPUT, "internal: large-item selection mismatch"};
-        bk2.alloc(B);
-        sort_keys(bsel.p, bk2.p, B, 32 + bits_for(K));
-        mk_nhr_big_back(bk2.p, bslots.p, B, nhr.p, st);
-      }
-    }
-    headRank.release();
-    Pm.release();
-    itemOfSlot.release();
-
-    // ---- counterSmallerThanHead (FN:1523-1603)
-    counter.alloc((uint64_t)H + 1);
-    counter.zero(st);
-    uint64_t W = 0;
-    {
-      // work volume (statistics only): sum of untilNext
-      DBuf<uint64_t> wsum;
-      wsum.alloc(1);
-      auto u64in = rocprim::make_transform_iterator(sUntil.p, WidenU64());
-      size_t b = 0;
-      HIPCHK(rocprim::reduce(nullptr, b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
-      HIPCHK(rocprim::reduce(scratch(b), b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
-      W = read1(wsum.p);
-      // windows over reference positions
-      DBuf<uint32_t> wflag, wincl, winStart, crossCnt, crossOff, crossList;
-      wflag.alloc(n);
-      wincl.alloc(n);
-      const uint32_t winPos = std::min(1024u, env_u32("CMSBWT_WINPOS", 1024)),
-                     slotCap = std::min(4096u, env_u32("CMSBWT_WINSLOTS", 4096));
-      mk_win_flags(posBegin.p, sSlot.p, n, std::max(1u, winPos), slotCap, wflag.p, st);
-      inscan(wflag.p, wincl.p, n, rocprim::plus<uint32_t>());
-      const uint32_t nw = read1(wincl.p + (n - 1));
-      winStart.alloc((uint64_t)nw + 1);
-      mk_win_starts(wflag.p, wincl.p, n, winStart.p, st);
-      HIPCHK(hipMemcpyAsync(winStart.p + nw, &n, 4, hipMemcpyHostToDevice, st));
-      wflag.release();
-      // crossing lists: (window, item) pairs sorted by window
-      DBuf<uint32_t> itemOff, keyW, keyW2, valQ;
-      crossCnt.alloc(K);
-      itemOff.alloc(K);
-      mk_win_cross(S, K, wincl.p, n, crossCnt.p, nullptr, nullptr, nullptr, cstats.p + 4, 0, st);
-      exscan(crossCnt.p, itemOff.p, 0u, K);
-      const uint32_t ncross = read1(itemOff.p + (K - 1)) + read1(crossCnt.p + (K - 1));
-      keyW.alloc(std::max<uint32_t>(ncross, 1));
-      keyW2.alloc(std::max<uint32_t>(ncross, 1));
-      valQ.alloc(std::max<uint32_t>(ncross, 1));
-      crossList.alloc(std::max<uint32_t>(ncross, 1));
-      mk_win_cross(S, K, wincl.p, n, crossCnt.p, itemOff.p, keyW.p, valQ.p, cstats.p + 4, 1, st);
-      sort_pairs(keyW.p, keyW2.p, valQ.p, crossList.p, ncross, bits_for(nw));
-      crossOff.alloc((uint64_t)nw + 1);
-      mk_win_cross_off(keyW2.p, ncross, nw, crossOff.p, st);
-      wincl.release();
-      const bool check = !orderInvariant || env_u32("CMSBWT_FORCE_CHECK", 0) != 0;
-      HIPCHK(hipEventRecord(ev0, st));
-      mk_counter_win(S, posBegin.p, posF.p, nhr.p, winStart.p, nw, crossOff.p, crossList.p, counter.p, cstats.p, n,
-                     slotCap, check, st);
-      HIPCHK(hipGetLastError());
-      HIPCHK(hipEventRecord(ev1, st));
-      sync();
-      float ms = 0;
-      HIPCHK(hipEventElapsedTime(&ms, ev0, ev1));
-      counter_kernel_ms = ms;
-      windows = nw;
-      crossings = ncross;
-    }
-    unsigned long long cs[8];
-    HIPCHK(hipMemcpyAsync(cs, cstats.p, sizeof(cs), hipMemcpyDeviceToHost, st));
-    sync();
-    if (env_u32("CMSBWT_COUNTER_STATS", 0))
-      fprintf(stderr, "[counter] bad %llu good %llu nothing %llu windows %u crossings %u\n", cs[0], cs[1], cs[2],
-              windows, crossings);
-    stats.counter_bad = cs[0];
-    stats.counter_good = cs[1];
-    stats.counter_nothing = cs[2];
-    stats.order_violations = cs[3];
-    if (cs[4]) throw InputError{CMSBWT_EINPUT, "counter target beyond the reference (reference UB)"};
-    if (cs[3]) throw InputError{CMSBWT_EORDER,
-                                "MatchInSet comparator is not a strict weak order on this input (" +
-                                    std::to_string(cs[3]) + " ambiguous comparisons); std::map layout would "
-                                    "depend on insertion history"};
-    W_work = W;
-    stats.counter_kernel_ms = counter_kernel_ms;
-    stats.counter_work = W;
-
-    // ---- buckets (FN:1162-1171) and inversion (FN:1618-1628, done as a gather)
-    bucket.alloc(n);
-    {
-      DBuf<int32_t> cnt;
-      cnt.alloc(n);
-      inscan(diff.p, cnt.p, n, rocprim::plus<int32_t>());
-      mk_bucket(cnt.p, hasHead.p, n, bucket.p, st);
-    }
-
-    // ---- writer (FN:1631-1777) as segments + run-length merge
-    WriterIn wi{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, sCount.p, headBase.p, bwtHeads.p, counter.p,
-                n, E, rle};
-    // units: the E end phrases, then SA ranks 1..n-1; runs counted per unit,
-    // joined across unit boundaries, emitted as (start, char) and packed
-    const uint64_t U64 = (uint64_t)E + n - 1;
-    if (U64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer units"};
-    const uint32_t Uw = (uint32_t)U64;
-    DBuf<uint32_t> wruns, whl, wprev;
-    DBuf<unsigned long long> wsym, wrunOff, wsymOff;
-    wruns.alloc(Uw); whl.alloc(Uw); wprev.alloc(Uw); wsym.alloc(Uw); wrunOff.alloc(Uw); wsymOff.alloc(Uw);
-    mk_wr_count(wi, Uw, wruns.p, wsym.p, whl.p, st);
-    exscan(whl.p, wprev.p, 0u, Uw, LastNonEmpty());
-    mk_wr_adjust(whl.p, wprev.p, Uw, wruns.p, st);
-    auto runs64 = rocprim::make_transform_iterator(wruns.p, WidenU64());
-    exscan(runs64, wrunOff.p, 0ull, Uw);
-    exscan(wsym.p, wsymOff.p, 0ull, Uw);
-    const uint64_t Rn = read1(wrunOff.p + (Uw - 1)) + read1(wruns.p + (Uw - 1));
-    const uint64_t symbols = read1(wsymOff.p + (Uw - 1)) + read1(wsym.p + (Uw - 1));
-    DBuf<unsigned long long> runStart;
-    DBuf<uint8_t> runChar;
-    runStart.alloc(std::max<uint64_t>(Rn, 1)); runChar.alloc(std::max<uint64_t>(Rn, 1));
-    mk_wr_emit(wi, Uw, wrunOff.p, wsymOff.p, wprev.p, runStart.p, runChar.p, st);
-    runs.alloc(Rn * 9);
-    mk_wr_records(runStart.p, runChar.p, Rn, symbols, runs.p, st);
-    HIPCHK(hipGetLastError());
-    sync();
-    nruns = Rn;
-    lastRle = rle;
-    merged = true;
-    stats.keys = K;
-    stats.current_sum = H;
-    stats.runs = Rn;
-    stats.symbols = symbols;
-    stats.positions = count_positions(sPos);
-    stats.t_merge_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  }
-  float counter_kernel_ms = 0;
-  uint32_t windows = 0, crossings = 0;
-  bool orderInvariant = false;  // set by ms_walk (k_finalize), false for imported shards
-  uint64_t W_work = 0;
-
-  uint64_t count_positions(DBuf<uint32_t>& sPos) {
-    // phrasesSet.size(): distinct positions holding items (n-1 always present)
-    DBuf<unsigned long long> c;
-    c.alloc(1);
-    c.zero(st);
-    mk_count_distinct(sPos.p, K, c.p, st);
-    return read1(c.p);
-  }
-
-  // =====================================================================
-  void copy_runs(uint8_t* out, uint64_t cap) {
-    if (!merged) throw InputError{CMSBWT_EARG, "run merge first"};
-    if (cap < nruns * 9) throw InputError{CMSBWT_EARG, "output buffer too small"};
-    if (nruns) HIPCHK(hipMemcpyAsync(out, runs.p, nruns * 9, hipMemcpyDeviceToHost, st));
-    sync();
-  }
-
-  void write_output(const std::string& outname, int rle) {
-    if (!merged) throw InputError{CMSBWT_EARG, "run merge first"};
-    if (rle != lastRle) throw InputError{CMSBWT_EARG, "merge was run with a different output format"};
-    auto t0 = std::chrono::steady_clock::now();
-    std::vector<uint8_t> host(nruns * 9);
-    copy_runs(host.data(), host.size());
-    if (rle) {
-      FILE* f = fopen((outname + ".rl_bwt").c_str(), "wb");
-      if (!f) throw InputError{CMSBWT_EIO, "cannot open " + outname + ".rl_bwt"};
-      fwrite(host.data(), 1, host.size(), f);
-      fclose(f);
-    } else {
-      FILE* f = fopen((outname + ".bwt").c_str(), "wb");
-      if (!f) throw InputError{CMSBWT_EIO, "cannot open " + outname + ".bwt"};
-      std::vector<uint8_t> buf(1 << 20);
-      size_t fill = 0;
-      for (uint64_t j = 0; j < nruns; j++) {
-        uint64_t len;
-        memcpy(&len, host.data() + 9 * j, 8);
-        uint8_t c = host[9 * j + 8];
-        while (len) {
-          uint64_t k = std::min<uint64_t>(len, buf.size() - fill);
-          memset(buf.data() + fill, c, k);
-          fill += k;
-          len -= k;
-          if (fill == buf.size()) { fwrite(buf.data(), 1, fill, f); fill = 0; }
-        }
-      }
-      if (fill) fwrite(buf.data(), 1, fill, f);
-      fclose(f);
-    }
-    if (R.n < 1000000) {  // FN:919-924 small-reference side output
-      std::vector<unsigned long long> c((uint64_t)H + 1);
-      HIPCHK(hipMemcpyAsync(c.data(), counter.p, c.size() * 8, hipMemcpyDeviceToHost, st));
-      sync();
-      FILE* f = fopen((outname + ".counterSmallerThanHead_true").c_str(), "wb");
-      if (!f) throw InputError{CMSBWT_EIO, "cannot open counter file"};
-      fwrite(c.data(), 8, c.size(), f);
-      fclose(f);
-    }
-    stats.t_write_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-  }
-
-  void walk_import(uint64_t heads, uint64_t nd, uint64_t nchars, uint32_t flags, const void* const* a) {
-    if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
-    if (heads >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^31-1 heads"};
-    walked = merged = false;
-    H = (uint32_t)heads;
-    hStart.alloc(H); hPos.alloc(H); hLen.alloc(H); hIsa.alloc(H); hTonext.alloc(H);
-    hSmall.alloc(H); hChar.alloc(H); hNext.alloc(H);
-    diff.alloc((uint64_t)R.n + 1);
-    hasHead.alloc(R.n);
-    auto in = [&](void* d, const void* s, uint64_t b) {
-      if (b) HIPCHK(hipMemcpyAsync(d, s, b, hipMemcpyDefault, st));
-    };
-    in(hStart.p, a[0], (uint64_t)H * 4); in(hPos.p, a[1], (uint64_t)H * 4); in(hLen.p, a[2], (uint64_t)H * 4);
-    in(hSmall.p, a[3], H); in(hChar.p, a[4], H); in(hIsa.p, a[5], (uint64_t)H * 4);
-    in(hTonext.p, a[6], (uint64_t)H * 4); in(hNext.p, a[7], (uint64_t)H * 2);
-    in(diff.p, a[8], ((uint64_t)R.n + 1) * 4); in(hasHead.p, a[9], R.n);
-    sync();
-    ndocs = nd;
-    chars = nchars;
-    collLoaded = walked = true;
-    orderInvariant = (flags & 1u) != 0;
-    stats.heads = H;
-    stats.ndocs = nd;
-    stats.chars = nchars;
-  }
-
-  // parity copies
-  uint64_t copy_array(const std::string& name, void* out) {
-    auto cp = [&](const void* d, uint64_t bytes) -> uint64_t {
-      if (out && bytes) {
-        HIPCHK(hipMemcpyAsync(out, d, bytes, hipMemcpyDefault, st));
-        sync();
-      }
-      return bytes;
-    };
-    if (name.rfind("h_", 0) == 0 && !walked) throw InputError{CMSBWT_EARG, "run ms_walk first"};
-    if (name == "h_start") return cp(hStart.p, (uint64_t)H * 4);
-    if (name == "h_pos") return cp(hPos.p, (uint64_t)H * 4);
-    if (name == "h_len") return cp(hLen.p, (uint64_t)H * 4);
-    if (name == "h_smaller") return cp(hSmall.p, H);
-    if (name == "h_lchar") return cp(hChar.p, H);
-    if (name == "h_isa") return cp(hIsa.p, (uint64_t)H * 4);
-    if (name == "h_tonext") return cp(hTonext.p, (uint64_t)H * 4);
-    if (name == "h_nexthead") return cp(hNext.p, (uint64_t)H * 2);
-    if (name == "diff") return cp(diff.p, ((uint64_t)R.n + 1) * 4);
-    if (name == "hashead") return cp(hasHead.p, R.n);
-    if (!merged) throw InputError{CMSBWT_EARG, "run merge first"};
-    if (name == "bucket") return cp(bucket.p, (uint64_t)R.n * 8);
-    if (name == "rank2head") return cp(T.p, ((uint64_t)H + 1) * 4);
-    if (name == "head2rank") return cp(saT.p, ((uint64_t)H + 1) * 4);
-    if (name == "bwtheads") return cp(bwtHeads.p, H);
-    if (name == "counters") return cp(counter.p, ((uint64_t)H + 1) * 8);
-    throw InputError{CMSBWT_EARG, "unknown array " + name};
-  }
-};
-
-}  // namespace cmsbwt
+// engine.hip — the C ABI of include/cmsbwt.h over cmsbwt::Engine (engine.h).
+#include "engine.h"
 
 // =========================================================================
 // C ABI
@@ -1383,6 +243,89 @@ int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path
             (unsigned long long)s.runs);
   cmsbwt_ctx_destroy(ctx);
   return CMSBWT_OK;
+}
+
+// ---- position-sharded merge (include/cmsbwt.h "Multi-GPU merge")
+int cmsbwt_dm_begin(cmsbwt_ctx* ctx, uint32_t world, uint32_t rank, uint64_t heads_total, uint64_t docs_total,
+                    uint32_t flags, const int32_t* diff, const uint8_t* hashead, int rle) {
+  if (!ctx) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_begin(world, rank, heads_total, docs_total, flags, diff, hashead, rle); });
+}
+int cmsbwt_dm_route_heads(cmsbwt_ctx* ctx, uint64_t* counts) {
+  if (!ctx || !counts) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_route_heads(counts); });
+}
+int cmsbwt_dm_pack_heads(cmsbwt_ctx* ctx, int32_t* out) {
+  if (!ctx) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_pack_heads(out); });
+}
+int cmsbwt_dm_group(cmsbwt_ctx* ctx, const int32_t* recv, uint64_t nrecv, uint32_t* sa_counts) {
+  if (!ctx || !sa_counts) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_group(recv, nrecv, sa_counts); });
+}
+int cmsbwt_dm_labels(cmsbwt_ctx* ctx, const uint32_t* sa_counts, uint32_t* back) {
+  if (!ctx || !sa_counts) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_labels(sa_counts, back); });
+}
+int cmsbwt_dm_dbl_init(cmsbwt_ctx* ctx, const uint32_t* labels, uint64_t* active) {
+  if (!ctx || !active) return CMSBWT_EARG;
+  return guard(ctx, [&] { *active = ctx->e->dm_dbl_init(labels); });
+}
+int cmsbwt_dm_dbl_route(cmsbwt_ctx* ctx, uint64_t h, uint64_t* counts) {
+  if (!ctx || !counts) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_dbl_route(h, counts); });
+}
+int cmsbwt_dm_dbl_pack(cmsbwt_ctx* ctx, int32_t* out) {
+  if (!ctx) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_dbl_pack(out); });
+}
+int cmsbwt_dm_dbl_sort(cmsbwt_ctx* ctx, const int32_t* recv, uint64_t nrecv, uint32_t* result) {
+  if (!ctx) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_dbl_sort(recv, nrecv, result); });
+}
+int cmsbwt_dm_dbl_apply(cmsbwt_ctx* ctx, const uint32_t* back, uint64_t* active) {
+  if (!ctx || !active) return CMSBWT_EARG;
+  return guard(ctx, [&] { *active = ctx->e->dm_dbl_apply(back); });
+}
+int cmsbwt_dm_pack_ranks(cmsbwt_ctx* ctx, int32_t* out) {
+  if (!ctx) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_pack_ranks(out); });
+}
+int cmsbwt_dm_load_ranks(cmsbwt_ctx* ctx, const int32_t* recv) {
+  if (!ctx) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_load_ranks(recv); });
+}
+int cmsbwt_dm_route_halo(cmsbwt_ctx* ctx, uint64_t* item_counts, uint64_t* word_counts) {
+  if (!ctx || !item_counts || !word_counts) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_route_halo(item_counts, word_counts); });
+}
+int cmsbwt_dm_pack_halo(cmsbwt_ctx* ctx, int32_t* headers, int32_t* words) {
+  if (!ctx) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_pack_halo(headers, words); });
+}
+int cmsbwt_dm_counter(cmsbwt_ctx* ctx, const int32_t* headers, uint64_t nitems, const int32_t* words, uint64_t nwords,
+                      uint64_t* stats6) {
+  if (!ctx || !stats6) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_counter(headers, nitems, words, nwords, stats6); });
+}
+int cmsbwt_dm_units(cmsbwt_ctx* ctx, int64_t* units) {
+  if (!ctx || !units) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_units(units); });
+}
+int cmsbwt_dm_emit(cmsbwt_ctx* ctx, const int64_t* units, uint64_t* nlocal) {
+  if (!ctx || !units || !nlocal) return CMSBWT_EARG;
+  return guard(ctx, [&] { *nlocal = ctx->e->dm_emit(units); });
+}
+int cmsbwt_dm_copy_stream(cmsbwt_ctx* ctx, uint64_t* starts, uint8_t* chars) {
+  if (!ctx) return CMSBWT_EARG;
+  return guard(ctx, [&] { ctx->e->dm_copy_stream((unsigned long long*)starts, chars); });
+}
+int cmsbwt_dm_finish(cmsbwt_ctx* ctx, const uint64_t* const* starts, const uint8_t* const* chars,
+                     const uint64_t* counts, const uint64_t* gstats) {
+  if (!ctx || !starts || !chars || !counts || !gstats) return CMSBWT_EARG;
+  return guard(ctx, [&] {
+    ctx->e->dm_finish((const unsigned long long* const*)starts, chars, counts, gstats);
+  });
 }
 
 }  // extern "C"

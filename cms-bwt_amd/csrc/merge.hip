@@ -623,10 +623,11 @@ __global__ void k_item_sk(ItemsSoA it, uint32_t K) {
 // boundary at p when the first slot of p enters a new half-window block of
 // slots, or every winPos positions
 __global__ void k_win_flags(const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ slot, uint32_t n,
-                            uint32_t winPos, uint32_t half, uint32_t* __restrict__ flag) {
+                            uint32_t P0, uint32_t P1, uint32_t winPos, uint32_t half, uint32_t* __restrict__ flag) {
   uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
   if (p >= n) return;
-  if (p == 0 || p % winPos == 0) { flag[p] = 1; return; }
+  if (p < P0 || p >= P1) { flag[p] = 0; return; }  // windows cover the target range [P0, P1) only
+  if (p == P0 || (p - P0) % winPos == 0) { flag[p] = 1; return; }
   uint32_t a = slot[posBegin[p - 1]] / half, b = slot[posBegin[p]] / half;
   flag[p] = a != b ? 1u : 0u;
 }
@@ -652,9 +653,9 @@ __global__ void k_win_cross(const ItemsSoA it, uint32_t K, const uint32_t* __res
   if (u) {
     uint64_t last = (uint64_t)p + u;
     if (last >= n) { if (!fill) atomicAdd(errs, 1ull); last = n - 1; }
-    wf = winIncl[p];                         // = window index of p, plus one
-    const uint32_t wl = winIncl[last] - 1;   // window of the last target
-    c = wl >= wf ? wl - wf + 1 : 0;
+    wf = winIncl[p];                         // = window index of p, plus one (0 before the range)
+    const uint32_t il = winIncl[last];       // = window of the last target, plus one
+    c = il > wf ? il - wf : 0;
   }
   if (!fill) { cnt[q] = c; return; }
   const uint32_t o = off[q];
@@ -696,6 +697,11 @@ struct WriterArgs {
   uint32_t n;
   uint32_t E;
   int rle;                   // 1: .rl_bwt remainder quirk (FN:1761-1770); 0: .bwt (FN:1678-1686)
+  // position-sharded merge: head characters by local slot, and only the
+  // units whose position lies in [P0, P1) produce segments (bwtSlot == null:
+  // one GPU, characters by head rank)
+  const uint8_t* bwtSlot;
+  uint32_t P0, P1;
 };
 
 template <bool EMIT>
@@ -744,6 +750,11 @@ __device__ __forceinline__ uint64_t d_segments(const WriterArgs& A, uint32_t r, 
 // is SA rank r >= 1 (the same walk as d_segments).
 template <class F>
 __device__ __forceinline__ void d_unit_segments(const WriterArgs& A, uint32_t u, F&& f) {
+  if (A.bwtSlot) {  // sharded: the end phrases' unit belongs to the owner of position n-1
+    const uint32_t pu = u < A.E ? A.n - 1 : (uint32_t)A.sa[u - A.E + 1];
+    if (pu < A.P0 || pu >= A.P1) return;
+    if (u < A.E) { f(A.bwtSlot[A.slot[A.posBegin[A.n - 1]] + u], 1ull); return; }
+  }
   if (u < A.E) { f(A.bwtHeads[u], 1ull); return; }
   const uint32_t r = u - A.E + 1;
   const uint32_t p = (uint32_t)A.sa[r];
@@ -754,13 +765,13 @@ __device__ __forceinline__ void d_unit_segments(const WriterArgs& A, uint32_t u,
   int64_t acc = b;
   const uint32_t i0 = A.posBegin[p], i1 = A.posBegin[p + 1];
   const uint32_t s0 = A.slot[i0];
-  const uint32_t hb = A.headBase[r];
+  const uint32_t hb = A.bwtSlot ? 0u : A.headBase[r];
   for (uint32_t q = i0; q < i1; q++) {
     const uint32_t sb = A.slot[q], se = sb + A.count[q];
     for (uint32_t s = sb; s < se; s++) {
       const unsigned long long cs = A.counter[s];
       if (cs) { f(c, cs); acc += (int64_t)cs; }
-      f(A.bwtHeads[hb + (s - s0)], 1ull);
+      f(A.bwtSlot ? A.bwtSlot[s] : A.bwtHeads[hb + (s - s0)], 1ull);
       acc++;
     }
     if (A.rle && acc != 0) f(c, (unsigned long long)(-acc));  // FN:1761-1770 quirk
@@ -1011,9 +1022,9 @@ void mk_nhr_keys(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uin
 void mk_low32(const uint64_t* key, uint32_t* out, uint64_t n, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_low32, g1(n), dim3(256), 0, st, key, out, n);
 }
-void mk_win_flags(const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t winPos, uint32_t slotCap,
-                  uint32_t* flag, hipStream_t st) {
-  hipLaunchKernelGGL(k_win_flags, g1(n), dim3(256), 0, st, posBegin, slot, n, winPos, std::max(1u, slotCap / 2),
+void mk_win_flags(const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t P0, uint32_t P1,
+                  uint32_t winPos, uint32_t slotCap, uint32_t* flag, hipStream_t st) {
+  hipLaunchKernelGGL(k_win_flags, g1(n), dim3(256), 0, st, posBegin, slot, n, P0, P1, winPos, std::max(1u, slotCap / 2),
                      flag);
 }
 void mk_win_starts(const uint32_t* flag, const uint32_t* winIncl, uint32_t n, uint32_t* winStart, hipStream_t st) {
@@ -1047,20 +1058,18 @@ void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, h
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st) {
   hipLaunchKernelGGL(k_bucket, g1(n), dim3(256), 0, st, countIncl, hasHead, n, bucket);
 }
+static WriterArgs writer_args(const WriterIn& w) {
+  return WriterArgs{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.count, w.headBase, w.bwtHeads, w.counter,
+                    w.n, w.E, w.rle, w.bwtSlot, w.P0, w.P1};
+}
 void mk_seg_count(const WriterIn& w, unsigned long long* segN, hipStream_t st) {
-  WriterArgs A{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.count, w.headBase, w.bwtHeads, w.counter,
-               w.n, w.E, w.rle};
+  WriterArgs A = writer_args(w);
   hipLaunchKernelGGL(k_seg_count, g1(w.n), dim3(256), 0, st, A, segN);
 }
 void mk_seg_emit(const WriterIn& w, const unsigned long long* segOff, uint8_t* sc, unsigned long long* sn,
                  hipStream_t st) {
-  WriterArgs A{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.count, w.headBase, w.bwtHeads, w.counter,
-               w.n, w.E, w.rle};
+  WriterArgs A = writer_args(w);
   hipLaunchKernelGGL(k_seg_emit, g1(w.n), dim3(256), 0, st, A, segOff, sc, sn);
-}
-static WriterArgs writer_args(const WriterIn& w) {
-  return WriterArgs{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.count, w.headBase, w.bwtHeads, w.counter,
-                    w.n, w.E, w.rle};
 }
 void mk_wr_count(const WriterIn& w, uint32_t U, uint32_t* runs, unsigned long long* sym, uint32_t* hl, hipStream_t st) {
   if (U) hipLaunchKernelGGL(k_wr_count, g1(U), dim3(256), 0, st, writer_args(w), U, runs, sym, hl);

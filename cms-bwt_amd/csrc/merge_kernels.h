@@ -19,6 +19,8 @@ struct WriterIn {
   uint32_t n;
   uint32_t E;
   int rle;
+  const uint8_t* bwtSlot = nullptr;  // sharded merge: head characters by local slot
+  uint32_t P0 = 0, P1 = 0;           // sharded merge: owned position range
 };
 
 void mk_iota(uint32_t* p, uint64_t n, hipStream_t st);
@@ -77,8 +79,8 @@ void mk_head_ranks(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint32_
 void mk_nhr_keys(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uint32_t* headRank,
                  const uint16_t* nexthead, uint64_t* key, hipStream_t st);
 void mk_low32(const uint64_t* key, uint32_t* out, uint64_t n, hipStream_t st);
-void mk_win_flags(const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t winPos, uint32_t slotCap,
-                  uint32_t* flag, hipStream_t st);
+void mk_win_flags(const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t P0, uint32_t P1,
+                  uint32_t winPos, uint32_t slotCap, uint32_t* flag, hipStream_t st);
 void mk_win_starts(const uint32_t* flag, const uint32_t* winIncl, uint32_t n, uint32_t* winStart, hipStream_t st);
 void mk_win_cross(const ItemsSoA& it, uint32_t K, const uint32_t* winIncl, uint32_t n, uint32_t* cnt,
                   const uint32_t* off, uint32_t* keyW, uint32_t* valQ, unsigned long long* errs, int fill,
@@ -106,5 +108,50 @@ void mk_run_pack(const uint8_t* sc, const unsigned long long* runId, const unsig
                  unsigned long long* runEnd, uint8_t* runChar, hipStream_t st);
 void mk_run_records(const unsigned long long* runEnd, const uint8_t* runChar, uint64_t R, uint8_t* out,
                     hipStream_t st);
+
+// dist_kernels.hip: position-sharded merge (multi-GPU)
+void mk_dm_owner(const uint32_t* vals, const uint32_t* idx, uint64_t n, const uint32_t* split, uint32_t world,
+                 uint32_t* dest, hipStream_t st);
+void mk_dm_bounds(const uint32_t* sorted, uint64_t n, uint32_t world, uint32_t* bounds, hipStream_t st);
+void mk_dm_pack_heads(const uint32_t* perm, const HeadsSoA& h, uint64_t n, int32_t* out, hipStream_t st);
+void mk_dm_unpack_heads(const int32_t* in, uint64_t n, const HeadsSoA& h, hipStream_t st);
+void mk_dm_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t Eown,
+                     uint32_t* out, hipStream_t st);
+void mk_dm_group_labels(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
+                        const uint32_t* posBegin, const uint32_t* isaRef, const uint32_t* headBase, uint32_t n,
+                        uint32_t* back, uint32_t* gItem, hipStream_t st);
+void mk_dm_grp_init(const uint32_t* perm, const uint32_t* in, uint64_t n, uint32_t* grp, uint32_t* actFlag,
+                    hipStream_t st);
+void mk_dm_dbl_pack(const uint32_t* aPerm, const uint32_t* act, const uint32_t* grp, uint32_t h, uint64_t n,
+                    uint32_t H, int32_t* out, uint32_t* err, hipStream_t st);
+void mk_dm_dbl_keys(const int32_t* in, uint64_t n, unsigned long long* key, uint32_t* val, hipStream_t st);
+void mk_dm_dbl_marks(const unsigned long long* key, uint64_t n, uint32_t* gs, uint32_t* ks, hipStream_t st);
+void mk_dm_dbl_result(const unsigned long long* key, const uint32_t* val, const uint32_t* gsMax,
+                      const uint32_t* ksMax, uint64_t n, uint32_t* res, hipStream_t st);
+void mk_dm_dbl_apply(const uint32_t* aPerm, const uint32_t* act, const uint32_t* back, uint64_t n, uint32_t* grp,
+                     uint32_t* keep, hipStream_t st);
+void mk_dm_pack_ranks(const uint32_t* perm, const uint32_t* grp, const uint16_t* nexthead, uint64_t n, uint32_t H,
+                      int32_t* out, uint32_t* err, hipStream_t st);
+void mk_dm_load_ranks(const int32_t* in, const uint32_t* Pm, const uint32_t* itemOfSlot, const ItemsSoA& it,
+                      const uint32_t* gItem, const uint8_t* lchar, uint32_t H, uint32_t* nhr, uint8_t* bwtSlot,
+                      uint32_t* err, hipStream_t st);
+void mk_dm_halo_count(const ItemsSoA& it, uint32_t K, const uint32_t* split, uint32_t world, uint32_t rank,
+                      uint32_t n, uint32_t* c, hipStream_t st);
+void mk_dm_halo_fill(const uint32_t* c, const uint32_t* off, uint32_t K, uint32_t rank, uint32_t* dest,
+                     uint32_t* item, hipStream_t st);
+void mk_dm_pair_words(const uint32_t* item, uint32_t np, const uint32_t* count, uint32_t* w, hipStream_t st);
+void mk_dm_halo_pack(const uint32_t* item, uint32_t np, const ItemsSoA& it, const uint32_t* nhr, const uint32_t* wOff,
+                     int32_t* hdr, int32_t* words, hipStream_t st);
+void mk_dm_halo_unpack(const int32_t* hdr, uint32_t nh, const ItemsSoA& c, hipStream_t st);
+void mk_dm_units_pack(const uint32_t* runs, const uint32_t* hl, const unsigned long long* sym, uint32_t U,
+                      int64_t* out, hipStream_t st);
+void mk_dm_units_unpack(const int64_t* in, uint32_t U, uint32_t* runs, uint32_t* hl, unsigned long long* sym,
+                        hipStream_t st);
+void mk_dm_own_runs(const uint32_t* runs, uint32_t U, const int32_t* sa, uint32_t E, uint32_t n, uint32_t P0,
+                    uint32_t P1, unsigned long long* out, hipStream_t st);
+void mk_dm_place(const uint32_t* runs, const unsigned long long* runOff, const unsigned long long* srcOff, uint32_t U,
+                 const int32_t* sa, uint32_t E, uint32_t n, uint32_t P0, uint32_t P1,
+                 const unsigned long long* srcStart, const uint8_t* srcChar, unsigned long long* runStart,
+                 uint8_t* runChar, hipStream_t st);
 
 }  // namespace cmsbwt

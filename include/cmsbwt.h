@@ -126,6 +126,50 @@ int cmsbwt_copy_array(cmsbwt_ctx* ctx, const char* name, void* out, uint64_t* by
 int cmsbwt_walk_import(cmsbwt_ctx* ctx, uint64_t heads, uint64_t ndocs, uint64_t chars, uint32_t flags,
                        const void* const* arrays);
 
+/* Multi-GPU merge, sharded by reference position (replaces
+ * the single-process merge of FN:1387-1777 when documents are sharded over
+ * `world` ranks).  Rank k owns positions [k*n/world, (k+1)*n/world) and the
+ * head-string group labels [1 + k*H/world, 1 + (k+1)*H/world).  Every
+ * pointer is DEVICE memory of this context's GPU; the caller moves data
+ * between the calls (cmsbwt/dist.py: all-to-all / all-reduce over RCCL):
+ *   ms_walk; all-reduce "diff" (sum) and "hashead" (max) -> dm_begin
+ *   dm_route_heads -> counts; dm_pack_heads -> 5 int32/head; all-to-all
+ *   dm_group(recv) -> sa_counts[2n]; all-reduce(sum) -> dm_labels -> back
+ *   (1 word per received head); reverse all-to-all -> dm_dbl_init
+ *   while (all-reduced active > 0): dm_dbl_route(h) -> counts;
+ *     dm_dbl_pack -> 2 words/element; all-to-all; dm_dbl_sort -> result;
+ *     reverse all-to-all -> dm_dbl_apply; h *= 2
+ *   dm_pack_ranks -> 2 words/head; all-to-all (head counts) -> dm_load_ranks
+ *   dm_route_halo -> counts; dm_pack_halo -> 6 words/item + nhr words;
+ *     all-to-all -> dm_counter -> {bad, good, nothing, violations, errors, items}
+ *   dm_units -> int64[2*(E+n-1)]; all-reduce(sum) -> dm_emit -> nlocal;
+ *   dm_copy_stream; gather to rank 0 -> dm_finish (rank 0) -> runs.
+ * flags bit 0: every shard reported stats.order_invariant. */
+int cmsbwt_dm_begin(cmsbwt_ctx* ctx, uint32_t world, uint32_t rank, uint64_t heads_total, uint64_t docs_total,
+                    uint32_t flags, const int32_t* diff, const uint8_t* hashead, int rle);
+int cmsbwt_dm_route_heads(cmsbwt_ctx* ctx, uint64_t* counts);
+int cmsbwt_dm_pack_heads(cmsbwt_ctx* ctx, int32_t* out);
+int cmsbwt_dm_group(cmsbwt_ctx* ctx, const int32_t* recv, uint64_t nrecv, uint32_t* sa_counts);
+int cmsbwt_dm_labels(cmsbwt_ctx* ctx, const uint32_t* sa_counts, uint32_t* back);
+int cmsbwt_dm_dbl_init(cmsbwt_ctx* ctx, const uint32_t* labels, uint64_t* active);
+int cmsbwt_dm_dbl_route(cmsbwt_ctx* ctx, uint64_t h, uint64_t* counts);
+int cmsbwt_dm_dbl_pack(cmsbwt_ctx* ctx, int32_t* out);
+int cmsbwt_dm_dbl_sort(cmsbwt_ctx* ctx, const int32_t* recv, uint64_t nrecv, uint32_t* result);
+int cmsbwt_dm_dbl_apply(cmsbwt_ctx* ctx, const uint32_t* back, uint64_t* active);
+int cmsbwt_dm_pack_ranks(cmsbwt_ctx* ctx, int32_t* out);
+int cmsbwt_dm_load_ranks(cmsbwt_ctx* ctx, const int32_t* recv);
+int cmsbwt_dm_route_halo(cmsbwt_ctx* ctx, uint64_t* item_counts, uint64_t* word_counts);
+int cmsbwt_dm_pack_halo(cmsbwt_ctx* ctx, int32_t* headers, int32_t* words);
+int cmsbwt_dm_counter(cmsbwt_ctx* ctx, const int32_t* headers, uint64_t nitems, const int32_t* words,
+                      uint64_t nwords, uint64_t* stats6);
+int cmsbwt_dm_units(cmsbwt_ctx* ctx, int64_t* units);
+int cmsbwt_dm_emit(cmsbwt_ctx* ctx, const int64_t* units, uint64_t* nlocal);
+int cmsbwt_dm_copy_stream(cmsbwt_ctx* ctx, uint64_t* starts, uint8_t* chars);
+/* rank 0: starts/chars/counts per source rank (device pointers); gstats =
+ * {heads, keys, ndocs, chars, bad, good, nothing, violations} over all ranks */
+int cmsbwt_dm_finish(cmsbwt_ctx* ctx, const uint64_t* const* starts, const uint8_t* const* chars,
+                     const uint64_t* counts, const uint64_t* gstats);
+
 /* Host-only helpers (no GPU needed), exposed for tests of the host logic:
  * the collection reader (FN:1138-1275) and the reference suffix array
  * (libsais call site FN:247).  For the reader, pass NULL buffers to query

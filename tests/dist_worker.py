@@ -68,9 +68,71 @@ def gpu_sharded(rank, world, port, work):
     b, e = cdist.shard_range(len(docs), world, rank)
     eng.load_collection([bytes.fromhex(d) for d in docs[b:e]])
     for _ in range(2):  # twice: the second step reuses imported state correctly
-        cdist.sharded_step(eng, "cpu", rle=True)
+        cdist.gather_step(eng, "cpu", rle=True)
     if rank == 0:
         open(os.path.join(work, "runs.bin"), "wb").write(eng.runs_bytes())
+    eng.close()
+    dist.destroy_process_group()
+
+
+def cpu_transport(rank, world, port, work):
+    """The sharded merge's exchange primitives on host tensors: uneven
+    all-to-all (records of several words, empty splits), count exchange,
+    all-reduce and all-gather, checked against their definitions."""
+    import torch
+    import cmsbwt.dist as cdist
+    dist = _init(rank, world, port)
+    x = cdist.Transport("cpu")
+    assert (x.world, x.rank, x.staged) == (world, rank, False)
+    # rank r sends (r + d) % 3 records of 5 words to rank d; record = (r, d, k, r*d, -1)
+    send_counts = [(rank + d) % 3 for d in range(world)]
+    rows = [[rank, d, k, rank * d, -1] for d in range(world) for k in range(send_counts[d])]
+    send = torch.tensor(rows, dtype=torch.int32).reshape(-1, 5)
+    recv_counts = x.counts(send_counts)
+    assert recv_counts == [(s + rank) % 3 for s in range(world)]
+    got = x.a2a(send, send_counts, recv_counts)
+    want = [[s, rank, k, s * rank, -1] for s in range(world) for k in range(recv_counts[s])]
+    assert got.tolist() == want
+    # gather-to-rank-0 pattern of the run streams (uint8 and int64)
+    n = 3 + rank
+    sc = [n if d == 0 else 0 for d in range(world)]
+    counts = [v[0] for v in x.allgather_ints([n])]
+    rc = counts if rank == 0 else [0] * world
+    g8 = x.a2a(torch.full((n,), 7 + rank, dtype=torch.uint8), sc, rc)
+    g64 = x.a2a(torch.full((n,), (1 << 40) + rank, dtype=torch.int64), sc, rc)
+    if rank == 0:
+        assert g8.tolist() == [7 + r for r in range(world) for _ in range(3 + r)]
+        assert g64.tolist() == [(1 << 40) + r for r in range(world) for _ in range(3 + r)]
+    # all-reduce sum / max
+    t = torch.arange(6, dtype=torch.int64) * (rank + 1)
+    x.allreduce(t, "sum")
+    assert t.tolist() == [k * world * (world + 1) // 2 for k in range(6)]
+    u = torch.tensor([rank, 5 - rank], dtype=torch.uint8)
+    x.allreduce(u, "max")
+    assert u.tolist() == [world - 1, 5]
+    if rank == 0:
+        open(os.path.join(work, "ok"), "w").write("ok")
+    dist.destroy_process_group()
+
+
+def gpu_position_sharded(rank, world, port, work):
+    """Ranks sharing one GPU run the position-sharded merge over gloo (device
+    tensors staged through host memory); rank 0 writes its runs."""
+    import cmsbwt
+    import cmsbwt.dist as cdist
+    dist = _init(rank, world, port)
+    cfg = json.load(open(os.path.join(work, "cfg.json")))
+    eng = cmsbwt.Engine(0)
+    eng.initialize_reference(cfg["ref"])
+    docs = cfg["docs"]
+    b, e = cdist.shard_range(len(docs), world, rank)
+    eng.load_collection([bytes.fromhex(d) for d in docs[b:e]])
+    x = cdist.Transport("cuda:0")
+    for it in range(cfg.get("steps", 1)):
+        cdist.sharded_step(eng, "cuda:0", rle=cfg["rle"], xfer=x)
+        if rank == 0:
+            open(os.path.join(work, f"runs{it}.bin"), "wb").write(eng.runs_bytes())
+            json.dump(eng.stats().as_dict(), open(os.path.join(work, "stats.json"), "w"))
     eng.close()
     dist.destroy_process_group()
 

@@ -1,0 +1,76 @@
+"""GPU: the position-sharded merge (dist_merge.hip, cmsbwt.dist.sharded_step)
+produces the oracle's .rl_bwt / .bwt bytes and statistics.
+
+world == 1 runs every stage of the sharded pipeline in one process (identity
+exchange); world 2 and 3 run as processes sharing the test GPU, exchanging over
+gloo (host staging) exactly the collectives bench.py issues over RCCL."""
+import json
+import os
+
+import pytest
+
+import cases
+from test_multirank import spawn
+
+pytestmark = pytest.mark.gpu
+
+
+def _oracle_files(oracle, tmp_path, case, rle):
+    d, rp, cp, prefix = cases.materialise(tmp_path, case)
+    rc, ost, _ = oracle.run(rp, cp, os.path.join(d, "oracle"), rle=rle, prefix=prefix)
+    assert rc == 0
+    want = open(os.path.join(d, "oracle") + (".rl_bwt" if rle else ".bwt"), "rb").read()
+    return d, rp, cp, prefix, ost, want
+
+
+def _expand(runs: bytes) -> bytes:
+    import cmsbwt
+    lens, chars = cmsbwt.decode_rl(runs)
+    return b"".join(bytes([c]) * int(k) for k, c in zip(lens, chars))
+
+
+@pytest.mark.parametrize("rle", [True, False], ids=["rl_bwt", "bwt"])
+@pytest.mark.parametrize("case", cases.small_cases(), ids=lambda c: c[0])
+def test_sharded_world1_matches_oracle(engine, oracle, tmp_path, case, rle):
+    import cmsbwt.dist as cdist
+    d, rp, cp, prefix, ost, want = _oracle_files(oracle, tmp_path, case, rle)
+    engine.initialize_reference(rp)
+    engine.load_collection_file(cp, prefix)
+    cdist.sharded_step(engine, "cuda:0", rle=rle, xfer=cdist.Transport("cuda:0", 1, 0))
+    runs = engine.runs_bytes()
+    assert (runs if rle else _expand(runs)) == want
+    st = engine.stats()
+    assert (st.heads, st.keys, st.rank) == (ost["heads"], ost["keys"], ost["rank"])
+    assert (st.counter_bad, st.counter_good, st.counter_nothing) == (ost["bad"], ost["good"], ost["nothing"])
+
+
+def _multi(oracle, tmp_path, case, world, rle, steps=1):
+    d, rp, cp, prefix, ost, want = _oracle_files(oracle, tmp_path, case, rle)
+    docs, _ = cases.py_read_docs(open(cp, "rb").read(), prefix)
+    if len(docs) < world:
+        pytest.skip("fewer documents than ranks")
+    work = str(tmp_path)
+    json.dump({"ref": rp, "docs": [x.hex() for x in docs], "rle": rle, "steps": steps},
+              open(os.path.join(work, "cfg.json"), "w"))
+    spawn("gpu_position_sharded", world, work)
+    for it in range(steps):
+        runs = open(os.path.join(work, f"runs{it}.bin"), "rb").read()
+        assert (runs if rle else _expand(runs)) == want, f"step {it}"
+    st = json.load(open(os.path.join(work, "stats.json")))
+    assert (st["heads"], st["keys"], st["rank"]) == (ost["heads"], ost["keys"], ost["rank"])
+    assert (st["counter_bad"], st["counter_good"], st["counter_nothing"]) == (ost["bad"], ost["good"], ost["nothing"])
+
+
+MULTI = ["copies_5k_1pct", "copies_20k_multiline", "copies_3k_5pct", "identical_copies", "unrelated_random",
+         "blank_lines_and_empty_docs", "tiny_docs", "prefix_cut"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("case", [c for c in cases.small_cases() if c[0] in MULTI], ids=lambda c: c[0])
+def test_sharded_multi_rank_matches_oracle(oracle, tmp_path, case, world):
+    _multi(oracle, tmp_path, case, world, rle=True)
+
+
+def test_sharded_four_ranks_plain_bwt_repeated(oracle, tmp_path):
+    case = ("copies_40k",) + cases.copies_case(7, 40000, 9, 0.004) + (cases.UINT64_MAX,)
+    _multi(oracle, tmp_path, case, 4, rle=False, steps=2)

@@ -69,3 +69,10 @@ def test_shard_range_partitions(world):
         assert rs[0][0] == 0 and rs[-1][1] == total
         assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
         assert max(b - a for a, b in rs) - min(b - a for a, b in rs) <= 1
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_merge_transport_gloo(tmp_path, world):
+    """The exchange primitives of the position-sharded merge (cmsbwt.dist.Transport)."""
+    spawn("cpu_transport", world, str(tmp_path))
+    assert os.path.exists(os.path.join(str(tmp_path), "ok"))
