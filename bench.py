@@ -112,11 +112,12 @@ def main():
     c0, c1 = cdist.shard_range(args.copies, world, rank)
     eng.load_synth(args.seed, 1 + c0, c1 - c0, args.p, leading_empty_doc=(rank == 0))
     device = f"cuda:{local}"
-    gather = os.environ.get("CMSBWT_DIST", "sharded") == "gather"
-    xfer = cdist.Transport(device) if world > 1 else None
+    mode = os.environ.get("CMSBWT_DIST", "sharded")  # N>1: sharded | gather; "sharded1": sharded path at N=1
+    gather = mode == "gather"
+    xfer = cdist.Transport(device) if (world > 1 or mode == "sharded1") else None
 
     def step():
-        if world == 1:
+        if world == 1 and mode != "sharded1":
             eng.step(rle=True)
         elif gather:  # all heads to rank 0, single-GPU merge there
             cdist.gather_step(eng, device, rle=True)

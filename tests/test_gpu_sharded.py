@@ -74,3 +74,28 @@ def test_sharded_multi_rank_matches_oracle(oracle, tmp_path, case, world):
 def test_sharded_four_ranks_plain_bwt_repeated(oracle, tmp_path):
     case = ("copies_40k",) + cases.copies_case(7, 40000, 9, 0.004) + (cases.UINT64_MAX,)
     _multi(oracle, tmp_path, case, 4, rle=False, steps=2)
+
+
+def test_sharded_world1_config3_golden(engine):
+    """The headline workload at full size (10 MB ref + 1000 copies @0.1 %,
+    10 GB, SURVEY App. B run t4) through every stage of the sharded merge:
+    the .rl_bwt equals the oracle's (sha256 committed) and the reference's
+    recorded headNumber / Rank / run count."""
+    import hashlib
+    import sys
+    import cmsbwt.dist as cdist
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import gen_np
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+    ref, text, off = gen_np.gen_arrays(10_000_000, 1000, 0.001, 4)
+    engine.load_reference_bytes(ref)
+    engine.load_collection_array(text, off)
+    del text
+    cdist.sharded_step(engine, "cuda:0", rle=True, xfer=cdist.Transport("cuda:0", 1, 0))
+    st = engine.stats()
+    assert st.heads == g["survey"]["t4"]["headNumber"]
+    assert st.rank == g["survey"]["t4"]["Rank"]
+    assert st.runs == g["survey"]["t4"]["rl_runs"]
+    assert (st.counter_bad, st.counter_good, st.counter_nothing) == \
+        (g["t4"]["counterBad"], g["t4"]["counterGood"], g["t4"]["counterDoNothing"])
+    assert hashlib.sha256(engine.runs_bytes()).hexdigest() == g["t4"]["rl_bwt_sha256"]
