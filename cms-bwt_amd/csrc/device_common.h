@@ -32,9 +32,17 @@ struct DevRef {
   const int2* kmer;
   const uint8_t* kmap;  // 256 entries, 0xff = byte absent from the reference text
   uint32_t kmerK, kmerB;
-  // Child table (walk only): ld[k] = min(LCP[k], 2^24-1) << 8 | x[SA[k]+LCP[k]]
-  // for k >= 1; nullptr disables the small-interval extension.
+  // Child table (walk only): ld[k] = min(LCP[k], 2^16-1) << 16 | D[k] << 8 | U[k]
+  // with D[k] = x[SA[k]+LCP[k]] (where suffix k leaves suffix k-1) and
+  // U[k] = x[SA[k]+LCP[k+1]] (where it leaves suffix k+1); nullptr disables
+  // the small-interval extension.
   const uint32_t* ld;
+  // Adjacency records (walk only), 4 words each: r, then LCP[r], LCP[r-1] ..
+  // LCP[r-5] and LCP[r+1] .. LCP[r+6] as bytes clipped to 255.  pr[k] is the
+  // record of r = psi(k) = ISA[SA[k]+1] (r = 0xffffffff when SA[k] = n-1),
+  // ir[q] the record of r = ISA[q].  nullptr disables them.
+  const uint4* pr;
+  const uint4* ir;
 };
 
 // One restart chunk of the MS walk: positions [a, b) of document `doc`.

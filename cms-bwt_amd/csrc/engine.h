@@ -168,6 +168,7 @@ struct Engine {
   DBuf<uint32_t> disa;
   DBuf<int2> dkmer;
   DBuf<uint32_t> dld;
+  DBuf<uint4> dpr, dir;
   DBuf<uint8_t> dkmap;
   DevRef R{};
 
@@ -361,6 +362,7 @@ struct Engine {
     R.n = n;
     build_kmer_table();
     build_child_table();
+    build_adjacency_records();
     sync();
     refLoaded = true;
     stats.n = n;
@@ -420,27 +422,73 @@ struct Engine {
     R.kmerB = B;
   }
 
-  // Child table of the uniform-step walk: ld[k] packs LCP[k] (clipped to 24
+  // Child table of the uniform-step walk: ld[k] packs LCP[k] (clipped to 16
   // bits) with D[k] = x[SA[k] + LCP[k]], the first character in which suffix
-  // SA[k] differs from SA[k-1].  Inside an lcp-interval of depth off, the
-  // children start at lb and at every k with LCP[k] == off, and D[k] is the
-  // child's character, so one character of computeMSFactorAt over a small
-  // interval needs one window of ld instead of two binary searches.
+  // SA[k] differs from SA[k-1], and U[k] = x[SA[k] + LCP[k+1]], the one in
+  // which it differs from SA[k+1].  Inside an lcp-interval of depth off the
+  // children start at lb and at every k with LCP[k] == off; child j > 0 has
+  // character D[start], the first child U[(start of child 1) - 1], so one
+  // character of computeMSFactorAt over a small interval needs one window of
+  // ld instead of two binary searches (FN:94-149).
   void build_child_table() {
     R.ld = nullptr;
     if (!env_u32("CMSBWT_EXT8", 1)) return;
     const uint32_t n = hix.n;
     std::vector<uint32_t> ld((size_t)n + 16, 0);
-    for (uint32_t k = 1; k < n; k++) {
-      const uint32_t l = (uint32_t)std::max<int32_t>(hix.lcp[k], 0);
-      const uint64_t at = (uint64_t)(uint32_t)hix.sa[k] + l;
-      const uint8_t d = at < n ? (uint8_t)hix.x[at] : 0;
-      ld[k] = (std::min<uint32_t>(l, 0xffffffu) << 8) | d;
+    auto chr = [&](uint32_t k, int32_t l) -> uint32_t {
+      const uint64_t at = (uint64_t)(uint32_t)hix.sa[k] + (uint32_t)std::max<int32_t>(l, 0);
+      return at < n ? (uint8_t)hix.x[at] : 0u;
+    };
+    for (uint32_t k = 0; k < n; k++) {
+      const int32_t l = std::max<int32_t>(hix.lcp[k], 0);
+      const uint32_t d = k ? chr(k, l) : 0u;
+      const uint32_t u = hix.lcp[k + 1] >= 0 ? chr(k, hix.lcp[k + 1]) : 0u;
+      ld[k] = (std::min<uint32_t>((uint32_t)l, 0xffffu) << 16) | (d << 8) | u;
     }
     dld.alloc((uint64_t)n + 16);
     HIPCHK(hipMemcpyAsync(dld.p, ld.data(), ((size_t)n + 16) * 4, hipMemcpyHostToDevice, st));
     sync();  // `ld` is pageable
     R.ld = dld.p;
+  }
+
+  // Adjacency records of the uniform-step walk (device_common.h): after
+  // contractLeft (FN:34-43) and after the skip loop (FN:1187) adjustInterval
+  // (FN:11-25) starts at r = psi(lb), psi(rb) or ISA[pos+1]; the record loaded
+  // with r holds the 6 LCP entries on either side, so for lengths 1..254 and
+  // intervals ending within them the new interval is known in that same load.
+  // Entries outside [0, n] are 0 and never decide: LCP[0] = 0 and LCP[n] = -1
+  // (stored as 0) end both scans first.
+  void build_adjacency_records() {
+    R.pr = R.ir = nullptr;
+    const uint32_t n = hix.n;
+    auto lc = [&](int64_t k) -> uint32_t {
+      if (k < 0 || k > (int64_t)n) return 0;
+      const int32_t v = hix.lcp[k];
+      return v < 0 ? 0u : (uint32_t)std::min<int32_t>(v, 255);
+    };
+    auto rec = [&](uint32_t r, uint32_t* o) {
+      uint32_t w[3] = {0, 0, 0};
+      for (int j = 0; j < 6; j++) w[j / 4] |= lc((int64_t)r - j) << (8 * (j % 4));
+      for (int j = 0; j < 6; j++) w[(6 + j) / 4] |= lc((int64_t)r + 1 + j) << (8 * ((6 + j) % 4));
+      o[0] = r;
+      o[1] = w[0];
+      o[2] = w[1];
+      o[3] = w[2];
+    };
+    std::vector<uint32_t> pr(4 * ((size_t)n + 16), 0), ir(4 * ((size_t)n + 16), 0);
+    for (uint32_t k = 0; k < n; k++) {
+      const uint32_t s = (uint32_t)hix.sa[k];
+      if (s == n - 1) pr[4 * (size_t)k] = 0xffffffffu;
+      else rec(hix.isa[s + 1], &pr[4 * (size_t)k]);
+      rec(hix.isa[k], &ir[4 * (size_t)k]);
+    }
+    dpr.alloc((uint64_t)n + 16);
+    dir.alloc((uint64_t)n + 16);
+    HIPCHK(hipMemcpyAsync(dpr.p, pr.data(), ((size_t)n + 16) * 16, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(dir.p, ir.data(), ((size_t)n + 16) * 16, hipMemcpyHostToDevice, st));
+    sync();  // pageable
+    R.pr = dpr.p;
+    R.ir = dir.p;
   }
 
   // =====================================================================
@@ -571,7 +619,7 @@ struct Engine {
     }
     if (w2stats.p) {
       static const char* names[32] = {"done", "next", "bs_text", "bs_sa", "bs_x", "fail_sa", "lce_sa", "lce",
-                                       "skip1", "skip0", "gallop", "skipbs", "isa1", "con1", "con2", "adj",
+                                       "skip1", "skip0", "gallop", "skipbs", "isa1", "conp", "ext1", "adj",
                                        "kmer_text", "kmer_tab", "ext_a", "ext_b", "lce_coop", "c_adj0", "c_adv",
                                        "c_post", "c_char", "-", "scan0", "scan1", "scan2", "scan3", "wave_steps",
                                        "coop_steps"};

@@ -22,14 +22,18 @@
 //   SKIP1       PLCP[T-16..T-1]                ISA1 / SKIP0 (FN:1176-1185)
 //   SKIP0       PLCP[pos+1]                    ISA1 / GALLOP
 //   GALLOP/SKIPBS  one PLCP probe              ISA1
-//   ISA1        ISA[pos+1]                     ADJ0          (FN:1187)
-//   CON1/CON2   SA[lb],SA[rb] / ISA[..+1]      ADJ0 / ADV    (FN:34-43)
+//   ISA1        record of ISA[pos+1]           ADV / ADJ0    (FN:1187, FN:11-25)
+//   CONP        records of psi(lb), psi(rb)    ADV / ADJ0    (FN:34-43, FN:11-25)
+//               (a record carries the 6 LCP entries on either side of r, so
+//               adjustInterval usually ends in the same load)
 //   ADJ         8 LCP entries for PSV + 8 for NSV  ADJ / ADV (FN:11-25)
 //   KMER_TEXT/KMER_TAB  restart: K text bytes, then the K-mer's SA interval
 //               (= the state after K matched characters from the root)
-//   EXT_A/EXT_B one character over an interval of <= 16 suffixes without a
+//   EXT1        one character over an interval of <= 16 suffixes without a
 //               binary search: its children at depth off start where LCP ==
-//               off, with first characters D (= x[SA[k]+LCP[k]]) and x[SA[lb]+off]
+//               off; child characters D[start] and, for the first, U[end]
+//   EXT_A/EXT_B the same when the interval has one child at depth off (its
+//               character is x[SA[lb]+off]: SA[lb], then the byte)
 //   compute phases (no load): ADJ0 (start adjustInterval), ADV (next
 //   position, FN:1195-1196), POST (head record FN:1154-1171 and the
 //   contraction choice FN:1175-1194), CHAR (next character, FN:45-62).
@@ -61,8 +65,8 @@ enum : uint32_t {
   PH_GALLOP,
   PH_SKIPBS,
   PH_ISA1,
-  PH_CON1,
-  PH_CON2,
+  PH_CONP,
+  PH_EXT1,
   PH_ADJ,
   PH_KMER_TEXT,
   PH_KMER_TAB,
@@ -298,8 +302,34 @@ k_ms_walk2(Walk2Args A) {
     len -= s;
     pos += s;
     phase = PH_ISA1;
-    ad0 = (uintptr_t)(R.isa + pos + 1);
-    use = U0D;
+    if (R.ir) { ad0 = (uintptr_t)(R.ir + pos + 1); use = U0Q; }
+    else { ad0 = (uintptr_t)(R.isa + pos + 1); use = U0D; }
+  };
+  // adjustInterval(lo, hi, len) from the records of lo (PSV side: LCP[lo],
+  // LCP[lo-1], ..) and of hi (NSV side: LCP[hi+1], ..); the general scan
+  // (ADJ0/ADJ) when the answer is not inside them
+  auto adj_records = [&](uint32_t lo, uint32_t hi, const uint4& rl, const uint4& rh) {
+    if (len - 1u < 254u) {
+      const uint64_t pw = rl.y | ((uint64_t)rl.z << 32);          // bytes 0..5
+      const uint64_t nw = (rh.z >> 16) | ((uint64_t)rh.w << 16);  // bytes 0..5
+      int jp = -1, jn = -1;
+#pragma unroll
+      for (int j = 5; j >= 0; j--) {
+        if (((pw >> (8 * j)) & 0xff) < len) jp = j;
+        if (((nw >> (8 * j)) & 0xff) < len) jn = j;
+      }
+      if (jp >= 0 && jn >= 0) {
+        lb = (int32_t)lo - jp;
+        rb = (int32_t)hi + jn;
+        phase = PC_ADV;
+        use = 0;
+        return;
+      }
+    }
+    u0 = (int32_t)lo;
+    u5 = (int32_t)hi;
+    phase = PC_ADJ0;
+    use = 0;
   };
   // gallop (u4 = step, u1 = lo, below the cap u2 where the predicate holds)
   // then binary search on (u1, u2]
@@ -438,11 +468,11 @@ k_ms_walk2(Walk2Args A) {
         const uint64_t TT = (uint64_t)pos + 1 + len;
         ad0 = P + 4ull * (TT >= 16 ? TT - 16 : 0);
         use = U0Q | U1Q | U4Q | U5Q;
-      } else {  // FN:1190-1194: contractLeft
-        phase = PH_CON1;
-        ad0 = SA + 4ull * (uint32_t)lb;
-        ad2 = SA + 4ull * (uint32_t)rb;
-        use = U0D | U2D;
+      } else {  // FN:1190-1194: contractLeft from the psi records of lb and rb
+        phase = PH_CONP;
+        ad0 = (uintptr_t)(R.pr + (uint32_t)lb);
+        ad2 = (uintptr_t)(R.pr + (uint32_t)rb);
+        use = U0Q | U2Q;
       }
     }
     if (phase == PC_CHAR) {  // next character of computeMSFactorAt at j = i + len
@@ -450,11 +480,11 @@ k_ms_walk2(Walk2Args A) {
         phase = PH_LCE_SA;
         ad0 = SA + 4ull * (uint32_t)lb;
         use = U0D;
-      } else if (R.ld && rb - lb < 16 && len < 0xffffffu) {
-        phase = PH_EXT_A;
-        ad0 = SA + 4ull * (uint32_t)lb;
+      } else if (R.ld && rb - lb < 16 && len < 0xffffu) {
+        phase = PH_EXT1;
+        ad0 = (uintptr_t)(R.ld + lb);
         ad2 = T + i + len;
-        use = U0D | U2B;
+        use = U0Q | U1Q | U4Q | U5Q | U2B;
       } else {
         begin_bs();
       }
@@ -620,31 +650,19 @@ k_ms_walk2(Walk2Args A) {
         break;
       }
       case PH_ISA1: {
-        u0 = u5 = (int32_t)v0.x;
-        phase = PC_ADJ0;
-        use = 0;
+        if (R.ir) adj_records(v0.x, v0.x, v0, v0);
+        else { u0 = u5 = (int32_t)v0.x; phase = PC_ADJ0; use = 0; }
         break;
       }
-      case PH_CON1: {
-        const uint32_t sl = v0.x, sh = v2.x;
-        if (sl == n - 1 || sh == n - 1) {  // root (FN:37-39)
+      case PH_CONP: {
+        if (v0.x == 0xffffffffu || v2.x == 0xffffffffu) {  // SA[lb] or SA[rb] = n-1: root (FN:37-39)
           lb = 0;
           rb = (int32_t)n - 1;
           phase = PC_ADV;
           use = 0;
         } else {
-          phase = PH_CON2;
-          ad0 = (uintptr_t)(R.isa + sl + 1);
-          ad2 = (uintptr_t)(R.isa + sh + 1);
-          use = U0D | U2D;
+          adj_records(v0.x, v2.x, v0, v2);
         }
-        break;
-      }
-      case PH_CON2: {
-        u0 = (int32_t)v0.x;
-        u5 = (int32_t)v2.x;
-        phase = PC_ADJ0;
-        use = 0;
         break;
       }
       case PH_ADJ: {
@@ -658,40 +676,52 @@ k_ms_walk2(Walk2Args A) {
       case PH_EXT_A: {
         u0 = (int32_t)v2.x;  // the text character
         phase = PH_EXT_B;
-        ad0 = (uintptr_t)(R.ld + lb + 1);
+        ad0 = (uintptr_t)(R.ld + lb);
         ad2 = X + v0.x + len;
         use = U0Q | U1Q | U4Q | U5Q | U2B;
         break;
       }
+      case PH_EXT1:
       case PH_EXT_B: {
-        // children of [lb, rb] at depth off = len, in character order: the
-        // first starts at lb with character x[SA[lb]+off], the others at each
-        // k with LCP[k] == off with character D[k]
-        const uint32_t c = (uint32_t)u0;
+        // children of [lb, rb] at depth off = len, in character order: they
+        // start at lb and at each k in (lb, rb] with LCP[k] == off; child j > 0
+        // has character D[k], the first x[SA[lb]+off] (EXT_B: loaded) =
+        // U[(start of the second child) - 1] (EXT1)
+        const bool one = phase == PH_EXT1;
+        const uint32_t c = one ? (v2.x & 0xff) : (uint32_t)u0;
         const uint32_t e[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
                                 v4.x, v4.y, v4.z, v4.w, v5.x, v5.y, v5.z, v5.w};
         const int32_t S1 = rb - lb;
         bool valid = true;
-        int32_t lo = -1, hi = -1, mm = rb + 1;
-        uint32_t curChar = v2.x & 0xff;
+        int32_t lo = -1, hi = -1, mm = rb + 1, k1 = 0;
+        uint32_t curChar = one ? 0x100u : (v2.x & 0xff);
         int32_t curStart = lb;
 #pragma unroll
-        for (int k = 0; k < 15; k++) {
-          if (k < S1) {
-            const uint32_t l = e[k] >> 8;
+        for (int k = 1; k < 16; k++) {
+          if (k <= S1) {
+            const uint32_t l = e[k] >> 16;
             if (l < len) valid = false;
             if (l == len) {
-              if (curChar == c) { lo = curStart; hi = lb + k; }
+              if (!k1) {
+                k1 = k;
+                if (one) curChar = e[k - 1] & 0xff;
+              }
+              if (curChar == c) { lo = curStart; hi = lb + k - 1; }
               if (curChar > c && mm == rb + 1) mm = curStart;
-              curChar = e[k] & 0xff;
-              curStart = lb + 1 + k;
+              curChar = (e[k] >> 8) & 0xff;
+              curStart = lb + k;
             }
           }
         }
         if (curChar == c) { lo = curStart; hi = rb; }
-        if (curChar > c && mm == rb + 1) mm = curStart;
+        if (curChar > c && curChar < 0x100u && mm == rb + 1) mm = curStart;
         if (!valid) {  // not an lcp-interval of depth off (root after contraction)
           begin_bs();
+        } else if (one && !k1) {  // a single child: its character needs SA[lb]
+          phase = PH_EXT_A;
+          ad0 = SA + 4ull * (uint32_t)lb;
+          ad2 = T + i + len;
+          use = U0D | U2B;
         } else if (lo >= 0) {  // FN:79-84: one more matched character
           lb = lo;
           rb = hi;
