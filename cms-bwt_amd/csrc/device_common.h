@@ -26,11 +26,16 @@ struct DevRef {
   uint32_t lvlOff[kMaxLevels];     // lvl[k] == lcp + lvlOff[k] (one buffer, 16-B aligned levels)
   int nlvl;
   uint32_t n;
-  // Restart table (walk only): SA interval [kmer[c].x, kmer[c].y] of every
-  // K-mer over the reference's own alphabet, c = sum kmap[byte] << (B*(K-1-d));
-  // empty intervals have x > y.  kmer == nullptr disables it.
-  const int2* kmer;
-  const uint8_t* kmap;  // 256 entries, 0xff = byte absent from the reference text
+  // Prefix-rank tables (walk only): over the reference's own alphabet (kmap:
+  // byte -> symbol, 0xff = absent; B bits per symbol), for every length
+  // l = 1..kmerK and every l-symbol string P (code c = sum P[d] << B(l-1-d)),
+  // pfx[pfxOff[l] + 2c] = the number of suffixes of x smaller than P in their
+  // first l bytes (where P's SA interval starts, or P's insertion point when
+  // it does not occur) and pfx[pfxOff[l] + 2c + 1] = the number of suffixes
+  // starting with P.  pfx == nullptr disables them.
+  const uint32_t* pfx;
+  uint32_t pfxOff[17];
+  const uint8_t* kmap;  // 256 entries
   uint32_t kmerK, kmerB;
   // Child table (walk only): ld[k] = min(LCP[k], 2^16-1) << 16 | D[k] << 8 | U[k]
   // with D[k] = x[SA[k]+LCP[k]] (where suffix k leaves suffix k-1) and

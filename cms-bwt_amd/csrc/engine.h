@@ -166,7 +166,7 @@ struct Engine {
   DBuf<uint8_t> dx, dbwt;
   DBuf<int32_t> dsa, dlcp, dplcp;
   DBuf<uint32_t> disa;
-  DBuf<int2> dkmer;
+  DBuf<uint32_t> dpfx;
   DBuf<uint32_t> dld;
   DBuf<uint4> dpr, dir;
   DBuf<uint8_t> dkmap;
@@ -360,7 +360,7 @@ struct Engine {
     R.plcp = dplcp.p;
     R.bwt = dbwt.p;
     R.n = n;
-    build_kmer_table();
+    build_prefix_tables();
     build_child_table();
     build_adjacency_records();
     sync();
@@ -369,24 +369,40 @@ struct Engine {
     stats.t_index_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
 
-  // Restart table of the uniform-step walk: a chunk restart at the SA root
-  // (K extensions by binary search, ~2 K log n dependent loads) becomes one
-  // table lookup when the K text bytes are all reference bytes and the K-mer
-  // occurs.  The table is exactly the SA range of each K-prefix, i.e. the
-  // state computeMSFactorAt (FN:45-88) reaches after K matched characters.
-  void build_kmer_table() {
-    R.kmer = nullptr;
+  // Prefix-rank tables of the uniform-step walk (device_common.h).  With P's
+  // interval known for every l <= K, an extension of computeMSFactorAt
+  // (FN:45-88) at depth < K over a large interval jumps to the longest
+  // matching depth by a few table probes, and a mismatch there has its
+  // insertion point (FN:65-76) in the table too, instead of two binary
+  // searches (FN:94-149) per character.  Start_l[c] counts the suffixes s
+  // smaller than the l-string P of code c: those whose first l bytes are all
+  // symbols with code < c, and those whose first non-symbol byte b (or end of
+  // x) is at t < l with threshold code(s[0..t)) << B(l-t) + r(b) << B(l-1-t)
+  // <= c, r(b) = the number of symbols below b (the augmentation bytes of
+  // FN:231-237 are non-symbols anywhere in the byte order).  Stored with it:
+  // Count_l[c], the suffixes starting with P (a non-symbol may sort between P
+  // and its successor code, so the interval end is Start + Count, not the
+  // next Start).  Only ASCII references: there the walk's signed (FN:55) and
+  // unsigned orders agree.
+  void build_prefix_tables() {
+    R.pfx = nullptr;
     R.kmap = nullptr;
     R.kmerK = R.kmerB = 0;
-    if (!env_u32("CMSBWT_KMER", 1)) return;
+    memset(R.pfxOff, 0, sizeof(R.pfxOff));
+    if (!env_u32("CMSBWT_PFX", 1)) return;
     const uint32_t n = hix.n;
     uint64_t cnt[256] = {0};
     for (uint64_t k = 0; k < hix.ref_len; k++) cnt[(uint8_t)hix.x[k]]++;
     std::vector<uint8_t> map(256, 0xff);
+    std::vector<uint32_t> below(256, 0);  // r(b): symbols smaller than byte b
     uint32_t sigma = 0;
-    for (int c = 0; c < 256; c++)
+    for (int c = 0; c < 256; c++) {
+      below[c] = sigma;
       if (cnt[c]) map[c] = (uint8_t)sigma++;
+    }
     if (sigma < 2 || sigma > 64) return;
+    for (int c = 128; c < 256; c++)
+      if (cnt[c]) return;  // ASCII references only
     uint32_t B = 1;
     while ((1u << B) < sigma) B++;
     uint32_t lg = 1;
@@ -394,29 +410,50 @@ struct Engine {
     const uint32_t maxBits = std::min<uint32_t>(env_u32("CMSBWT_KMER_BITS", 24), std::max<uint32_t>(lg + 1, 12));
     const uint32_t K = std::min<uint32_t>(maxBits / B, 16);
     if (K < 3) return;
-    const uint64_t entries = 1ull << (B * K);
-    std::vector<int2> tab(entries + 2, make_int2(1, 0));
-    for (uint32_t i = 0; i < n; i++) {
-      const uint32_t s0 = (uint32_t)hix.sa[i];
-      if ((uint64_t)s0 + K > n) continue;
-      uint64_t code = 0;
-      bool ok = true;
-      for (uint32_t d = 0; d < K && ok; d++) {
-        const uint8_t m = map[(uint8_t)hix.x[s0 + d]];
-        ok = m != 0xff;
-        code = (code << B) | m;
-      }
-      if (!ok) continue;
-      int2& e = tab[code];
-      if (e.x > e.y) e = make_int2((int)i, (int)i);
-      else e.y = (int)i;  // SA order: ranges of one K-prefix are contiguous
+    uint64_t total = 0;
+    for (uint32_t l = 1; l <= K; l++) {
+      R.pfxOff[l] = (uint32_t)total;
+      total += 2 * ((1ull << (B * l)) + 1);
     }
-    dkmer.alloc(entries + 2);
-    HIPCHK(hipMemcpyAsync(dkmer.p, tab.data(), (entries + 2) * sizeof(int2), hipMemcpyHostToDevice, st));
+    std::vector<uint32_t> tab(total + 4, 0);
+    std::vector<uint32_t> cur(n, 0);
+    std::vector<uint8_t> term(n, 0);
+    std::vector<uint32_t> cf, ct;
+    for (uint32_t l = 1; l <= K; l++) {
+      const uint64_t E = 1ull << (B * l);
+      cf.assign(E + 1, 0);
+      ct.assign(E + 1, 0);
+      for (uint32_t p = 0; p < n; p++) {
+        uint32_t sym = 0;  // past the first non-symbol: zero padding
+        if (!term[p]) {
+          const uint64_t at = (uint64_t)p + l - 1;
+          if (at >= n) {  // end of x: below everything
+            term[p] = 1;
+          } else {
+            const uint8_t b = (uint8_t)hix.x[at];
+            if (map[b] == 0xff) { term[p] = 1; sym = below[b]; }  // may carry (r(b) = 2^B)
+            else sym = map[b];
+          }
+        }
+        cur[p] = (cur[p] << B) + sym;
+        (term[p] ? ct : cf)[cur[p]]++;
+      }
+      // (Start_l[c], Count_l[c]): Start = sum_{k < c} cf[k] + sum_{k <= c} ct[k]
+      uint32_t* o = tab.data() + R.pfxOff[l];
+      uint64_t sf = 0, stt = 0;
+      for (uint64_t c = 0; c <= E; c++) {
+        stt += ct[c];
+        o[2 * c] = (uint32_t)(sf + stt);
+        o[2 * c + 1] = cf[c];
+        sf += cf[c];
+      }
+    }
+    dpfx.alloc(total + 4);
+    HIPCHK(hipMemcpyAsync(dpfx.p, tab.data(), (total + 4) * 4, hipMemcpyHostToDevice, st));
     dkmap.alloc(256);
     HIPCHK(hipMemcpyAsync(dkmap.p, map.data(), 256, hipMemcpyHostToDevice, st));
     sync();  // `tab` and `map` are pageable
-    R.kmer = dkmer.p;
+    R.pfx = dpfx.p;
     R.kmap = dkmap.p;
     R.kmerK = K;
     R.kmerB = B;
@@ -620,7 +657,7 @@ struct Engine {
     if (w2stats.p) {
       static const char* names[32] = {"done", "next", "bs_text", "bs_sa", "bs_x", "fail_sa", "lce_sa", "lce",
                                        "skip1", "skip0", "gallop", "skipbs", "isa1", "conp", "ext1", "adj",
-                                       "kmer_text", "kmer_tab", "ext_a", "ext_b", "lce_coop", "c_adj0", "c_adv",
+                                       "pfx_text", "pfx_probe", "ext_a", "ext_b", "lce_coop", "c_adj0", "c_adv",
                                        "c_post", "c_char", "-", "scan0", "scan1", "scan2", "scan3", "wave_steps",
                                        "coop_steps"};
       std::vector<unsigned long long> h(32);
@@ -936,9 +973,12 @@ struct Engine {
 
     // ---- ranks (FN:1432-1453)
     DBuf<uint32_t> itemsSA, headsSA, itemRankBase, headBase;
+    // rank2head (T) is only kept for parity copies (CMSBWT_KEEP_STAGES=1):
+    // the suffix sort below needs the group labels, not the ranks themselves
+    const bool keepT = env_u32("CMSBWT_KEEP_STAGES", 0) != 0;
     itemsSA.alloc(n); headsSA.alloc(n); itemRankBase.alloc(n); headBase.alloc(n);
     mk_sa_counts(dsa.p, posBegin.p, sSlot.p, n, E, itemsSA.p, headsSA.p, st);
-    exscan(itemsSA.p, itemRankBase.p, 0u, n);
+    if (keepT) exscan(itemsSA.p, itemRankBase.p, 0u, n);
     exscan(headsSA.p, headBase.p, 0u, n);
     itemsSA.release(); headsSA.release();
     T.alloc((uint64_t)H + 1);
@@ -970,10 +1010,13 @@ struct Engine {
       DBuf<uint32_t> rankBase, gBase;
       rankBase.alloc(n);
       gBase.alloc(n);
-      mk_pos_rank_base(posBegin.p, sSlot.p, disa.p, itemRankBase.p, headBase.p, n, E, rankBase.p, gBase.p, st);
-      mk_ranks_slot(S, itemOfSlot.p, Pm.p, H, rankBase.p, gBase.p, n, T.p, saT.p, grp.p, actv.p, st);
+      mk_pos_rank_base(posBegin.p, sSlot.p, disa.p, itemRankBase.p, headBase.p, n, E, keepT ? rankBase.p : nullptr,
+                       gBase.p, st);
+      mk_ranks_slot(S, itemOfSlot.p, Pm.p, H, rankBase.p, gBase.p, n, keepT ? T.p : nullptr, saT.p, grp.p, actv.p,
+                    st);
     }
     itemRankBase.release();
+    keptT = keepT;
     stats.rank = (uint64_t)E + 2 + (uint64_t)(K - 1);
 
     // ---- suffix sort of the head string (libsais_int, FN:1455-1459)
@@ -1111,6 +1154,7 @@ struct Engine {
     stats.t_merge_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   float counter_kernel_ms = 0;
+  bool keptT = false;  // rank2head written by the last merge
   uint32_t windows = 0, crossings = 0;
   bool orderInvariant = false;  // set by ms_walk (k_finalize), false for imported shards
   uint64_t W_work = 0;
@@ -1224,7 +1268,10 @@ struct Engine {
     if (!merged) throw InputError{CMSBWT_EARG, "run merge first"};
     if (dm.on) throw InputError{CMSBWT_EARG, "merge stage arrays are not kept by the sharded merge"};
     if (name == "bucket") return cp(bucket.p, (uint64_t)R.n * 8);
-    if (name == "rank2head") return cp(T.p, ((uint64_t)H + 1) * 4);
+    if (name == "rank2head") {
+      if (!keptT) throw InputError{CMSBWT_EARG, "rank2head is kept only with CMSBWT_KEEP_STAGES=1"};
+      return cp(T.p, ((uint64_t)H + 1) * 4);
+    }
     if (name == "head2rank") return cp(saT.p, ((uint64_t)H + 1) * 4);
     if (name == "bwtheads") return cp(bwtHeads.p, H);
     if (name == "counters") return cp(counter.p, ((uint64_t)H + 1) * 8);

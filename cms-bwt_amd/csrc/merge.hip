@@ -307,7 +307,7 @@ __global__ void k_pos_rank_base(const uint32_t* __restrict__ posBegin, const uin
   const uint32_t b = posBegin[p];
   if (b == posBegin[p + 1]) return;  // no items here
   const uint32_t r = isaRef[p];
-  rankBase[p] = E + 2 + itemRankBase[r] - b;
+  if (rankBase) rankBase[p] = E + 2 + itemRankBase[r] - b;
   gBase[p] = 1 + headBase[r] - slot[b];
 }
 __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ itemOfSlot,
@@ -319,14 +319,14 @@ __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ ite
   const uint32_t q = itemOfSlot[s], idx = Pm[s];
   const uint32_t sq = it.slot[q], m = s - sq, p = it.pos[q];
   if (p == n - 1) {  // end phrases: one rank each, in document order
-    T[idx] = (int32_t)(1 + m);
+    if (T) T[idx] = (int32_t)(1 + m);
     sa[1 + m] = idx;
     grp[idx] = 1 + m;
     actv[s] = 0xffffffffu;
     return;
   }
   const uint32_t g = gBase[p] + sq;
-  T[idx] = (int32_t)(rankBase[p] + q);
+  if (T) T[idx] = (int32_t)(rankBase[p] + q);  // rank2head: kept for parity copies only
   sa[g + m] = idx;
   grp[idx] = g;
   // unresolved members (items with >= 2 heads): their sa positions

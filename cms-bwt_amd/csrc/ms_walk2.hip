@@ -27,8 +27,11 @@
 //               (a record carries the 6 LCP entries on either side of r, so
 //               adjustInterval usually ends in the same load)
 //   ADJ         8 LCP entries for PSV + 8 for NSV  ADJ / ADV (FN:11-25)
-//   KMER_TEXT/KMER_TAB  restart: K text bytes, then the K-mer's SA interval
-//               (= the state after K matched characters from the root)
+//   PFX_TEXT    K text bytes: codes of t[i..i+l) for l <= K   PFX_PROBE / BS
+//   PFX_PROBE   prefix-rank table entries of length-l codes: the SA interval
+//               of t[i..i+l) or, when it does not occur, its insertion point;
+//               a binary search over l finds the longest match (restarts from
+//               the root and extensions at depth < K over large intervals)
 //   EXT1        one character over an interval of <= 16 suffixes without a
 //               binary search: its children at depth off start where LCP ==
 //               off; child characters D[start] and, for the first, U[end]
@@ -68,8 +71,8 @@ enum : uint32_t {
   PH_CONP,
   PH_EXT1,
   PH_ADJ,
-  PH_KMER_TEXT,
-  PH_KMER_TAB,
+  PH_PFX_TEXT,
+  PH_PFX_PROBE,
   PH_EXT_A,
   PH_EXT_B,
   PH_LCE_COOP,  // served by the whole wave (no lane load)
@@ -86,6 +89,12 @@ enum : uint32_t {
 #define GPTR(T, a) ((const __attribute__((address_space(1))) T*)(a))
 __device__ __forceinline__ uint32_t ld1(uintptr_t a) { return *GPTR(uint8_t, a); }
 __device__ __forceinline__ uint32_t ld4(uintptr_t a) { return *GPTR(uint32_t, a); }
+// 8 bytes at a 4-byte aligned address
+__device__ __forceinline__ uint2 ld8(uintptr_t a) {
+  typedef uint32_t u2u __attribute__((ext_vector_type(2), aligned(4)));
+  const u2u v = *GPTR(u2u, a);
+  return make_uint2(v.x, v.y);
+}
 // 16 bytes at any address (gfx950 global loads allow unaligned dwordx4)
 __device__ __forceinline__ uint4 ldu16(uintptr_t a) {
   typedef uint32_t u4u __attribute__((ext_vector_type(4), aligned(1)));
@@ -104,6 +113,8 @@ enum : uint32_t {
   U2B = 128,  // byte at B
   U4Q = 256,  // 16 B at A + 32
   U5Q = 512,  // 16 B at A + 48
+  U0E = 1024, // 8 B at A
+  U2E = 2048, // 8 B at B
 };
 // First differing byte of two 16-byte strings: 16 if equal.
 __device__ __forceinline__ uint32_t diff16(const uint4& x, const uint4& t, uint8_t& xc, uint8_t& tc) {
@@ -247,8 +258,10 @@ k_ms_walk2(Walk2Args A) {
   __shared__ unsigned long long sc[STATS ? 32 : 1];
   __shared__ uint8_t kmapL[256];
   __shared__ uint32_t lvlL[2 * kMaxLevels];
+  __shared__ uint32_t pfxL[17];
   if (STATS && threadIdx.x < 32) sc[threadIdx.x] = 0;
-  if (A.R.kmer) kmapL[threadIdx.x] = A.R.kmap[threadIdx.x];  // blockDim == 256
+  if (A.R.pfx) kmapL[threadIdx.x] = A.R.kmap[threadIdx.x];  // blockDim == 256
+  if (threadIdx.x < 17) pfxL[threadIdx.x] = A.R.pfxOff[threadIdx.x];
   if (threadIdx.x == 0) {
 #pragma unroll
     for (int k = 0; k < kMaxLevels; k++) {
@@ -296,6 +309,16 @@ k_ms_walk2(Walk2Args A) {
     ad0 = T + i + len;
     ad2 = SA + 4ull * (uint32_t)u3;
     use = U0B | U2D;
+  };
+  // next character(s) over a large interval: prefix-rank tables below depth K
+  auto begin_search = [&]() {
+    if (R.pfx && len < R.kmerK) {
+      phase = PH_PFX_TEXT;
+      ad0 = T + i;
+      use = U0Q;
+    } else {
+      begin_bs();
+    }
   };
   auto skip_done = [&](uint32_t s) {
     i += s;
@@ -405,8 +428,8 @@ k_ms_walk2(Walk2Args A) {
           rb = (int32_t)n - 1;
           prevPos = 0xfffffffeu;  // prevPos + 1 never equals a position
           smaller = false;
-          if (R.kmer) {
-            phase = PH_KMER_TEXT;
+          if (R.pfx) {
+            phase = PH_PFX_TEXT;
             ad0 = T + i;
             use = U0Q;
           } else {
@@ -486,7 +509,7 @@ k_ms_walk2(Walk2Args A) {
         ad2 = T + i + len;
         use = U0Q | U1Q | U4Q | U5Q | U2B;
       } else {
-        begin_bs();
+        begin_search();
       }
     }
 
@@ -511,6 +534,8 @@ k_ms_walk2(Walk2Args A) {
     if (use & U3Q) v3 = ldu16(ad2 + 16);
     if (use & U4Q) v4 = ldu16(ad0 + 32);
     if (use & U5Q) v5 = ldu16(ad0 + 48);
+    if (use & U0E) { const uint2 w = ld8(ad0); v0.x = w.x; v0.y = w.y; }
+    if (use & U2E) { const uint2 w = ld8(ad2); v2.x = w.x; v2.y = w.y; }
     // ---- one state-machine step (load phases)
     switch (phase) {
       case PH_BS_TEXT: {  // c = t[j]; the first probe's SA value is in slot 2
@@ -737,37 +762,89 @@ k_ms_walk2(Walk2Args A) {
         }
         break;
       }
-      case PH_KMER_TEXT: {
+      case PH_PFX_TEXT: {  // codes of the longest symbol prefix t[i..i+m), m <= K
         const uint32_t K = R.kmerK, Bb = R.kmerB;
-        uint64_t code = 0;
-        bool ok = true;
+        uint32_t code = 0, m = 0;
+        bool run = true;
 #pragma unroll
         for (uint32_t d = 0; d < 16; d++) {
-          if (d < K) {
+          if (d < K && run) {
             const uint32_t w = d < 4 ? v0.x : d < 8 ? v0.y : d < 12 ? v0.z : v0.w;
-            const uint32_t m = kmapL[(w >> (8 * (d & 3))) & 0xff];
-            ok = ok && m != 0xff;
-            code = (code << Bb) | (m & 0xff);
+            const uint32_t mp = kmapL[(w >> (8 * (d & 3))) & 0xff];
+            if (mp == 0xff) run = false;
+            else { code = (code << Bb) | mp; m = d + 1; }
           }
         }
-        if (ok) {
-          phase = PH_KMER_TAB;
-          ad0 = (uintptr_t)(R.kmer + code);
-          use = U0Q;
-        } else {
-          phase = PC_CHAR;  // from the root
-          use = 0;
+        // the next byte is no symbol (document end), or len = 0 away from the
+        // root: character by character
+        if (m <= len || (len == 0 && !(lb == 0 && rb == (int32_t)n - 1))) {
+          begin_bs();
+          break;
+        }
+        u6 = (int32_t)code;
+        u7 = (int32_t)m;
+        u8 = 0;
+        phase = PH_PFX_PROBE;
+        ad0 = (uintptr_t)(R.pfx + pfxL[m] + 2 * code);
+        use = U0E;
+        if (len > 0) {  // the interval must be exactly t[i..i+len)'s (not the root of FN:37-39)
+          ad2 = (uintptr_t)(R.pfx + pfxL[len] + 2 * (code >> (Bb * (m - len))));
+          use |= U2E;
         }
         break;
       }
-      case PH_KMER_TAB: {
-        if ((int32_t)v0.x <= (int32_t)v0.y) {
-          lb = (int32_t)v0.x;
-          rb = (int32_t)v0.y;
-          len = R.kmerK;
+      case PH_PFX_PROBE: {
+        const uint32_t Bb = R.kmerB, m = (uint32_t)u7, code = (uint32_t)u6;
+        uint32_t lo, hi, ins;
+        if (!u8) {  // depth m (and the check of depth len)
+          if (len > 0 && (v2.x != (uint32_t)lb || v2.y != (uint32_t)(rb - lb) + 1)) {
+            begin_bs();
+            break;
+          }
+          if (v0.y) {  // t[i..i+m) occurs: its interval, depth m
+            lb = (int32_t)v0.x;
+            rb = (int32_t)(v0.x + v0.y) - 1;
+            len = m;
+            phase = PC_CHAR;
+            use = 0;
+            break;
+          }
+          lo = len;
+          hi = m;
+          ins = v0.x;
+        } else {
+          lo = (uint32_t)u1;
+          hi = (uint32_t)u2;
+          ins = (uint32_t)u3;
+          if (v0.y) {
+            lo = (uint32_t)u4;
+            lb = (int32_t)v0.x;
+            rb = (int32_t)(v0.x + v0.y) - 1;
+          } else {
+            hi = (uint32_t)u4;
+            ins = v0.x;
+          }
         }
-        phase = PC_CHAR;
-        use = 0;
+        if (hi - lo > 1) {  // t[i..i+lo) occurs, t[i..i+hi) does not
+          const uint32_t mid = (lo + hi) >> 1;
+          u1 = (int32_t)lo;
+          u2 = (int32_t)hi;
+          u3 = (int32_t)ins;
+          u4 = (int32_t)mid;
+          u8 = 1;
+          ad0 = (uintptr_t)(R.pfx + pfxL[mid] + 2 * (code >> (Bb * (m - mid))));
+          use = U0E;
+          break;
+        }
+        // depth lo matches and the symbol at lo does not: insertion point of
+        // t[i..i+lo+1) (FN:65-76)
+        len = lo;
+        int32_t mm = (int32_t)ins;
+        smaller = true;
+        if (mm == rb + 1) { mm = rb; smaller = false; }
+        phase = PH_FAIL_SA;
+        ad0 = SA + 4ull * (uint32_t)mm;
+        use = U0D;
         break;
       }
       default:

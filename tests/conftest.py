@@ -5,6 +5,8 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+# parity tests compare every stage array, including rank2head (not kept by default)
+os.environ.setdefault("CMSBWT_KEEP_STAGES", "1")
 sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "cms-bwt_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
