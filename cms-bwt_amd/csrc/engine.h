@@ -1040,16 +1040,33 @@ struct Engine {
       DBuf<uint64_t> k64, k64b;
       val.alloc(U); val2.alloc(U); lab.alloc(U); labMax.alloc(U); keep.alloc(U);
       k64.alloc(U); k64b.alloc(U);
-      // groups are visited in suffix-array order (k_dbl_apply writes the
-      // u-th smallest key to the u-th smallest active sa position): act is
-      // sorted above
+      // groups are visited in suffix-array order (a group's members take its
+      // sa positions in key order): act is sorted above, so every group is a
+      // contiguous range of act.  Groups of <= 32 members are sorted by one
+      // thread each; the members of larger groups by one radix sort.
+      const uint32_t maxSmall = env_u32("CMSBWT_DBL_SMALL", 32);
+      DBuf<uint32_t> gflag, gs, big, io, origB, actB, valB, keepB;
+      DBuf<uint64_t> keyB;
+      gflag.alloc(U); gs.alloc(U); big.alloc(U); io.alloc(U);
+      mk_iota(io.p, U, st);
       for (uint64_t hstep = 1; U > 0; hstep <<= 1) {
         if (hstep > H) throw InputError{CMSBWT_EINPUT, "internal: head-string suffix sort did not converge"};
         mk_dbl_keys(act.p, saT.p, grp.p, (uint32_t)hstep, U, k64.p, val.p, st);
-        sort_pairs(k64.p, k64b.p, val.p, val2.p, U, 32 + bH);
-        mk_dbl_apply(act.p, k64b.p, val2.p, U, saT.p, lab.p, st);
-        inscan(lab.p, labMax.p, U, rocprim::maximum<uint32_t>());
-        mk_dbl_groups(act.p, k64b.p, val2.p, labMax.p, U, grp.p, keep.p, st);
+        mk_dbl_gstart(k64.p, U, gflag.p, st);
+        const uint32_t G = select_flagged(io.p, gflag.p, gs.p, U);
+        HIPCHK(hipMemsetAsync(big.p, 0, (size_t)U * 4, st));
+        mk_dbl_small(gs.p, G, U, act.p, k64.p, val.p, saT.p, grp.p, keep.p, big.p, maxSmall, st);
+        origB.alloc(U);
+        const uint32_t B = select_flagged(io.p, big.p, origB.p, U);
+        if (B) {
+          actB.alloc(B); valB.alloc(B); keyB.alloc(B); keepB.alloc(B);
+          mk_dbl_gather_big(origB.p, B, act.p, k64.p, val.p, actB.p, keyB.p, valB.p, st);
+          sort_pairs(keyB.p, k64b.p, valB.p, val2.p, B, 32 + bH);
+          mk_dbl_apply(actB.p, k64b.p, val2.p, B, saT.p, lab.p, st);
+          inscan(lab.p, labMax.p, B, rocprim::maximum<uint32_t>());
+          mk_dbl_groups(actB.p, k64b.p, val2.p, labMax.p, B, grp.p, keepB.p, st);
+          mk_scatter_u32(keepB.p, origB.p, B, keep.p, st);
+        }
         U = select_flagged(act.p, keep.p, act2.p, U);
         std::swap(act.p, act2.p);
       }

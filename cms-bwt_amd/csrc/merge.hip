@@ -257,6 +257,63 @@ __global__ void k_dbl_groups(const uint32_t* __restrict__ act, const uint64_t* _
   keep[u] = (startHere && endHere) ? 0u : 1u;
 }
 
+// ---- per-group doubling round.  Keys are in act order and a group is a run
+// of equal high words (its label), so each group is a contiguous range: small
+// groups are sorted by one thread each, large ones go through a radix sort.
+__global__ void k_dbl_gstart(const uint64_t* __restrict__ key, uint32_t U, uint32_t* __restrict__ flag) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u < U) flag[u] = (u == 0 || (key[u] >> 32) != (key[u - 1] >> 32)) ? 1u : 0u;
+}
+__global__ void k_dbl_small(const uint32_t* __restrict__ gs, uint32_t G, uint32_t U, const uint32_t* __restrict__ act,
+                            uint64_t* __restrict__ key, uint32_t* __restrict__ val, uint32_t* __restrict__ sa,
+                            uint32_t* __restrict__ grp, uint32_t* __restrict__ keep, uint32_t* __restrict__ big,
+                            uint32_t maxSmall) {
+  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
+  if (g >= G) return;
+  const uint32_t u0 = gs[g], u1 = g + 1 < G ? gs[g + 1] : U;
+  if (u1 - u0 > maxSmall) {
+    for (uint32_t u = u0; u < u1; u++) big[u] = 1;
+    return;
+  }
+  for (uint32_t a = u0 + 1; a < u1; a++) {  // insertion sort by (label, label of suffix + h)
+    const uint64_t kk = key[a];
+    const uint32_t vv = val[a];
+    uint32_t b = a;
+    while (b > u0 && key[b - 1] > kk) {
+      key[b] = key[b - 1];
+      val[b] = val[b - 1];
+      b--;
+    }
+    key[b] = kk;
+    val[b] = vv;
+  }
+  // the u-th member takes the group's u-th sa position; equal keys share the
+  // label of their first position; a member alone in its run is resolved
+  uint32_t rs = u0;
+  for (uint32_t u = u0; u < u1; u++) {
+    if (u > u0 && key[u] != key[u - 1]) rs = u;
+    const bool endRun = u + 1 == u1 || key[u + 1] != key[u];
+    sa[act[u]] = val[u];
+    grp[val[u]] = act[rs];
+    keep[u] = (rs == u && endRun) ? 0u : 1u;
+  }
+}
+__global__ void k_dbl_gather_big(const uint32_t* __restrict__ orig, uint32_t B, const uint32_t* __restrict__ act,
+                                 const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                                 uint32_t* __restrict__ actB, uint64_t* __restrict__ keyB, uint32_t* __restrict__ valB) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint32_t u = orig[b];
+  actB[b] = act[u];
+  keyB[b] = key[u];
+  valB[b] = val[u];
+}
+__global__ void k_scatter_u32(const uint32_t* __restrict__ src, const uint32_t* __restrict__ idx, uint32_t n,
+                              uint32_t* __restrict__ dst) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < n) dst[idx[b]] = src[b];
+}
+
 // FN:1468-1472: rank of each head and BWTheads (listOfChars in rank order)
 __global__ void k_head_ranks(const uint32_t* __restrict__ sa, const uint8_t* __restrict__ lchar, uint32_t H,
                              uint32_t* __restrict__ headRank, uint8_t* __restrict__ bwtHeads) {
@@ -1010,6 +1067,20 @@ void mk_dbl_apply(const uint32_t* act, const uint64_t* key, const uint32_t* val,
 void mk_dbl_groups(const uint32_t* act, const uint64_t* key, const uint32_t* val, const uint32_t* labMax,
                    uint32_t U, uint32_t* grp, uint32_t* keep, hipStream_t st) {
   if (U) hipLaunchKernelGGL(k_dbl_groups, g1(U), dim3(256), 0, st, act, key, val, labMax, U, grp, keep);
+}
+void mk_dbl_gstart(const uint64_t* key, uint32_t U, uint32_t* flag, hipStream_t st) {
+  if (U) hipLaunchKernelGGL(k_dbl_gstart, g1(U), dim3(256), 0, st, key, U, flag);
+}
+void mk_dbl_small(const uint32_t* gs, uint32_t G, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val,
+                  uint32_t* sa, uint32_t* grp, uint32_t* keep, uint32_t* big, uint32_t maxSmall, hipStream_t st) {
+  if (G) hipLaunchKernelGGL(k_dbl_small, g1(G), dim3(256), 0, st, gs, G, U, act, key, val, sa, grp, keep, big, maxSmall);
+}
+void mk_dbl_gather_big(const uint32_t* orig, uint32_t B, const uint32_t* act, const uint64_t* key, const uint32_t* val,
+                       uint32_t* actB, uint64_t* keyB, uint32_t* valB, hipStream_t st) {
+  if (B) hipLaunchKernelGGL(k_dbl_gather_big, g1(B), dim3(256), 0, st, orig, B, act, key, val, actB, keyB, valB);
+}
+void mk_scatter_u32(const uint32_t* src, const uint32_t* idx, uint32_t n, uint32_t* dst, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_scatter_u32, g1(n), dim3(256), 0, st, src, idx, n, dst);
 }
 void mk_head_ranks(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint32_t* headRank, uint8_t* bwtHeads,
                    hipStream_t st) {

@@ -76,6 +76,13 @@ void mk_dbl_groups(const uint32_t* act, const uint64_t* key, const uint32_t* val
                    uint32_t U, uint32_t* grp, uint32_t* keep, hipStream_t st);
 void mk_head_ranks(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint32_t* headRank, uint8_t* bwtHeads,
                    hipStream_t st);
+// per-group doubling round (small groups sorted by one thread each)
+void mk_dbl_gstart(const uint64_t* key, uint32_t U, uint32_t* flag, hipStream_t st);
+void mk_dbl_small(const uint32_t* gs, uint32_t G, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val,
+                  uint32_t* sa, uint32_t* grp, uint32_t* keep, uint32_t* big, uint32_t maxSmall, hipStream_t st);
+void mk_dbl_gather_big(const uint32_t* orig, uint32_t B, const uint32_t* act, const uint64_t* key, const uint32_t* val,
+                       uint32_t* actB, uint64_t* keyB, uint32_t* valB, hipStream_t st);
+void mk_scatter_u32(const uint32_t* src, const uint32_t* idx, uint32_t n, uint32_t* dst, hipStream_t st);
 void mk_nhr_keys(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uint32_t* headRank,
                  const uint16_t* nexthead, uint64_t* key, hipStream_t st);
 void mk_low32(const uint64_t* key, uint32_t* out, uint64_t n, hipStream_t st);

@@ -88,6 +88,14 @@ def test_counter_window_geometry(engine, oracle, tmp_path, case, geom):
     _compare(engine, oracle, tmp_path, case, env=geom)
 
 
+@pytest.mark.parametrize("small", ["2", "1000000"], ids=["radix_groups", "thread_groups"])
+@pytest.mark.parametrize("case", cases.small_cases()[:4], ids=lambda c: c[0])
+def test_doubling_group_paths(engine, oracle, tmp_path, case, small):
+    """Head-string suffix sort: groups above CMSBWT_DBL_SMALL members go through
+    the radix path, smaller ones are sorted per thread; both give the oracle's SA."""
+    _compare(engine, oracle, tmp_path, case, env={"CMSBWT_DBL_SMALL": small})
+
+
 @pytest.mark.parametrize("case", cases.large_cases(), ids=lambda c: c[0])
 def test_large_reference_path(engine, oracle, tmp_path, case):
     _compare(engine, oracle, tmp_path, case, rle=True)
