@@ -140,6 +140,11 @@ struct DBuf {
     owner = nullptr;
   }
   uint64_t bytes() const { return n * sizeof(T); }
+  void swap_in(DBuf& o) {  // take o's buffer (ours goes to o)
+    std::swap(p, o.p);
+    std::swap(n, o.n);
+    std::swap(owner, o.owner);
+  }
 };
 
 static uint32_t env_u32(const char* name, uint32_t dflt) {
@@ -846,21 +851,19 @@ struct Engine {
     mk_item_count(aFirst.p, aCount.p, K, H, st);
     key.release();
     key2.release();
-    // map order inside each position (match.h:27-33): stable sort by class/len, then by pos
-    DBuf<uint32_t> io, io2, ik, ik2;
-    io.alloc(K); io2.alloc(K); ik.alloc(K); ik2.alloc(K);
-    mk_iota(io.p, K, st);
-    mk_item_key(aLen.p, aSmall.p, io.p, ik.p, K, st);
-    sort_pairs(ik.p, ik2.p, io.p, io2.p, K, 32);
-    mk_gather(aPos.p, io2.p, ik.p, K, st);
-    sort_pairs(ik.p, ik2.p, io2.p, io.p, K, bN);
-    ik.release(); ik2.release(); io2.release();
+    // map order inside each position (match.h:27-33): one thread per
+    // position reorders its items, already sorted by (len, isaNext)
+    DBuf<uint32_t> pbA, order;
+    pbA.alloc((uint64_t)n + 1);
+    order.alloc(K);
+    mk_pos_begin(aPos.p, K, n, pbA.p, st);
+    mk_map_order(pbA.p, aLen.p, aSmall.p, n, order.p, st);
     S.pos.alloc(K); S.len.alloc(K); S.isa.alloc(K); S.until.alloc(K); S.count.alloc(K); S.first.alloc(K);
     S.slot.alloc((uint64_t)K + 1); S.small.alloc(K); S.sk.alloc(K);
     ItemsSoA SS = S.soa();
-    mk_item_permute(A0, io.p, SS, K, st);
+    mk_item_permute(A0, order.p, SS, K, st);
     mk_item_sk(SS, K, st);
-    io.release();
+    order.release();
     aPos.release(); aLen.release(); aIsa.release(); aUntil.release(); aCount.release(); aFirst.release();
     aSmall.release();
     // slots = prefixSumForPositions (FN:1504-1515)
@@ -870,34 +873,35 @@ struct Engine {
       HIPCHK(hipMemcpyAsync(S.slot.p + K, &hh, 4, hipMemcpyHostToDevice, st));
       sync();  // hh is a stack variable
     }
-    S.posBegin.alloc((uint64_t)n + 1);
+    S.posBegin.swap_in(pbA);  // positions are unchanged by the reordering
     S.posF.alloc(n);
-    mk_pos_begin(S.pos.p, K, n, S.posBegin.p, st);
     mk_pos_f(S.pos.p, S.small.p, S.posBegin.p, K, n, S.posF.p, st);
   }
 
   // FN:1480-1494 sort of each item's next-head ranks (slot order): small
   // items by an in-place insertion sort, large ones by one global (item, nhr) sort
   void sort_nhr_items(const ItemsSoA& S, uint32_t K, const uint32_t* itemOfSlotP, uint32_t* nhrP, uint32_t H) {
-    DBuf<uint32_t> bigItem;
-    bigItem.alloc(K);
-    mk_nhr_sort_small(S, K, nhrP, bigItem.p, st);
-    DBuf<unsigned long long> bk, bk2, bsel;
-    DBuf<uint32_t> bflag, bslots, iotaS;
-    bk.alloc(H); bflag.alloc(H);
-    mk_nhr_big_keys(itemOfSlotP, bigItem.p, nhrP, H, bk.p, bflag.p, st);
-    bsel.alloc(H);
-    const uint32_t B = select_flagged_u64(bk.p, bflag.p, bsel.p, H);
-    if (B) {
-      iotaS.alloc(H);
-      mk_iota(iotaS.p, H, st);
-      bslots.alloc(B);
-      const uint32_t B2 = select_flagged(iotaS.p, bflag.p, bslots.p, H);
-      if (B2 != B) throw InputError{CMSBWT_EINPUT, "internal: large-item selection mismatch"};
-      bk2.alloc(B);
-      sort_keys(bsel.p, bk2.p, B, 32 + bits_for(K));
-      mk_nhr_big_back(bk2.p, bslots.p, B, nhrP, st);
-    }
+    (void)itemOfSlotP;
+    (void)H;
+    DBuf<uint32_t> bigList;
+    bigList.alloc((uint64_t)K + 1);
+    HIPCHK(hipMemsetAsync(bigList.p, 0, 4, st));
+    mk_nhr_sort_small(S, K, nhrP, bigList.p, st);
+    const uint32_t nb = K ? read1(bigList.p) : 0;
+    if (!nb) return;
+    // the large items in item order, their members at exclusive offsets
+    DBuf<uint32_t> items, cnt, off;
+    items.alloc(nb); cnt.alloc(nb); off.alloc(nb);
+    sort_keys(bigList.p + 1, items.p, nb, bits_for(K));
+    mk_item_counts_of(items.p, nb, S.count, cnt.p, st);
+    exscan(cnt.p, off.p, 0u, nb);
+    const uint32_t B = read1(off.p + (nb - 1)) + read1(cnt.p + (nb - 1));
+    DBuf<unsigned long long> bk, bk2;
+    DBuf<uint32_t> bslots;
+    bk.alloc(B); bk2.alloc(B); bslots.alloc(B);
+    mk_nhr_big_fill(items.p, off.p, nb, S, nhrP, bk.p, bslots.p, st);
+    sort_keys(bk.p, bk2.p, B, 32 + bits_for(K));
+    mk_nhr_big_back(bk2.p, bslots.p, B, nhrP, st);
   }
 
   // counterSmallerThanHead (FN:1523-1603) over the target positions [P0, P1):

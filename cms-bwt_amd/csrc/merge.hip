@@ -257,6 +257,30 @@ __global__ void k_dbl_groups(const uint32_t* __restrict__ act, const uint64_t* _
   keep[u] = (startHere && endHere) ? 0u : 1u;
 }
 
+// ---- map order
+// map order of one position's items (sorted by (len, isaNext)): smaller=true
+// items in that order, then smaller=false items by len descending, isaNext
+// ascending for equal len (match.h:27-33 on consistent data)
+__global__ void k_map_order(const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ len,
+                            const uint8_t* __restrict__ sm, uint32_t n, uint32_t* __restrict__ order) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  const uint32_t b = posBegin[p], e = posBegin[p + 1];
+  if (b == e) return;
+  uint32_t w = b;
+  for (uint32_t q = b; q < e; q++)
+    if (sm[q]) order[w++] = q;
+  uint32_t ge = e;
+  while (ge > b) {
+    const uint32_t L = len[ge - 1];
+    uint32_t gs = ge - 1;
+    while (gs > b && len[gs - 1] == L) gs--;
+    for (uint32_t q = gs; q < ge; q++)
+      if (!sm[q]) order[w++] = q;
+    ge = gs;
+  }
+}
+
 // ---- per-group doubling round.  Keys are in act order and a group is a run
 // of equal high words (its label), so each group is a contiguous range: small
 // groups are sorted by one thread each, large ones go through a radix sort.
@@ -398,14 +422,15 @@ __global__ void k_nhr_slot(const uint32_t* __restrict__ Pm, const uint32_t* __re
   nhr[s] = headRank[idx + nexthead[idx]];
 }
 // Sort each item's nhr segment: insertion sort in place for <= kSmallSeg
-// members; larger items are flagged (slot-wise) for one global sort.
+// members; larger items are appended to a list (bigList[0] = their number)
+// for one global sort of their members.
 constexpr uint32_t kSmallSeg = 32;
 __global__ void k_nhr_sort_small(const ItemsSoA it, uint32_t K, uint32_t* __restrict__ nhr,
-                                 uint32_t* __restrict__ bigItem) {
+                                 uint32_t* __restrict__ bigList) {
   uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= K) return;
   const uint32_t c = it.count[q];
-  bigItem[q] = c > kSmallSeg ? 1u : 0u;
+  if (c > kSmallSeg) bigList[1 + atomicAdd(bigList, 1u)] = q;
   if (c < 2 || c > kSmallSeg) return;
   uint32_t* a = nhr + it.slot[q];
   for (uint32_t x = 1; x < c; x++) {
@@ -415,15 +440,21 @@ __global__ void k_nhr_sort_small(const ItemsSoA it, uint32_t K, uint32_t* __rest
     a[y] = v;
   }
 }
-// keys (item, nhr) and slots of the members of large items
-__global__ void k_nhr_big_keys(const uint32_t* __restrict__ itemOfSlot, const uint32_t* __restrict__ bigItem,
-                               const uint32_t* __restrict__ nhr, uint32_t H, unsigned long long* __restrict__ key,
-                               uint32_t* __restrict__ flag) {
-  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= H) return;
-  const uint32_t q = itemOfSlot[s];
-  flag[s] = bigItem[q];
-  key[s] = ((unsigned long long)q << 32) | nhr[s];
+// keys (item, nhr) and slots of the members of the large items (list sorted
+// by item, members at the exclusive offsets of their counts): one block per item
+__global__ void k_nhr_big_fill(const uint32_t* __restrict__ items, const uint32_t* __restrict__ off,
+                               const ItemsSoA it, const uint32_t* __restrict__ nhr,
+                               unsigned long long* __restrict__ key, uint32_t* __restrict__ slots) {
+  const uint32_t q = items[blockIdx.x], o = off[blockIdx.x], s0 = it.slot[q], c = it.count[q];
+  for (uint32_t m = threadIdx.x; m < c; m += blockDim.x) {
+    key[o + m] = ((unsigned long long)q << 32) | nhr[s0 + m];
+    slots[o + m] = s0 + m;
+  }
+}
+__global__ void k_item_counts_of(const uint32_t* __restrict__ items, uint32_t nb, const uint32_t* __restrict__ count,
+                                 uint32_t* __restrict__ out) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b < nb) out[b] = count[items[b]];
 }
 __global__ void k_nhr_big_back(const unsigned long long* __restrict__ sorted, const uint32_t* __restrict__ slots,
                                uint32_t B, uint32_t* __restrict__ nhr) {
@@ -1009,12 +1040,15 @@ void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, const uint16_t* n
                  hipStream_t st) {
   if (H) hipLaunchKernelGGL(k_nhr_slot, g1(H), dim3(256), 0, st, Pm, headRank, nexthead, H, nhr);
 }
-void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigItem, hipStream_t st) {
-  if (K) hipLaunchKernelGGL(k_nhr_sort_small, g1(K), dim3(256), 0, st, it, K, nhr, bigItem);
+void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigList, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_nhr_sort_small, g1(K), dim3(256), 0, st, it, K, nhr, bigList);
 }
-void mk_nhr_big_keys(const uint32_t* itemOfSlot, const uint32_t* bigItem, const uint32_t* nhr, uint32_t H,
-                     unsigned long long* key, uint32_t* flag, hipStream_t st) {
-  if (H) hipLaunchKernelGGL(k_nhr_big_keys, g1(H), dim3(256), 0, st, itemOfSlot, bigItem, nhr, H, key, flag);
+void mk_nhr_big_fill(const uint32_t* items, const uint32_t* off, uint32_t nb, const ItemsSoA& it, const uint32_t* nhr,
+                     unsigned long long* key, uint32_t* slots, hipStream_t st) {
+  if (nb) hipLaunchKernelGGL(k_nhr_big_fill, dim3(nb), dim3(256), 0, st, items, off, it, nhr, key, slots);
+}
+void mk_item_counts_of(const uint32_t* items, uint32_t nb, const uint32_t* count, uint32_t* out, hipStream_t st) {
+  if (nb) hipLaunchKernelGGL(k_item_counts_of, g1(nb), dim3(256), 0, st, items, nb, count, out);
 }
 void mk_nhr_big_back(const unsigned long long* sorted, const uint32_t* slots, uint32_t B, uint32_t* nhr,
                      hipStream_t st) {
@@ -1067,6 +1101,10 @@ void mk_dbl_apply(const uint32_t* act, const uint64_t* key, const uint32_t* val,
 void mk_dbl_groups(const uint32_t* act, const uint64_t* key, const uint32_t* val, const uint32_t* labMax,
                    uint32_t U, uint32_t* grp, uint32_t* keep, hipStream_t st) {
   if (U) hipLaunchKernelGGL(k_dbl_groups, g1(U), dim3(256), 0, st, act, key, val, labMax, U, grp, keep);
+}
+void mk_map_order(const uint32_t* posBegin, const uint32_t* len, const uint8_t* sm, uint32_t n, uint32_t* order,
+                  hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_map_order, g1(n), dim3(256), 0, st, posBegin, len, sm, n, order);
 }
 void mk_dbl_gstart(const uint64_t* key, uint32_t U, uint32_t* flag, hipStream_t st) {
   if (U) hipLaunchKernelGGL(k_dbl_gstart, g1(U), dim3(256), 0, st, key, U, flag);

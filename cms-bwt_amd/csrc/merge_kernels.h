@@ -48,9 +48,10 @@ void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_
                    uint32_t* grp, uint32_t* actv, hipStream_t st);
 void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, const uint16_t* nexthead, uint32_t H, uint32_t* nhr,
                  hipStream_t st);
-void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigItem, hipStream_t st);
-void mk_nhr_big_keys(const uint32_t* itemOfSlot, const uint32_t* bigItem, const uint32_t* nhr, uint32_t H,
-                     unsigned long long* key, uint32_t* flag, hipStream_t st);
+void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigList, hipStream_t st);
+void mk_nhr_big_fill(const uint32_t* items, const uint32_t* off, uint32_t nb, const ItemsSoA& it, const uint32_t* nhr,
+                     unsigned long long* key, uint32_t* slots, hipStream_t st);
+void mk_item_counts_of(const uint32_t* items, uint32_t nb, const uint32_t* count, uint32_t* out, hipStream_t st);
 void mk_nhr_big_back(const unsigned long long* sorted, const uint32_t* slots, uint32_t B, uint32_t* nhr,
                      hipStream_t st);
 void mk_item_permute(const ItemsSoA& in, const uint32_t* order, const ItemsSoA& out, uint32_t K, hipStream_t st);
@@ -76,6 +77,9 @@ void mk_dbl_groups(const uint32_t* act, const uint64_t* key, const uint32_t* val
                    uint32_t U, uint32_t* grp, uint32_t* keep, hipStream_t st);
 void mk_head_ranks(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint32_t* headRank, uint8_t* bwtHeads,
                    hipStream_t st);
+// map order of each position's items (one thread per position)
+void mk_map_order(const uint32_t* posBegin, const uint32_t* len, const uint8_t* sm, uint32_t n, uint32_t* order,
+                  hipStream_t st);
 // per-group doubling round (small groups sorted by one thread each)
 void mk_dbl_gstart(const uint64_t* key, uint32_t U, uint32_t* flag, hipStream_t st);
 void mk_dbl_small(const uint32_t* gs, uint32_t G, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val,

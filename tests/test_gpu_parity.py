@@ -88,6 +88,13 @@ def test_counter_window_geometry(engine, oracle, tmp_path, case, geom):
     _compare(engine, oracle, tmp_path, case, env=geom)
 
 
+@pytest.mark.parametrize("case", cases.small_cases()[:4], ids=lambda c: c[0])
+def test_grouping_three_sorts(engine, oracle, tmp_path, case):
+    """Grouping (FN:1387-1416) by three LSD sorts (the path for fields wider
+    than one 64-bit key) gives the oracle's items, ranks and runs."""
+    _compare(engine, oracle, tmp_path, case, env={"CMSBWT_GROUP3": "1"})
+
+
 @pytest.mark.parametrize("small", ["2", "1000000"], ids=["radix_groups", "thread_groups"])
 @pytest.mark.parametrize("case", cases.small_cases()[:4], ids=lambda c: c[0])
 def test_doubling_group_paths(engine, oracle, tmp_path, case, small):
