@@ -64,18 +64,19 @@ def cpu_baseline(ref_len, copies, p, seed):
 
 def pmc_traffic(args):
     """Beyond-L2 bytes per launch of the walk kernel from the committed PMC
-    summary (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE, separate passes, KiB
-    units; tools/gpu_prof.sh), for the default workload only.  FETCH_SIZE is
-    TCC_EA0_RDREQ x 64 B and includes Infinity-Cache hits; the walk's reads
-    are scattered 1..16-byte loads, so no streaming-read correction applies."""
+    summary (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes, KiB
+    units; tools/gpu_prof.sh), for the default workload only.  Per
+    MI355X_MICROARCH.md (HBM): FETCH_SIZE = TCC_EA0_RDREQ x 64 B counts half
+    the bytes of 128-B requests on gfx950, so it is doubled; both counters
+    include Infinity-Cache hits."""
     default = (args.ref_len, args.copies, args.p, args.seed) == (10_000_000, 1000, 0.001, 4)
     path = os.path.join(ROOT, "profiles", "r01_pmc.json")
     if not default or not os.path.exists(path):
         return None, None
     try:
         d = json.load(open(path))["k_ms_walk2"]
-        b = (d["FETCH_SIZE"]["per_launch"] + d["WRITE_SIZE"]["per_launch"]) * 1024.0
-        return int(b), "profiles/r01_pmc.json (FETCH_SIZE+WRITE_SIZE per launch)"
+        b = (2 * d["FETCH_SIZE"]["per_launch"] + d["WRITE_SIZE"]["per_launch"]) * 1024.0
+        return int(b), "profiles/r01_pmc.json (2 x FETCH_SIZE + WRITE_SIZE per launch)"
     except (KeyError, ValueError):
         return None, None
 
