@@ -44,7 +44,7 @@ def synth_reference(L: int, seed: int) -> bytes:
     return np.frombuffer(b"ACGT", dtype=np.uint8)[(h >> np.uint64(62)).astype(np.int64)].tobytes()
 
 
-def cpu_baseline(ref_len, copies, p, seed):
+def cpu_baseline(ref_len, copies, p, seed, rle=True):
     """Oracle (single-threaded CPU restatement) on a bounded sample of the same
     workload, collection stage only (parse .. .rl_bwt closed)."""
     import oracle_lib
@@ -52,7 +52,7 @@ def cpu_baseline(ref_len, copies, p, seed):
     with tempfile.TemporaryDirectory() as td:
         pre = os.path.join(td, "s")
         subprocess.run([gen, str(ref_len), str(copies), str(p), str(seed), pre], check=True)
-        rc, st, (t_idx, t_coll) = oracle_lib.run(pre + ".ref.fa", pre + ".coll.fa", pre + "_o", rle=True)
+        rc, st, (t_idx, t_coll) = oracle_lib.run(pre + ".ref.fa", pre + ".coll.fa", pre + "_o", rle=rle)
         if rc:
             raise RuntimeError(f"oracle rc={rc}")
     chars = ref_len * copies
@@ -92,6 +92,8 @@ def main():
     ap.add_argument("--seed", type=int, default=4)
     ap.add_argument("--cpu-copies", type=int, default=10)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--plain", action="store_true",
+                    help="plain .bwt instead of .rl_bwt (BASELINE config 5 runs without -r)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -117,13 +119,15 @@ def main():
     gather = mode == "gather"
     xfer = cdist.Transport(device) if (world > 1 or mode == "sharded1") else None
 
+    rle = not args.plain
+
     def step():
         if world == 1 and mode != "sharded1":
-            eng.step(rle=True)
+            eng.step(rle=rle)
         elif gather:  # all heads to rank 0, single-GPU merge there
-            cdist.gather_step(eng, device, rle=True)
+            cdist.gather_step(eng, device, rle=rle)
         else:         # merge sharded by reference position (dist_merge.hip)
-            cdist.sharded_step(eng, device, rle=True, xfer=xfer)
+            cdist.sharded_step(eng, device, rle=rle, xfer=xfer)
 
     def barrier():
         torch.cuda.synchronize(local)
@@ -161,12 +165,14 @@ def main():
     achieved = b_ms / t_ms / 1e9 if t_ms > 0 else 0.0
     traffic, traffic_src = pmc_traffic(args) if world == 1 else (None, None)
     out = {
-        "metric": "collection MB/s to .rl_bwt (10 MB ref + 1000 copies @0.1% SNP)",
+        "metric": ("collection MB/s to .bwt" if args.plain else
+                   "collection MB/s to .rl_bwt (10 MB ref + 1000 copies @0.1% SNP)"),
         "value": round(value, 3), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (counter-based generator in HBM, SURVEY.md §8d)",
-        "config": {"workload": f"{args.ref_len // 10**6} MB ref + {args.copies} copies @{args.p * 100:g}% SNP, -r",
+        "config": {"workload": f"{args.ref_len // 10**6} MB ref + {args.copies} copies @{args.p * 100:g}% SNP"
+                               + ("" if args.plain else ", -r"),
                    "ref_len": args.ref_len, "copies": args.copies, "snp": args.p, "seed": args.seed,
                    "collection_bytes": chars_total, "heads": st.heads, "keys": st.keys, "runs": st.runs,
                    "parallelism": ((f"documents sharded over {world} GPUs, heads gathered to rank 0 over RCCL, merge on rank 0"
@@ -185,7 +191,7 @@ def main():
     }
     if rank == 0 and not args.no_cpu:
         try:
-            out["cpu_baseline"] = cpu_baseline(args.ref_len, args.cpu_copies, args.p, args.seed)
+            out["cpu_baseline"] = cpu_baseline(args.ref_len, args.cpu_copies, args.p, args.seed, rle=rle)
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"error": str(e)}
     if rank == 0:

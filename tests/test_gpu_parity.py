@@ -205,3 +205,44 @@ def test_config3_full_size_golden(engine):
     assert (st.counter_bad, st.counter_good, st.counter_nothing) == \
         (g["t4"]["counterBad"], g["t4"]["counterGood"], g["t4"]["counterDoNothing"])
     assert hashlib.sha256(engine.runs_bytes()).hexdigest() == g["t4"]["rl_bwt_sha256"]
+
+
+def _sha_file(path):
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 24), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def test_config5_proxy_golden(engine, tmp_path):
+    """BASELINE config 5's shape (100 MB reference, 1 % SNP, plain .bwt) on the
+    proxy SURVEY.md §8(a) prescribes, since the reference path cannot run the
+    full 200 copies: 100 MB ref + 4 copies @1 % (numpy generator seed 5).
+    Head/key/rank counts, counter statistics and the sha256 of both the plain
+    .bwt and the .rl_bwt equal the oracle's (tests/golden/make_c5proxy.py)."""
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import gen_np
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["c5p"]
+    L, C, p, seed, _ = g["args"]
+    ref, text, off = gen_np.gen_arrays(L, C, p, seed)
+    engine.load_reference_bytes(ref)
+    engine.load_collection_array(text, off)
+    del text
+    engine.step(rle=False)
+    st = engine.stats()
+    assert st.heads == g["headNumber"]
+    assert st.rank == g["Rank"]
+    assert (st.counter_bad, st.counter_good, st.counter_nothing) == \
+        (g["counterBad"], g["counterGood"], g["counterDoNothing"])
+    out = str(tmp_path / "c5p")
+    engine.write_output(out, rle=False)
+    assert os.path.getsize(out + ".bwt") == g["bwt_bytes"]
+    assert _sha_file(out + ".bwt") == g["bwt_sha256"]
+    engine.step(rle=True)
+    assert engine.stats().runs == g["rl_runs"]
+    import hashlib
+    assert hashlib.sha256(engine.runs_bytes()).hexdigest() == g["rl_bwt_sha256"]
