@@ -17,8 +17,14 @@
 #include <hip/hip_runtime.h>
 #include <rocprim/rocprim.hpp>
 
+#include <fcntl.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
 #include <algorithm>
+#include <atomic>
 #include <chrono>
+#include <thread>
 #include <fstream>
 #include <map>
 #include <string>
@@ -218,6 +224,7 @@ struct Engine {
   }
   ~Engine() {
     g_alloc = &alloc;
+    for (void* b : pinned) (void)hipHostFree(b);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     if (st) (void)hipStreamDestroy(st);
@@ -303,13 +310,85 @@ struct Engine {
   }
 
   // =====================================================================
+  // Reference index on the device (ref_index.hip): fills hix.sa/isa/lcp/plcp/
+  // bwt exactly as build_index() (host SA-IS + Φ) would.
+  void gpu_index(HostIndex& ix) {
+    auto now = [] { return std::chrono::steady_clock::now(); };
+    auto t0 = now();
+    const uint32_t n = ix.n;
+    DBuf<uint8_t> xd;
+    xd.alloc((uint64_t)n + 64);
+    HIPCHK(hipMemsetAsync(xd.p, 0, (uint64_t)n + 64, st));
+    HIPCHK(hipMemcpyAsync(xd.p, ix.x.data(), n, hipMemcpyHostToDevice, st));
+    DBuf<unsigned long long> k0, k1;
+    DBuf<uint32_t> v0, v1, rank, headIn, head, tie, act, act2;
+    DBuf<int32_t> sa;
+    k0.alloc(n); k1.alloc(n); v0.alloc(n); v1.alloc(n);
+    rank.alloc(n); headIn.alloc(n); head.alloc(n); tie.alloc(n); act.alloc(n); act2.alloc(n);
+    sa.alloc(n);
+    launch_ix_init(xd.p, n, k0.p, v0.p, st);
+    sort_pairs(k0.p, k1.p, v0.p, v1.p, n, 9 * kIdxH0);
+    launch_ix_heads(k1.p, nullptr, n, headIn.p, tie.p, st);
+    inscan(headIn.p, head.p, n, rocprim::maximum<uint32_t>());
+    launch_ix_place(v1.p, nullptr, head.p, n, sa.p, rank.p, st);
+    mk_iota(act2.p, n, st);
+    uint32_t U = select_flagged(act2.p, tie.p, act.p, n);
+    const int bits = 32 + bits_for(n);
+    uint64_t h = kIdxH0;
+    int rounds = 0;
+    while (U) {
+      if (++rounds > 40 || h >= 2ull * n) throw InputError{CMSBWT_EDEVICE, "internal: prefix doubling did not converge"};
+      launch_ix_keys(act.p, U, sa.p, rank.p, n, (uint32_t)std::min<uint64_t>(h, n), k0.p, v0.p, st);
+      sort_pairs(k0.p, k1.p, v0.p, v1.p, U, bits);
+      launch_ix_heads(k1.p, act.p, U, headIn.p, tie.p, st);
+      inscan(headIn.p, head.p, U, rocprim::maximum<uint32_t>());
+      launch_ix_place(v1.p, act.p, head.p, U, sa.p, rank.p, st);
+      U = select_flagged(act.p, tie.p, act2.p, U);
+      act.swap_in(act2);
+      h <<= 1;
+    }
+    sync();
+    auto t1 = now();
+    k0.release(); k1.release(); v0.release(); v1.release(); headIn.release(); head.release(); tie.release();
+    act.release(); act2.release();
+    DBuf<uint32_t> isa;
+    DBuf<int32_t> phi, plcpRaw, lcp, plcp;
+    DBuf<uint8_t> bwt;
+    isa.alloc((uint64_t)n + 1); phi.alloc(n); plcpRaw.alloc(n); lcp.alloc((uint64_t)n + 1); plcp.alloc(n);
+    bwt.alloc(n);
+    launch_ix_lcp(xd.p, sa.p, n, isa.p, phi.p, plcpRaw.p, lcp.p, bwt.p, plcp.p, st);
+    HIPCHK(hipGetLastError());
+    ix.sa.resize(n);
+    ix.isa.resize(n);
+    ix.lcp.resize((size_t)n + 1);
+    ix.plcp.resize(n);
+    ix.bwt.resize(n);
+    HIPCHK(hipMemcpyAsync(ix.sa.data(), sa.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(ix.isa.data(), isa.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(ix.lcp.data(), lcp.p, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(ix.plcp.data(), plcp.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(ix.bwt.data(), bwt.p, n, hipMemcpyDeviceToHost, st));
+    sync();
+    ix.t_sa = std::chrono::duration<double>(t1 - t0).count();
+    ix.t_lcp = std::chrono::duration<double>(now() - t1).count();
+  }
+
+  // =====================================================================
   // reference (FN:151-310)
   void load_reference_bytes(const std::string& trimmed) {
     auto t0 = std::chrono::steady_clock::now();
     for (unsigned char c : trimmed)
       if (c == 2) throw InputError{CMSBWT_EINPUT, "reference contains byte 0x02 (the document separator)"};
     if (trimmed.size() + 130 >= (1ull << 31)) throw InputError{CMSBWT_ELIMIT, "reference longer than 2^31 (int32 SA)"};
-    build_index(trimmed, hix);
+    {
+      const char* hi = getenv("CMSBWT_HOST_INDEX");
+      if (hi && *hi && *hi != '0') {
+        build_index(trimmed, hix);
+      } else {
+        augment_reference(trimmed, hix);
+        gpu_index(hix);
+      }
+    }
     const uint32_t n = hix.n;
     // Skip-search precondition: PLCP[q] + q non-decreasing.
     for (uint32_t q = 0; q + 1 < n; q++)
@@ -568,6 +647,144 @@ struct Engine {
     collLoaded = true;
     stats.t_upload_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
+  // ---- collection file -> HBM, lines resolved on the device (coll_read.hip)
+  std::vector<void*> pinned;  // 2 staging buffers per reader thread, kept across calls
+  uint64_t pinnedBytes = 0;
+  uint64_t collMeta[3] = {0, 0, 0};  // sn, chars, ndocs (parity copies)
+
+  // pread of the file into pinned buffers by `nt` threads, each DMAing its
+  // chunks to dst on its own stream (double-buffered: reading chunk c+2T
+  // overlaps the copy of chunk c).
+  void stream_file(int fd, uint64_t fsz, uint8_t* dst) {
+    const uint32_t nt = std::max(1u, std::min(64u, env_u32("CMSBWT_READ_THREADS", 8)));
+    const uint64_t CH = (uint64_t)std::max(1u, env_u32("CMSBWT_READ_CHUNK_MB", 32)) << 20;
+    if (pinned.size() < 2 * nt || pinnedBytes < CH) {
+      for (void* b : pinned) (void)hipHostFree(b);
+      pinned.assign(2 * nt, nullptr);
+      for (auto& b : pinned) HIPCHK(hipHostMalloc(&b, CH, hipHostMallocDefault));
+      pinnedBytes = CH;
+    }
+    const uint64_t nch = (fsz + CH - 1) / CH;
+    std::atomic<int> err{0};
+    std::vector<std::thread> th;
+    for (uint32_t k = 0; k < nt && k < nch; k++)
+      th.emplace_back([&, k] {
+        hipStream_t s = nullptr;
+        hipEvent_t ev[2] = {nullptr, nullptr};
+        bool used[2] = {false, false};
+        auto ok = [&](hipError_t e) { if (e != hipSuccess) err = 2; return e == hipSuccess; };
+        if (ok(hipSetDevice(device)) && ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking)) &&
+            ok(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming)) &&
+            ok(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming))) {
+          uint32_t it = 0;
+          for (uint64_t c = k; c < nch && !err; c += nt, it++) {
+            const int j = it & 1;
+            uint8_t* buf = (uint8_t*)pinned[2 * k + j];
+            if (used[j] && !ok(hipEventSynchronize(ev[j]))) break;
+            const uint64_t off = c * CH, want = std::min(CH, fsz - off);
+            uint64_t got = 0;
+            while (got < want) {
+              ssize_t r = pread(fd, buf + got, want - got, (off_t)(off + got));
+              if (r <= 0) { err = 1; break; }
+              got += (uint64_t)r;
+            }
+            if (err) break;
+            if (!ok(hipMemcpyAsync(dst + off, buf, want, hipMemcpyHostToDevice, s))) break;
+            if (!ok(hipEventRecord(ev[j], s))) break;
+            used[j] = true;
+          }
+        }
+        if (s) { (void)hipStreamSynchronize(s); (void)hipStreamDestroy(s); }
+        for (auto e : ev) if (e) (void)hipEventDestroy(e);
+      });
+    for (auto& t : th) t.join();
+    if (err == 1) throw InputError{CMSBWT_EIO, "read error on the collection file"};
+    if (err) throw HipError{"HIP error while streaming the collection file"};
+  }
+
+  // Same Collection as read_collection(path, UINT64_MAX) + upload_collection
+  // (tests/test_gpu_parity.py::test_gpu_reader_*), produced in HBM.
+  void load_collection_file_gpu(const std::string& path) {
+    if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
+    auto t0 = std::chrono::steady_clock::now();
+    reset_collection();
+    int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) throw InputError{CMSBWT_EIO, "Error opening file of sequence (" + path + ")"};
+    struct stat sbuf;
+    if (fstat(fd, &sbuf) != 0) { close(fd); throw InputError{CMSBWT_EIO, "cannot stat " + path}; }
+    const uint64_t fsz = (uint64_t)sbuf.st_size;
+    const uint64_t ntiles = (fsz + kRdTile - 1) / kRdTile;
+    DBuf<uint8_t> raw;
+    raw.alloc(ntiles * kRdTile + kRdTile);  // tiles read whole; '\n'/'>' lookups one past len
+    try {
+      stream_file(fd, fsz, raw.p);
+    } catch (...) {
+      close(fd);
+      throw;
+    }
+    close(fd);
+    DBuf<uint64_t> lastNl, carry;
+    lastNl.alloc(ntiles + 1);
+    carry.alloc(ntiles + 1);
+    HIPCHK(hipMemsetAsync(lastNl.p + ntiles, 0, 8, st));
+    launch_rd_lastnl(raw.p, fsz, ntiles, lastNl.p, st);
+    exscan(lastNl.p, carry.p, (uint64_t)0, ntiles + 1, rocprim::maximum<uint64_t>());
+    const uint64_t len = read1(carry.p + ntiles);  // 1 + last '\n': the lines
+    const uint64_t nt = (len + kRdTile - 1) / kRdTile;
+    DBuf<uint32_t> cnt, seps;
+    DBuf<uint64_t> ob, sb;
+    cnt.alloc(nt + 1);
+    seps.alloc(nt + 1);
+    ob.alloc(nt + 1);
+    sb.alloc(nt + 1);
+    HIPCHK(hipMemsetAsync(cnt.p + nt, 0, 4, st));
+    HIPCHK(hipMemsetAsync(seps.p + nt, 0, 4, st));
+    launch_rd_count(raw.p, len, nt, carry.p, cnt.p, seps.p, st);
+    exscan(cnt.p, ob.p, (uint64_t)0, nt + 1);
+    exscan(seps.p, sb.p, (uint64_t)0, nt + 1);
+    const uint64_t total = read1(ob.p + nt), nsep = read1(sb.p + nt);
+    dtext.alloc(total + 1 + kTextPad);
+    ddoc.alloc(nsep + 2);
+    HIPCHK(hipMemsetAsync(ddoc.p, 0, 8, st));
+    DBuf<uint8_t> pres;
+    DBuf<unsigned long long> bad;
+    pres.alloc(256);
+    bad.alloc(1);
+    uint8_t ph[256];
+    for (int b = 0; b < 256; b++) ph[b] = hix.present[b] ? 1 : 0;
+    HIPCHK(hipMemcpyAsync(pres.p, ph, 256, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemsetAsync(bad.p, 0xff, 8, st));
+    launch_rd_emit(raw.p, len, nt, carry.p, ob.p, sb.p, pres.p, dtext.p, ddoc.p, bad.p, st);
+    HIPCHK(hipGetLastError());
+    std::vector<uint64_t> off(nsep + 1);
+    HIPCHK(hipMemcpyAsync(off.data(), ddoc.p, (nsep + 1) * 8, hipMemcpyDeviceToHost, st));
+    const unsigned long long badv = read1(bad.p);
+    uint64_t size = total, sn = fsz;
+    if (total > off[nsep]) {  // tail document (FN:1269-1275)
+      const uint64_t e = total + 1;
+      HIPCHK(hipMemsetAsync(dtext.p + total, kSep, 1, st));
+      off.push_back(e);
+      HIPCHK(hipMemcpyAsync(ddoc.p + nsep + 1, &off.back(), 8, hipMemcpyHostToDevice, st));
+      size = e;
+      if (size < sn - 1) sn = size;
+    }
+    HIPCHK(hipMemsetAsync(dtext.p + size, kSep, kTextPad, st));
+    sync();
+    raw.release();
+    for (uint64_t d = 0; d + 1 < off.size(); d++)
+      if (off[d + 1] - off[d] - 1 >= (1ull << 32) - 1)
+        throw InputError{CMSBWT_ELIMIT, "document longer than 2^32 (uint32 positions)"};
+    if (badv != ~0ull)
+      throw InputError{CMSBWT_EINPUT, "collection byte " + std::to_string((int)(badv & 0xff)) +
+                                          " does not occur in the reference (reference behaviour undefined)"};
+    hdoc = std::move(off);
+    ndocs = hdoc.size() - 1;
+    chars = collChars = size - ndocs;
+    this->sn = sn;
+    collLoaded = true;
+    stats.t_upload_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+
   void load_synth(uint64_t seed, uint64_t copy_begin, uint64_t ncopies, double p, int leadingEmpty) {
     if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
     reset_collection();
@@ -1275,6 +1492,27 @@ struct Engine {
       }
       return bytes;
     };
+    if (name.rfind("ref_", 0) == 0 && !refLoaded) throw InputError{CMSBWT_EARG, "load a reference first"};
+    if (name == "ref_sa") return cp(dsa.p, (uint64_t)R.n * 4);
+    if (name == "ref_isa") return cp(disa.p, (uint64_t)R.n * 4);
+    if (name == "ref_lcp") return cp(dlcp.p, ((uint64_t)R.n + 1) * 4);
+    if (name == "ref_plcp") return cp(dplcp.p, (uint64_t)R.n * 4);
+    if (name == "ref_bwt") return cp(dbwt.p, R.n);
+    if (name == "coll_text") {
+      if (!collLoaded) throw InputError{CMSBWT_EARG, "load a collection first"};
+      return cp(dtext.p, hdoc.empty() ? 0 : hdoc.back());
+    }
+    if (name == "coll_off") {
+      if (!collLoaded) throw InputError{CMSBWT_EARG, "load a collection first"};
+      return cp(ddoc.p, hdoc.size() * 8);
+    }
+    if (name == "coll_meta") {
+      collMeta[0] = sn;
+      collMeta[1] = collChars;
+      collMeta[2] = ndocs;
+      if (out) memcpy(out, collMeta, 24);
+      return 24;
+    }
     if (name.rfind("h_", 0) == 0 && !walked) throw InputError{CMSBWT_EARG, "run ms_walk first"};
     if (name == "h_start") return cp(hStart.p, (uint64_t)H * 4);
     if (name == "h_pos") return cp(hPos.p, (uint64_t)H * 4);

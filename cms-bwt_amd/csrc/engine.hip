@@ -70,6 +70,14 @@ int cmsbwt_load_reference(cmsbwt_ctx* ctx, const uint8_t* ref, uint64_t len) {
 int cmsbwt_load_collection_file(cmsbwt_ctx* ctx, const char* path, uint64_t prefix) {
   if (!ctx || !path) return CMSBWT_EARG;
   return guard(ctx, [&] {
+    // Without -p the lines are resolved on the device over the raw bytes
+    // (coll_read.hip); the -p cut (FN:1142-1146) keeps the host reader, as
+    // does CMSBWT_HOST_READER=1.
+    const char* hr = getenv("CMSBWT_HOST_READER");
+    if (prefix == UINT64_MAX && !(hr && *hr && *hr != '0')) {
+      ctx->e->load_collection_file_gpu(path);
+      return;
+    }
     cmsbwt::Collection c;
     std::string err;
     if (!cmsbwt::read_collection(path, prefix, c, err)) throw cmsbwt::InputError{CMSBWT_EIO, err};

@@ -125,8 +125,7 @@ bool read_reference(const std::string& path, std::string& x, std::string& err) {
   return true;
 }
 
-void build_index(const std::string& trimmed, HostIndex& ix) {
-  auto now = [] { return std::chrono::steady_clock::now(); };
+void augment_reference(const std::string& trimmed, HostIndex& ix) {
   std::string& x = ix.x;
   x = trimmed;
   ix.ref_len = trimmed.size();
@@ -136,8 +135,16 @@ void build_index(const std::string& trimmed, HostIndex& ix) {
   for (int c = 3; c < 128; c++) if (!seen[c]) x.push_back((char)c);
   x.push_back((char)1);
   x.push_back((char)0);
-  const uint32_t n = (uint32_t)x.size();
-  ix.n = n;
+  ix.n = (uint32_t)x.size();
+  for (int c = 0; c < 256; c++) ix.present[c] = false;
+  for (uint32_t i = 0; i + 2 < ix.n; i++) ix.present[(uint8_t)x[i]] = true;
+}
+
+void build_index(const std::string& trimmed, HostIndex& ix) {
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  augment_reference(trimmed, ix);
+  const std::string& x = ix.x;
+  const uint32_t n = ix.n;
   auto t0 = now();
   {
     std::vector<int32_t> s(n);
@@ -172,8 +179,6 @@ void build_index(const std::string& trimmed, HostIndex& ix) {
     ix.plcp[i] = std::max(ix.lcp[ix.isa[i]], ix.lcp[(size_t)ix.isa[i] + 1]);
   ix.bwt.resize(n);
   for (uint32_t r = 0; r < n; r++) ix.bwt[r] = ix.sa[r] > 0 ? (uint8_t)x[ix.sa[r] - 1] : 0;
-  for (int c = 0; c < 256; c++) ix.present[c] = false;
-  for (uint32_t i = 0; i + 2 < n; i++) ix.present[(uint8_t)x[i]] = true;
   auto t2 = now();
   ix.t_sa = std::chrono::duration<double>(t1 - t0).count();
   ix.t_lcp = std::chrono::duration<double>(t2 - t1).count();

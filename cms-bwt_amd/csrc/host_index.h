@@ -25,6 +25,8 @@ void suffix_array_sais(const int32_t* s, int32_t* sa, int64_t n, int64_t k);
 
 // FN:155-213: read FASTA (first byte '>') or raw reference, trim.
 bool read_reference(const std::string& path, std::string& x, std::string& err);
+// FN:231-237: x = trimmed + absent bytes 3..127 + \1 \0; n, ref_len, present.
+void augment_reference(const std::string& trimmed, HostIndex& ix);
 // FN:231-297 on an already-read+trimmed sequence.
 void build_index(const std::string& trimmed, HostIndex& ix);
 

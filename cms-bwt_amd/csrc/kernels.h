@@ -57,6 +57,29 @@ void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint3
                      uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, int32_t* diff, uint8_t* hasHead,
                      uint32_t* errFlags, const uint32_t* hdoc, hipStream_t st);
 
+// coll_read.hip: the collection reader on the device (getline semantics of
+// FN:1138-1275 without -p) over raw file bytes in HBM, tiles of kRdTile bytes.
+constexpr uint32_t kRdTile = 16384;
+void launch_rd_lastnl(const uint8_t* raw, uint64_t len, uint64_t ntiles, uint64_t* lastNl1, hipStream_t st);
+void launch_rd_count(const uint8_t* raw, uint64_t len, uint64_t ntiles, const uint64_t* carry, uint32_t* cnt,
+                     uint32_t* seps, hipStream_t st);
+void launch_rd_emit(const uint8_t* raw, uint64_t len, uint64_t ntiles, const uint64_t* carry,
+                    const uint64_t* outBase, const uint64_t* sepBase, const uint8_t* present, uint8_t* out,
+                    uint64_t* docOff, unsigned long long* badByte, hipStream_t st);
+
+// ref_index.hip: reference index on the device (prefix-doubling SA, Φ-PLCP)
+constexpr uint32_t kIdxH0 = 7;      // initial key: 7 symbols of 9 bits
+constexpr uint32_t kIdxChunk = 64;  // positions per thread in the Φ-PLCP pass
+void launch_ix_init(const uint8_t* x, uint32_t n, unsigned long long* key, uint32_t* idx, hipStream_t st);
+void launch_ix_heads(const unsigned long long* key, const uint32_t* slot, uint32_t m, uint32_t* headIn, uint32_t* tie,
+                     hipStream_t st);
+void launch_ix_place(const uint32_t* val, const uint32_t* slot, const uint32_t* head, uint32_t m, int32_t* sa,
+                     uint32_t* rank, hipStream_t st);
+void launch_ix_keys(const uint32_t* act, uint32_t U, const int32_t* sa, const uint32_t* rank, uint32_t n, uint32_t h,
+                    unsigned long long* key, uint32_t* val, hipStream_t st);
+void launch_ix_lcp(const uint8_t* x, const int32_t* sa, uint32_t n, uint32_t* isa, int32_t* phi, int32_t* plcpRaw,
+                   int32_t* lcp, uint8_t* bwt, int32_t* plcp, hipStream_t st);
+
 // synth.hip
 void launch_synth_collection(uint8_t* text, uint64_t L, uint64_t seed, uint64_t copy_begin, uint64_t ncopies,
                              uint64_t pthr, uint64_t base, hipStream_t st);
