@@ -36,6 +36,7 @@ UINT64_MAX = (1 << 64) - 1
 
 ARRAYS = {  # name -> numpy dtype, as dumped by the oracle
     "ref_sa": "i4", "ref_isa": "u4", "ref_lcp": "i4", "ref_plcp": "i4", "ref_bwt": "u1",  # staged index
+    "ref_ld": "u4", "ref_pr": "u4", "ref_ir": "u4", "ref_pfx": "u4", "ref_lvl": "i4",  # walk tables
     "coll_text": "u1", "coll_off": "u8", "coll_meta": "u8",  # loaded collection (text+seps, offsets, sn/chars/ndocs)
     "h_start": "u4", "h_pos": "u4", "h_len": "u4", "h_smaller": "u1", "h_lchar": "u1",
     "h_isa": "u4", "h_tonext": "u4", "h_nexthead": "u2", "bucket": "i8",

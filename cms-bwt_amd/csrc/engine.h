@@ -310,67 +310,120 @@ struct Engine {
   }
 
   // =====================================================================
-  // Reference index on the device (ref_index.hip): fills hix.sa/isa/lcp/plcp/
-  // bwt exactly as build_index() (host SA-IS + Φ) would.
-  void gpu_index(HostIndex& ix) {
+  // Reference index and walk tables built on the device (ref_index.hip):
+  // the same arrays, layouts and tables as build_index() + stage_host(),
+  // without a host round trip (tests/test_gpu_index.py compares them).
+  void stage_device() {
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto t0 = now();
-    const uint32_t n = ix.n;
-    DBuf<uint8_t> xd;
-    xd.alloc((uint64_t)n + 64);
-    HIPCHK(hipMemsetAsync(xd.p, 0, (uint64_t)n + 64, st));
-    HIPCHK(hipMemcpyAsync(xd.p, ix.x.data(), n, hipMemcpyHostToDevice, st));
-    DBuf<unsigned long long> k0, k1;
-    DBuf<uint32_t> v0, v1, rank, headIn, head, tie, act, act2;
-    DBuf<int32_t> sa;
-    k0.alloc(n); k1.alloc(n); v0.alloc(n); v1.alloc(n);
-    rank.alloc(n); headIn.alloc(n); head.alloc(n); tie.alloc(n); act.alloc(n); act2.alloc(n);
-    sa.alloc(n);
-    launch_ix_init(xd.p, n, k0.p, v0.p, st);
-    sort_pairs(k0.p, k1.p, v0.p, v1.p, n, 9 * kIdxH0);
-    launch_ix_heads(k1.p, nullptr, n, headIn.p, tie.p, st);
-    inscan(headIn.p, head.p, n, rocprim::maximum<uint32_t>());
-    launch_ix_place(v1.p, nullptr, head.p, n, sa.p, rank.p, st);
-    mk_iota(act2.p, n, st);
-    uint32_t U = select_flagged(act2.p, tie.p, act.p, n);
-    const int bits = 32 + bits_for(n);
-    uint64_t h = kIdxH0;
-    int rounds = 0;
-    while (U) {
-      if (++rounds > 40 || h >= 2ull * n) throw InputError{CMSBWT_EDEVICE, "internal: prefix doubling did not converge"};
-      launch_ix_keys(act.p, U, sa.p, rank.p, n, (uint32_t)std::min<uint64_t>(h, n), k0.p, v0.p, st);
-      sort_pairs(k0.p, k1.p, v0.p, v1.p, U, bits);
-      launch_ix_heads(k1.p, act.p, U, headIn.p, tie.p, st);
-      inscan(headIn.p, head.p, U, rocprim::maximum<uint32_t>());
-      launch_ix_place(v1.p, act.p, head.p, U, sa.p, rank.p, st);
-      U = select_flagged(act.p, tie.p, act2.p, U);
-      act.swap_in(act2);
-      h <<= 1;
+    const uint32_t n = hix.n;
+    dx.alloc((uint64_t)n + kTextPad);
+    HIPCHK(hipMemsetAsync(dx.p, 0, n + kTextPad, st));
+    HIPCHK(hipMemcpyAsync(dx.p, hix.x.data(), n, hipMemcpyHostToDevice, st));
+    dsa.alloc((uint64_t)n + 16);
+    disa.alloc((uint64_t)n + 16);
+    dplcp.alloc((uint64_t)n + 17);
+    dbwt.alloc(n);
+    dsa.zero(st);
+    disa.zero(st);
+    dplcp.zero(st);
+    // LCP + block-minima levels in one buffer (layout of stage_host)
+    memset(&R, 0, sizeof(R));
+    std::vector<uint32_t> lvlLen;
+    {
+      uint64_t prev = n;
+      do {
+        prev = (prev + 63) / 64;
+        lvlLen.push_back((uint32_t)prev);
+      } while (prev > 64 && (int)lvlLen.size() < kMaxLevels);
+    }
+    auto pad = [](uint64_t k) { return (k + 16 + 3) & ~3ull; };
+    uint64_t total = pad((uint64_t)n + 1);
+    for (auto v : lvlLen) total += pad(v);
+    dlcp.alloc(total);
+    dlcp.zero(st);
+    {  // SA by prefix doubling
+      DBuf<unsigned long long> k0, k1;
+      DBuf<uint32_t> v0, v1, rank, headIn, head, tie, act, act2;
+      k0.alloc(n); k1.alloc(n); v0.alloc(n); v1.alloc(n);
+      rank.alloc(n); headIn.alloc(n); head.alloc(n); tie.alloc(n); act.alloc(n); act2.alloc(n);
+      int32_t* sa = dsa.p;
+      launch_ix_init(dx.p, n, k0.p, v0.p, st);
+      sort_pairs(k0.p, k1.p, v0.p, v1.p, n, 9 * kIdxH0);
+      launch_ix_heads(k1.p, nullptr, n, headIn.p, tie.p, st);
+      inscan(headIn.p, head.p, n, rocprim::maximum<uint32_t>());
+      launch_ix_place(v1.p, nullptr, head.p, n, sa, rank.p, st);
+      mk_iota(act2.p, n, st);
+      uint32_t U = select_flagged(act2.p, tie.p, act.p, n);
+      const int bits = 32 + bits_for(n);
+      uint64_t h = kIdxH0;
+      int rounds = 0;
+      while (U) {
+        if (++rounds > 40 || h >= 2ull * n) throw InputError{CMSBWT_EDEVICE, "internal: prefix doubling did not converge"};
+        launch_ix_keys(act.p, U, sa, rank.p, n, (uint32_t)std::min<uint64_t>(h, n), k0.p, v0.p, st);
+        sort_pairs(k0.p, k1.p, v0.p, v1.p, U, bits);
+        launch_ix_heads(k1.p, act.p, U, headIn.p, tie.p, st);
+        inscan(headIn.p, head.p, U, rocprim::maximum<uint32_t>());
+        launch_ix_place(v1.p, act.p, head.p, U, sa, rank.p, st);
+        U = select_flagged(act.p, tie.p, act2.p, U);
+        act.swap_in(act2);
+        h <<= 1;
+      }
     }
     sync();
     auto t1 = now();
-    k0.release(); k1.release(); v0.release(); v1.release(); headIn.release(); head.release(); tie.release();
-    act.release(); act2.release();
-    DBuf<uint32_t> isa;
-    DBuf<int32_t> phi, plcpRaw, lcp, plcp;
-    DBuf<uint8_t> bwt;
-    isa.alloc((uint64_t)n + 1); phi.alloc(n); plcpRaw.alloc(n); lcp.alloc((uint64_t)n + 1); plcp.alloc(n);
-    bwt.alloc(n);
-    launch_ix_lcp(xd.p, sa.p, n, isa.p, phi.p, plcpRaw.p, lcp.p, bwt.p, plcp.p, st);
+    DBuf<uint32_t> err;
+    err.alloc(1);
+    err.zero(st);
+    {
+      DBuf<int32_t> phi, plcpRaw;
+      phi.alloc(n);
+      plcpRaw.alloc(n);
+      launch_ix_lcp(dx.p, dsa.p, n, disa.p, phi.p, plcpRaw.p, dlcp.p, dbwt.p, dplcp.p, st);
+    }
+    launch_ix_plcp_check(dplcp.p, n, err.p, st);
+    uint64_t off = pad((uint64_t)n + 1);
+    const int32_t* prev = dlcp.p;
+    uint32_t prevLen = n;
+    int L = 0;
+    for (auto v : lvlLen) {
+      launch_ix_level(prev, prevLen, dlcp.p + off, v, st);
+      R.lvl[L] = dlcp.p + off;
+      R.lvlOff[L] = (uint32_t)off;
+      R.lvlLen[L] = v;
+      prev = dlcp.p + off;
+      prevLen = v;
+      off += pad(v);
+      L++;
+    }
+    R.nlvl = L;
+    R.x = dx.p;
+    R.sa = dsa.p;
+    R.isa = disa.p;
+    R.lcp = dlcp.p;
+    R.plcp = dplcp.p;
+    R.bwt = dbwt.p;
+    R.n = n;
+    if (read1(err.p)) throw InputError{CMSBWT_EINPUT, "internal: PLCP monotonicity violated"};
+    build_prefix_tables(true);
+    R.ld = nullptr;
+    if (env_u32("CMSBWT_EXT8", 1)) {
+      dld.alloc((uint64_t)n + 16);
+      dld.zero(st);
+      launch_ix_child(dx.p, dsa.p, dlcp.p, n, dld.p, st);
+      R.ld = dld.p;
+    }
+    dpr.alloc((uint64_t)n + 16);
+    dir.alloc((uint64_t)n + 16);
+    dpr.zero(st);
+    dir.zero(st);
+    launch_ix_adjacency(dsa.p, disa.p, dlcp.p, n, (uint32_t*)dpr.p, (uint32_t*)dir.p, st);
+    R.pr = dpr.p;
+    R.ir = dir.p;
     HIPCHK(hipGetLastError());
-    ix.sa.resize(n);
-    ix.isa.resize(n);
-    ix.lcp.resize((size_t)n + 1);
-    ix.plcp.resize(n);
-    ix.bwt.resize(n);
-    HIPCHK(hipMemcpyAsync(ix.sa.data(), sa.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(ix.isa.data(), isa.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(ix.lcp.data(), lcp.p, ((size_t)n + 1) * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(ix.plcp.data(), plcp.p, (size_t)n * 4, hipMemcpyDeviceToHost, st));
-    HIPCHK(hipMemcpyAsync(ix.bwt.data(), bwt.p, n, hipMemcpyDeviceToHost, st));
     sync();
-    ix.t_sa = std::chrono::duration<double>(t1 - t0).count();
-    ix.t_lcp = std::chrono::duration<double>(now() - t1).count();
+    hix.t_sa = std::chrono::duration<double>(t1 - t0).count();
+    hix.t_lcp = std::chrono::duration<double>(now() - t1).count();
   }
 
   // =====================================================================
@@ -380,15 +433,22 @@ struct Engine {
     for (unsigned char c : trimmed)
       if (c == 2) throw InputError{CMSBWT_EINPUT, "reference contains byte 0x02 (the document separator)"};
     if (trimmed.size() + 130 >= (1ull << 31)) throw InputError{CMSBWT_ELIMIT, "reference longer than 2^31 (int32 SA)"};
-    {
-      const char* hi = getenv("CMSBWT_HOST_INDEX");
-      if (hi && *hi && *hi != '0') {
-        build_index(trimmed, hix);
-      } else {
-        augment_reference(trimmed, hix);
-        gpu_index(hix);
-      }
+    const char* hi = getenv("CMSBWT_HOST_INDEX");
+    if (hi && *hi && *hi != '0') {
+      build_index(trimmed, hix);
+      stage_host();
+    } else {
+      augment_reference(trimmed, hix);
+      stage_device();
     }
+    refLoaded = true;
+    stats.n = hix.n;
+    stats.t_index_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+  }
+
+  // host SA-IS index (build_index) staged into HBM with the walk tables
+  // built on the host (CMSBWT_HOST_INDEX=1; the device build's reference)
+  void stage_host() {
     const uint32_t n = hix.n;
     // Skip-search precondition: PLCP[q] + q non-decreasing.
     for (uint32_t q = 0; q + 1 < n; q++)
@@ -444,13 +504,10 @@ struct Engine {
     R.plcp = dplcp.p;
     R.bwt = dbwt.p;
     R.n = n;
-    build_prefix_tables();
+    build_prefix_tables(false);
     build_child_table();
     build_adjacency_records();
     sync();
-    refLoaded = true;
-    stats.n = n;
-    stats.t_index_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
 
   // Prefix-rank tables of the uniform-step walk (device_common.h).  With P's
@@ -468,7 +525,7 @@ struct Engine {
   // and its successor code, so the interval end is Start + Count, not the
   // next Start).  Only ASCII references: there the walk's signed (FN:55) and
   // unsigned orders agree.
-  void build_prefix_tables() {
+  void build_prefix_tables(bool device) {
     R.pfx = nullptr;
     R.kmap = nullptr;
     R.kmerK = R.kmerB = 0;
@@ -498,6 +555,41 @@ struct Engine {
     for (uint32_t l = 1; l <= K; l++) {
       R.pfxOff[l] = (uint32_t)total;
       total += 2 * ((1ull << (B * l)) + 1);
+    }
+    if (device) {
+      dpfx.alloc(total + 4);
+      dpfx.zero(st);
+      dkmap.alloc(256);
+      HIPCHK(hipMemcpyAsync(dkmap.p, map.data(), 256, hipMemcpyHostToDevice, st));
+      DBuf<uint32_t> dbelow, cur, cf, ct, cfEx, ctIn;
+      DBuf<uint8_t> term;
+      dbelow.alloc(256);
+      HIPCHK(hipMemcpyAsync(dbelow.p, below.data(), 256 * 4, hipMemcpyHostToDevice, st));
+      cur.alloc(n);
+      term.alloc(n);
+      cur.zero(st);
+      term.zero(st);
+      const uint64_t Emax1 = (1ull << (B * K)) + 1;
+      cf.alloc(Emax1);
+      ct.alloc(Emax1);
+      cfEx.alloc(Emax1);
+      ctIn.alloc(Emax1);
+      for (uint32_t l = 1; l <= K; l++) {
+        const uint64_t E1 = (1ull << (B * l)) + 1;
+        HIPCHK(hipMemsetAsync(cf.p, 0, E1 * 4, st));
+        HIPCHK(hipMemsetAsync(ct.p, 0, E1 * 4, st));
+        launch_ix_pfx_count(dx.p, n, l, B, dkmap.p, dbelow.p, cur.p, term.p, cf.p, ct.p, st);
+        exscan(cf.p, cfEx.p, 0u, E1);
+        inscan(ct.p, ctIn.p, E1, rocprim::plus<uint32_t>());
+        launch_ix_pfx_write(cfEx.p, ctIn.p, cf.p, E1, dpfx.p + R.pfxOff[l], st);
+      }
+      HIPCHK(hipGetLastError());
+      sync();  // map/below are pageable
+      R.pfx = dpfx.p;
+      R.kmap = dkmap.p;
+      R.kmerK = K;
+      R.kmerB = B;
+      return;
     }
     std::vector<uint32_t> tab(total + 4, 0);
     std::vector<uint32_t> cur(n, 0);
@@ -1498,6 +1590,19 @@ struct Engine {
     if (name == "ref_lcp") return cp(dlcp.p, ((uint64_t)R.n + 1) * 4);
     if (name == "ref_plcp") return cp(dplcp.p, (uint64_t)R.n * 4);
     if (name == "ref_bwt") return cp(dbwt.p, R.n);
+    if (name == "ref_ld") return R.ld ? cp(dld.p, (uint64_t)R.n * 4) : 0;
+    if (name == "ref_pr") return cp(dpr.p, (uint64_t)R.n * 16);
+    if (name == "ref_ir") return cp(dir.p, (uint64_t)R.n * 16);
+    if (name == "ref_pfx") return R.pfx ? cp(dpfx.p, dpfx.n * 4) : 0;
+    if (name == "ref_lvl") {  // the block-minima levels, concatenated
+      uint64_t b = 0;
+      for (int L = 0; L < R.nlvl; L++) {
+        if (out) HIPCHK(hipMemcpyAsync((uint8_t*)out + b, R.lvl[L], (uint64_t)R.lvlLen[L] * 4, hipMemcpyDefault, st));
+        b += (uint64_t)R.lvlLen[L] * 4;
+      }
+      if (out) sync();
+      return b;
+    }
     if (name == "coll_text") {
       if (!collLoaded) throw InputError{CMSBWT_EARG, "load a collection first"};
       return cp(dtext.p, hdoc.empty() ? 0 : hdoc.back());

@@ -79,6 +79,17 @@ void launch_ix_keys(const uint32_t* act, uint32_t U, const int32_t* sa, const ui
                     unsigned long long* key, uint32_t* val, hipStream_t st);
 void launch_ix_lcp(const uint8_t* x, const int32_t* sa, uint32_t n, uint32_t* isa, int32_t* phi, int32_t* plcpRaw,
                    int32_t* lcp, uint8_t* bwt, int32_t* plcp, hipStream_t st);
+void launch_ix_plcp_check(const int32_t* plcp, uint32_t n, uint32_t* err, hipStream_t st);
+void launch_ix_level(const int32_t* prev, uint32_t prevLen, int32_t* cur, uint32_t curLen, hipStream_t st);
+void launch_ix_child(const uint8_t* x, const int32_t* sa, const int32_t* lcp, uint32_t n, uint32_t* ld,
+                     hipStream_t st);
+void launch_ix_adjacency(const int32_t* sa, const uint32_t* isa, const int32_t* lcp, uint32_t n, uint32_t* pr,
+                         uint32_t* ir, hipStream_t st);
+void launch_ix_pfx_count(const uint8_t* x, uint32_t n, uint32_t l, uint32_t B, const uint8_t* map,
+                         const uint32_t* below, uint32_t* cur, uint8_t* term, uint32_t* cf, uint32_t* ct,
+                         hipStream_t st);
+void launch_ix_pfx_write(const uint32_t* cfEx, const uint32_t* ctIn, const uint32_t* cf, uint64_t E1, uint32_t* o,
+                         hipStream_t st);
 
 // synth.hip
 void launch_synth_collection(uint8_t* text, uint64_t L, uint64_t seed, uint64_t copy_begin, uint64_t ncopies,

@@ -141,3 +141,128 @@ void launch_ix_lcp(const uint8_t* x, const int32_t* sa, uint32_t n, uint32_t* is
 }
 
 }  // namespace cmsbwt
+
+// ---------------------------------------------------------------- walk tables
+// Device builds of the tables engine.h's host staging fills (same layouts):
+// LCP block minima, child table, adjacency records, prefix-rank tables and the
+// PLCP skip precondition.
+namespace cmsbwt {
+
+__global__ void k_ix_plcp_check(const int32_t* __restrict__ plcp, uint32_t n, uint32_t* __restrict__ err) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q + 1 >= n) return;
+  if ((int64_t)plcp[q + 1] + 1 < (int64_t)plcp[q]) atomicOr(err, 1u);
+}
+
+__global__ void k_ix_level(const int32_t* __restrict__ prev, uint32_t prevLen, int32_t* __restrict__ cur,
+                           uint32_t curLen) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= curLen) return;
+  int32_t m = INT32_MAX;
+  const uint64_t e = (uint64_t)i * 64 + 64 < prevLen ? (uint64_t)i * 64 + 64 : prevLen;
+  for (uint64_t k = (uint64_t)i * 64; k < e; k++) m = prev[k] < m ? prev[k] : m;
+  cur[i] = m;
+}
+
+__device__ __forceinline__ uint32_t ix_chr(const uint8_t* x, const int32_t* sa, uint32_t n, uint32_t k, int32_t l) {
+  const uint64_t at = (uint64_t)(uint32_t)sa[k] + (uint32_t)(l > 0 ? l : 0);
+  return at < n ? x[at] : 0u;
+}
+
+__global__ void k_ix_child(const uint8_t* __restrict__ x, const int32_t* __restrict__ sa,
+                           const int32_t* __restrict__ lcp, uint32_t n, uint32_t* __restrict__ ld) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const int32_t l = lcp[k] > 0 ? lcp[k] : 0;
+  const uint32_t d = k ? ix_chr(x, sa, n, k, l) : 0u;
+  const uint32_t u = lcp[k + 1] >= 0 ? ix_chr(x, sa, n, k, lcp[k + 1]) : 0u;
+  ld[k] = ((uint32_t)(l < 0xffff ? l : 0xffff) << 16) | (d << 8) | u;
+}
+
+__device__ __forceinline__ uint32_t ix_lc(const int32_t* lcp, uint32_t n, int64_t k) {
+  if (k < 0 || k > (int64_t)n) return 0;
+  const int32_t v = lcp[k];
+  return v < 0 ? 0u : (uint32_t)(v < 255 ? v : 255);
+}
+
+__device__ __forceinline__ void ix_rec(const int32_t* lcp, uint32_t n, uint32_t r, uint4* o) {
+  uint32_t w[3] = {0, 0, 0};
+#pragma unroll
+  for (int j = 0; j < 6; j++) w[j / 4] |= ix_lc(lcp, n, (int64_t)r - j) << (8 * (j % 4));
+#pragma unroll
+  for (int j = 0; j < 6; j++) w[(6 + j) / 4] |= ix_lc(lcp, n, (int64_t)r + 1 + j) << (8 * ((6 + j) % 4));
+  *o = make_uint4(r, w[0], w[1], w[2]);
+}
+
+__global__ void k_ix_adjacency(const int32_t* __restrict__ sa, const uint32_t* __restrict__ isa,
+                               const int32_t* __restrict__ lcp, uint32_t n, uint4* __restrict__ pr,
+                               uint4* __restrict__ ir) {
+  const uint32_t k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k >= n) return;
+  const uint32_t s = (uint32_t)sa[k];
+  if (s == n - 1) pr[k] = make_uint4(0xffffffffu, 0, 0, 0);
+  else ix_rec(lcp, n, isa[s + 1], &pr[k]);
+  ix_rec(lcp, n, isa[k], &ir[k]);
+}
+
+// prefix-rank tables, one length l per launch (state cur/term carried over l)
+__global__ void k_ix_pfx_count(const uint8_t* __restrict__ x, uint32_t n, uint32_t l, uint32_t B,
+                               const uint8_t* __restrict__ map, const uint32_t* __restrict__ below,
+                               uint32_t* __restrict__ cur, uint8_t* __restrict__ term, uint32_t* __restrict__ cf,
+                               uint32_t* __restrict__ ct) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p >= n) return;
+  uint32_t sym = 0;
+  uint8_t t = term[p];
+  if (!t) {
+    const uint64_t at = (uint64_t)p + l - 1;
+    if (at >= n) {
+      t = 1;
+    } else {
+      const uint8_t b = x[at];
+      if (map[b] == 0xff) { t = 1; sym = below[b]; }
+      else sym = map[b];
+    }
+    term[p] = t;
+  }
+  const uint32_t c = (cur[p] << B) + sym;
+  cur[p] = c;
+  atomicAdd(t ? &ct[c] : &cf[c], 1u);
+}
+
+__global__ void k_ix_pfx_write(const uint32_t* __restrict__ cfEx, const uint32_t* __restrict__ ctIn,
+                               const uint32_t* __restrict__ cf, uint64_t E1, uint32_t* __restrict__ o) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= E1) return;
+  o[2 * c] = cfEx[c] + ctIn[c];
+  o[2 * c + 1] = cf[c];
+}
+
+static inline dim3 gix(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+
+void launch_ix_plcp_check(const int32_t* plcp, uint32_t n, uint32_t* err, hipStream_t st) {
+  if (n > 1) hipLaunchKernelGGL(k_ix_plcp_check, gix(n), dim3(256), 0, st, plcp, n, err);
+}
+void launch_ix_level(const int32_t* prev, uint32_t prevLen, int32_t* cur, uint32_t curLen, hipStream_t st) {
+  if (curLen) hipLaunchKernelGGL(k_ix_level, gix(curLen), dim3(256), 0, st, prev, prevLen, cur, curLen);
+}
+void launch_ix_child(const uint8_t* x, const int32_t* sa, const int32_t* lcp, uint32_t n, uint32_t* ld,
+                     hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_ix_child, gix(n), dim3(256), 0, st, x, sa, lcp, n, ld);
+}
+void launch_ix_adjacency(const int32_t* sa, const uint32_t* isa, const int32_t* lcp, uint32_t n, uint32_t* pr,
+                         uint32_t* ir, hipStream_t st) {
+  if (n)
+    hipLaunchKernelGGL(k_ix_adjacency, gix(n), dim3(256), 0, st, sa, isa, lcp, n, (uint4*)pr, (uint4*)ir);
+}
+void launch_ix_pfx_count(const uint8_t* x, uint32_t n, uint32_t l, uint32_t B, const uint8_t* map,
+                         const uint32_t* below, uint32_t* cur, uint8_t* term, uint32_t* cf, uint32_t* ct,
+                         hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_ix_pfx_count, gix(n), dim3(256), 0, st, x, n, l, B, map, below, cur, term, cf, ct);
+}
+void launch_ix_pfx_write(const uint32_t* cfEx, const uint32_t* ctIn, const uint32_t* cf, uint64_t E1, uint32_t* o,
+                         hipStream_t st) {
+  if (E1) hipLaunchKernelGGL(k_ix_pfx_write, gix(E1), dim3(256), 0, st, cfEx, ctIn, cf, E1, o);
+}
+
+}  // namespace cmsbwt

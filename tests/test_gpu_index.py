@@ -1,7 +1,9 @@
 """Reference index on the GPU (ref_index.hip)
 against the host build (SA-IS + Φ, host_index.cpp, itself checked against a
 brute-force suffix sort in test_host.py): SA, ISA, LCP (with LCP[n] = -1),
-the max-neighbour PLCP of FN:272-274 and the BWT must be identical.
+the max-neighbour PLCP of FN:272-274 and the BWT must be identical, and so
+must the walk tables built from them on the device (LCP block minima, child
+table, adjacency records, prefix-rank tables) vs their host builds.
 The references include long exact repeats and periodic strings (many
 doubling rounds) and raw references with non-ACGT bytes."""
 import os
@@ -13,7 +15,8 @@ import cases
 
 pytestmark = pytest.mark.gpu
 
-NAMES = ["ref_sa", "ref_isa", "ref_lcp", "ref_plcp", "ref_bwt"]
+NAMES = ["ref_sa", "ref_isa", "ref_lcp", "ref_plcp", "ref_bwt",
+         "ref_lvl", "ref_ld", "ref_pr", "ref_ir", "ref_pfx"]  # + the walk's tables (same layouts)
 
 
 def _arrays(engine, ref, host):

@@ -7,7 +7,8 @@ mkdir -p gpurun_out
 df -h /tmp | tail -1
 W=${E2E_DIR:-/tmp/e2e}
 mkdir -p $W
-for cfg in ${E2E_CONFIGS:-"10000000 100 0.001 3 c2" "10000000 1000 0.001 4 c3"}; do
+IFS=';' read -ra CFGS <<< "${E2E_CONFIGS:-10000000 100 0.001 3 c2;10000000 1000 0.001 4 c3}"
+for cfg in "${CFGS[@]}"; do
     set -- $cfg
     avail=$(df --output=avail -B1 /tmp | tail -1)
     need=$(( $1 * $2 * 13 / 10 ))
