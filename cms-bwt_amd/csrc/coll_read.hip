@@ -206,3 +206,67 @@ void launch_rd_emit(const uint8_t* raw, uint64_t len, uint64_t ntiles, const uin
 }
 
 }  // namespace cmsbwt
+
+// ---------------------------------------------------------------- output
+// Plain .bwt expansion of the runs (FN:1631-1694 writes N + D - 1 bytes):
+// bytes [o0, o0 + len) of the expanded BWT, 256 per thread; a thread finds
+// the run holding its first byte by binary search over the run starts and
+// walks forward.  Records are the packed 9-byte (u64 length, char) runs.
+namespace cmsbwt {
+
+__global__ void k_out_split(const uint8_t* __restrict__ rec, uint64_t R, unsigned long long* __restrict__ len,
+                            uint8_t* __restrict__ chr) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= R) return;
+  const uint8_t* r = rec + 9 * j;
+  unsigned long long v = 0;
+#pragma unroll
+  for (int b = 0; b < 8; b++) v |= (unsigned long long)r[b] << (8 * b);
+  len[j] = v;
+  chr[j] = r[8];
+}
+
+constexpr uint32_t kOutPerThread = 256;
+
+__global__ void k_out_expand(const unsigned long long* __restrict__ start, const uint8_t* __restrict__ chr, uint64_t R,
+                             uint64_t o0, uint64_t len, uint8_t* __restrict__ out) {
+  const uint64_t a = ((uint64_t)blockIdx.x * blockDim.x + threadIdx.x) * kOutPerThread;
+  if (a >= len) return;
+  const uint64_t p0 = o0 + a;
+  uint64_t lo = 0, hi = R;  // last run with start <= p0
+  while (hi - lo > 1) {
+    const uint64_t m = (lo + hi) >> 1;
+    if (start[m] <= p0) lo = m; else hi = m;
+  }
+  uint64_t r = lo;
+  uint64_t next = r + 1 < R ? start[r + 1] : ~0ull;
+  uint8_t c = chr[r];
+  const uint64_t e = a + kOutPerThread < len ? a + kOutPerThread : len;
+  uint64_t k = a;
+  while (k < e) {
+    if (o0 + k >= next) {
+      r++;
+      c = chr[r];
+      next = r + 1 < R ? start[r + 1] : ~0ull;
+      continue;
+    }
+    uint64_t stop = next - o0 < e ? next - o0 : e;  // bytes of run r in [k, stop)
+    for (; k < stop && (k & 15); k++) out[k] = c;
+    const uint32_t w = 0x01010101u * c;
+    for (; k + 16 <= stop; k += 16) *reinterpret_cast<uint4*>(out + k) = make_uint4(w, w, w, w);
+    for (; k < stop; k++) out[k] = c;
+  }
+}
+
+void launch_out_split(const uint8_t* rec, uint64_t R, unsigned long long* len, uint8_t* chr, hipStream_t st) {
+  if (R) hipLaunchKernelGGL(k_out_split, dim3((unsigned)((R + 255) / 256)), dim3(256), 0, st, rec, R, len, chr);
+}
+void launch_out_expand(const unsigned long long* start, const uint8_t* chr, uint64_t R, uint64_t o0, uint64_t len,
+                       uint8_t* out, hipStream_t st) {
+  const uint64_t th = (len + kOutPerThread - 1) / kOutPerThread;
+  if (R && len)
+    hipLaunchKernelGGL(k_out_expand, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, st, start, chr, R, o0, len,
+                       out);
+}
+
+}  // namespace cmsbwt

@@ -24,6 +24,10 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <deque>
+#include <functional>
+#include <mutex>
 #include <thread>
 #include <fstream>
 #include <map>
@@ -744,18 +748,23 @@ struct Engine {
   uint64_t pinnedBytes = 0;
   uint64_t collMeta[3] = {0, 0, 0};  // sn, chars, ndocs (parity copies)
 
+  // 2 * nt pinned buffers of CH bytes (reallocated only when the request changes)
+  void ensure_pinned(uint32_t nt, uint64_t CH) {
+    if (pinned.size() == 2 * nt && pinnedBytes == CH) return;
+    for (void* b : pinned) (void)hipHostFree(b);
+    pinned.assign(2 * nt, nullptr);
+    pinnedBytes = 0;
+    for (auto& b : pinned) HIPCHK(hipHostMalloc(&b, CH, hipHostMallocDefault));
+    pinnedBytes = CH;
+  }
+
   // pread of the file into pinned buffers by `nt` threads, each DMAing its
   // chunks to dst on its own stream (double-buffered: reading chunk c+2T
   // overlaps the copy of chunk c).
   void stream_file(int fd, uint64_t fsz, uint8_t* dst) {
     const uint32_t nt = std::max(1u, std::min(64u, env_u32("CMSBWT_READ_THREADS", 8)));
-    const uint64_t CH = (uint64_t)std::max(1u, env_u32("CMSBWT_READ_CHUNK_MB", 32)) << 20;
-    if (pinned.size() < 2 * nt || pinnedBytes < CH) {
-      for (void* b : pinned) (void)hipHostFree(b);
-      pinned.assign(2 * nt, nullptr);
-      for (auto& b : pinned) HIPCHK(hipHostMalloc(&b, CH, hipHostMallocDefault));
-      pinnedBytes = CH;
-    }
+    ensure_pinned(nt, (uint64_t)std::max(1u, env_u32("CMSBWT_READ_CHUNK_MB", 32)) << 20);
+    const uint64_t CH = pinnedBytes;
     const uint64_t nch = (fsz + CH - 1) / CH;
     std::atomic<int> err{0};
     std::vector<std::thread> th;
@@ -942,8 +951,11 @@ struct Engine {
       w2stats.alloc(32);
       w2stats.zero(st);
     }
-    // pool sized for ~3% heads + one partial block per chunk; grown on overflow
-    uint64_t cap = (uint64_t)nch + chars / 32 / kPoolB + 1024;
+    // pool sized for the head density of the previous walk on this engine
+    // (3 % at first) + one partial block per chunk; an overflow re-runs the
+    // walk with the measured size, so only the first walk of a denser
+    // workload pays twice (1 % SNP collections have ~10 % heads)
+    uint64_t cap = (uint64_t)nch + (uint64_t)((double)chars * poolDensity * 1.1) / kPoolB + 1024;
     DBuf<HeadRec> rec;
     DBuf<uint32_t> blkChunk, blkSeq;
     uint32_t usedBlocks = 0;
@@ -968,6 +980,7 @@ struct Engine {
       if (usedBlocks <= cap) break;
       cap = (uint64_t)usedBlocks + (uint64_t)nch + 1024;
     }
+    if (chars) poolDensity = std::max(1.0 / 32, (double)usedBlocks * kPoolB / (double)chars);
     if (w2stats.p) {
       static const char* names[32] = {"done", "next", "bs_text", "bs_sa", "bs_x", "fail_sa", "lce_sa", "lce",
                                        "skip1", "skip0", "gallop", "skipbs", "isa1", "conp", "ext1", "adj",
@@ -1483,6 +1496,7 @@ struct Engine {
     stats.positions = count_positions(sPos);
     stats.t_merge_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
+  double poolDensity = 1.0 / 32;  // head-pool records per collection char (learned per engine)
   float counter_kernel_ms = 0;
   bool keptT = false;  // rank2head written by the last merge
   uint32_t windows = 0, crossings = 0;
@@ -1506,37 +1520,119 @@ struct Engine {
     sync();
   }
 
+  // Device -> file through the pinned pool: chunk c (bytes [c*CH, ...)) is
+  // produced on `st` by produce(off, len) (a device pointer), copied into a
+  // pinned buffer and written with pwrite by one of the writer threads while
+  // the next chunks are produced and copied.
+  void stream_out(int fd, uint64_t total, const std::function<const uint8_t*(uint64_t, uint64_t)>& produce) {
+    const uint32_t nt = std::max(1u, std::min(64u, env_u32("CMSBWT_WRITE_THREADS", 8)));
+    ensure_pinned(nt, (uint64_t)std::max(1u, env_u32("CMSBWT_READ_CHUNK_MB", 32)) << 20);
+    const uint64_t CH = pinnedBytes;
+    const uint32_t NB = (uint32_t)pinned.size();
+    const uint64_t nch = (total + CH - 1) / CH;
+    std::vector<hipEvent_t> ev(NB, nullptr);
+    for (auto& e : ev) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    std::mutex mu;
+    std::condition_variable cv;
+    std::deque<uint64_t> q;
+    std::vector<char> busy(NB, 0);
+    bool done = false;
+    std::atomic<int> err{0};
+    std::vector<std::thread> th;
+    for (uint32_t k = 0; k < nt; k++)
+      th.emplace_back([&] {
+        while (true) {
+          uint64_t c;
+          {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return done || !q.empty(); });
+            if (q.empty()) return;
+            c = q.front();
+            q.pop_front();
+          }
+          const uint32_t b = (uint32_t)(c % NB);
+          const uint64_t off = c * CH, len = std::min(CH, total - off);
+          if (hipEventSynchronize(ev[b]) != hipSuccess) err = 2;
+          uint64_t put = 0;
+          while (!err && put < len) {
+            ssize_t w = pwrite(fd, (const uint8_t*)pinned[b] + put, len - put, (off_t)(off + put));
+            if (w <= 0) { err = 1; break; }
+            put += (uint64_t)w;
+          }
+          std::lock_guard<std::mutex> lk(mu);
+          busy[b] = 0;
+          cv.notify_all();
+        }
+      });
+    auto finish = [&] {
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        done = true;
+      }
+      cv.notify_all();
+      for (auto& t : th) t.join();
+      for (auto e : ev) (void)hipEventDestroy(e);
+    };
+    try {
+      for (uint64_t c = 0; c < nch && !err; c++) {
+        const uint32_t b = (uint32_t)(c % NB);
+        {
+          std::unique_lock<std::mutex> lk(mu);
+          cv.wait(lk, [&] { return !busy[b]; });
+          busy[b] = 1;
+        }
+        const uint64_t off = c * CH, len = std::min(CH, total - off);
+        const uint8_t* src = produce(off, len);
+        HIPCHK(hipMemcpyAsync(pinned[b], src, len, hipMemcpyDeviceToHost, st));
+        HIPCHK(hipEventRecord(ev[b], st));
+        std::lock_guard<std::mutex> lk(mu);
+        q.push_back(c);
+        cv.notify_all();
+      }
+    } catch (...) {
+      finish();
+      throw;
+    }
+    finish();
+    if (err == 1) throw InputError{CMSBWT_EIO, "write error"};
+    if (err) throw HipError{"HIP error while writing the output"};
+  }
+
   void write_output(const std::string& outname, int rle) {
     if (!merged) throw InputError{CMSBWT_EARG, "run merge first"};
     if (rle != lastRle) throw InputError{CMSBWT_EARG, "merge was run with a different output format"};
     auto t0 = std::chrono::steady_clock::now();
-    std::vector<uint8_t> host(nruns * 9);
-    copy_runs(host.data(), host.size());
-    if (rle) {
-      FILE* f = fopen((outname + ".rl_bwt").c_str(), "wb");
-      if (!f) throw InputError{CMSBWT_EIO, "cannot open " + outname + ".rl_bwt"};
-      fwrite(host.data(), 1, host.size(), f);
-      fclose(f);
-    } else {
-      FILE* f = fopen((outname + ".bwt").c_str(), "wb");
-      if (!f) throw InputError{CMSBWT_EIO, "cannot open " + outname + ".bwt"};
-      std::vector<uint8_t> buf(1 << 20);
-      size_t fill = 0;
-      for (uint64_t j = 0; j < nruns; j++) {
-        uint64_t len;
-        memcpy(&len, host.data() + 9 * j, 8);
-        uint8_t c = host[9 * j + 8];
-        while (len) {
-          uint64_t k = std::min<uint64_t>(len, buf.size() - fill);
-          memset(buf.data() + fill, c, k);
-          fill += k;
-          len -= k;
-          if (fill == buf.size()) { fwrite(buf.data(), 1, fill, f); fill = 0; }
-        }
+    const std::string path = outname + (rle ? ".rl_bwt" : ".bwt");
+    int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    if (fd < 0) throw InputError{CMSBWT_EIO, "cannot open " + path};
+    try {
+      if (rle) {  // FN:1695-1777: the packed 9-byte records as they are in HBM
+        stream_out(fd, nruns * 9, [&](uint64_t off, uint64_t) { return runs.p + off; });
+      } else {    // FN:1631-1694: the runs expanded on the device, chunk by chunk
+        DBuf<unsigned long long> rlen, rstart;
+        DBuf<uint8_t> rchr, chunk;
+        rlen.alloc(std::max<uint64_t>(nruns, 1));
+        rstart.alloc(std::max<uint64_t>(nruns, 1));
+        rchr.alloc(std::max<uint64_t>(nruns, 1));
+        launch_out_split(runs.p, nruns, rlen.p, rchr.p, st);
+        exscan(rlen.p, rstart.p, 0ull, nruns);
+        const uint64_t total = nruns ? read1(rstart.p + nruns - 1) + read1(rlen.p + nruns - 1) : 0;
+        ensure_pinned(std::max(1u, std::min(64u, env_u32("CMSBWT_WRITE_THREADS", 8))),
+                      (uint64_t)std::max(1u, env_u32("CMSBWT_READ_CHUNK_MB", 32)) << 20);
+        const uint64_t CH = pinnedBytes;
+        chunk.alloc(2 * CH);
+        uint64_t c = 0;
+        stream_out(fd, total, [&](uint64_t off, uint64_t len) {
+          uint8_t* dst = chunk.p + (c++ & 1) * CH;  // stream order: D2H of chunk c-2 precedes this
+          launch_out_expand(rstart.p, rchr.p, nruns, off, len, dst, st);
+          return dst;
+        });
       }
-      if (fill) fwrite(buf.data(), 1, fill, f);
-      fclose(f);
+    } catch (...) {
+      close(fd);
+      throw;
     }
+    if (close(fd) != 0) throw InputError{CMSBWT_EIO, "cannot close " + path};
     if (R.n < 1000000 && !dm.on) {  // FN:919-924 small-reference side output (single-GPU merge)
       std::vector<unsigned long long> c((uint64_t)H + 1);
       HIPCHK(hipMemcpyAsync(c.data(), counter.p, c.size() * 8, hipMemcpyDeviceToHost, st));

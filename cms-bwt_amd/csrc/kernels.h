@@ -67,6 +67,12 @@ void launch_rd_emit(const uint8_t* raw, uint64_t len, uint64_t ntiles, const uin
                     const uint64_t* outBase, const uint64_t* sepBase, const uint8_t* present, uint8_t* out,
                     uint64_t* docOff, unsigned long long* badByte, hipStream_t st);
 
+// coll_read.hip: plain .bwt expansion of the packed runs, bytes [o0, o0+len)
+// of the output into out (16-B aligned); start = exclusive scan of lengths
+void launch_out_split(const uint8_t* rec, uint64_t R, unsigned long long* len, uint8_t* chr, hipStream_t st);
+void launch_out_expand(const unsigned long long* start, const uint8_t* chr, uint64_t R, uint64_t o0, uint64_t len,
+                       uint8_t* out, hipStream_t st);
+
 // ref_index.hip: reference index on the device (prefix-doubling SA, Φ-PLCP)
 constexpr uint32_t kIdxH0 = 7;      // initial key: 7 symbols of 9 bits
 constexpr uint32_t kIdxChunk = 64;  // positions per thread in the Φ-PLCP pass

@@ -246,3 +246,31 @@ def test_config5_proxy_golden(engine, tmp_path):
     assert engine.stats().runs == g["rl_runs"]
     import hashlib
     assert hashlib.sha256(engine.runs_bytes()).hexdigest() == g["rl_bwt_sha256"]
+
+
+@pytest.mark.parametrize("threads,chunk_mb", [("3", "1"), ("8", "32")])
+def test_writer_streams_both_formats(engine, tmp_path, threads, chunk_mb):
+    """Output files through the pinned writer (device .bwt expansion, pwrite
+    threads): 1 MiB chunks over 3 writers split the 10 MB .bwt and the 7.6 MB
+    .rl_bwt of config 1 into many chunks; both equal the golden sha256."""
+    import hashlib
+    import json
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import gen_np
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["c1"]
+    pre = str(tmp_path / "c1")
+    gen_np.gen(1_000_000, 10, 0.001, 11, pre)
+    env = {"CMSBWT_WRITE_THREADS": threads, "CMSBWT_READ_CHUNK_MB": chunk_mb}
+    os.environ.update(env)
+    try:
+        engine.initialize_reference(pre + ".ref.fa")
+        engine.load_collection_file(pre + ".coll.fa")
+        for rle, ext, key in ((True, ".rl_bwt", "rl_bwt_sha256"), (False, ".bwt", "bwt_sha256")):
+            engine.step(rle=rle)
+            engine.write_output(pre + "_gpu", rle)
+            assert hashlib.sha256(open(pre + "_gpu" + ext, "rb").read()).hexdigest() == g[key], ext
+    finally:
+        for k in env:
+            os.environ.pop(k, None)
+    assert os.path.getsize(pre + "_gpu.bwt") == g["bwt_bytes"]
