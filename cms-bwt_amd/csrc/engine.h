@@ -379,6 +379,7 @@ struct Engine {
     DBuf<uint32_t> err;
     err.alloc(1);
     err.zero(st);
+    if (env_u32("CMSBWT_TIMING", 0)) fprintf(stderr, "[index] sa         %.3f s\n", std::chrono::duration<double>(t1 - t0).count());
     {
       DBuf<int32_t> phi, plcpRaw;
       phi.alloc(n);
@@ -409,7 +410,18 @@ struct Engine {
     R.bwt = dbwt.p;
     R.n = n;
     if (read1(err.p)) throw InputError{CMSBWT_EINPUT, "internal: PLCP monotonicity violated"};
+    const bool tm = env_u32("CMSBWT_TIMING", 0) != 0;
+    auto mark = [&](const char* what) {
+      if (!tm) return;
+      sync();
+      static auto last = now();
+      auto t = now();
+      fprintf(stderr, "[index] %-10s %.3f s\n", what, std::chrono::duration<double>(t - last).count());
+      last = t;
+    };
+    mark("lcp+levels");
     build_prefix_tables(true);
+    mark("pfx");
     R.ld = nullptr;
     if (env_u32("CMSBWT_EXT8", 1)) {
       dld.alloc((uint64_t)n + 16);
@@ -417,6 +429,7 @@ struct Engine {
       launch_ix_child(dx.p, dsa.p, dlcp.p, n, dld.p, st);
       R.ld = dld.p;
     }
+    mark("child");
     dpr.alloc((uint64_t)n + 16);
     dir.alloc((uint64_t)n + 16);
     dpr.zero(st);
@@ -426,6 +439,7 @@ struct Engine {
     R.ir = dir.p;
     HIPCHK(hipGetLastError());
     sync();
+    mark("adjacency");
     hix.t_sa = std::chrono::duration<double>(t1 - t0).count();
     hix.t_lcp = std::chrono::duration<double>(now() - t1).count();
   }
@@ -434,8 +448,8 @@ struct Engine {
   // reference (FN:151-310)
   void load_reference_bytes(const std::string& trimmed) {
     auto t0 = std::chrono::steady_clock::now();
-    for (unsigned char c : trimmed)
-      if (c == 2) throw InputError{CMSBWT_EINPUT, "reference contains byte 0x02 (the document separator)"};
+    if (memchr(trimmed.data(), 2, trimmed.size()))
+      throw InputError{CMSBWT_EINPUT, "reference contains byte 0x02 (the document separator)"};
     if (trimmed.size() + 130 >= (1ull << 31)) throw InputError{CMSBWT_ELIMIT, "reference longer than 2^31 (int32 SA)"};
     const char* hi = getenv("CMSBWT_HOST_INDEX");
     if (hi && *hi && *hi != '0') {
@@ -536,8 +550,7 @@ struct Engine {
     memset(R.pfxOff, 0, sizeof(R.pfxOff));
     if (!env_u32("CMSBWT_PFX", 1)) return;
     const uint32_t n = hix.n;
-    uint64_t cnt[256] = {0};
-    for (uint64_t k = 0; k < hix.ref_len; k++) cnt[(uint8_t)hix.x[k]]++;
+    const uint64_t* cnt = hix.hist;  // byte counts of the trimmed reference (augment_reference)
     std::vector<uint8_t> map(256, 0xff);
     std::vector<uint32_t> below(256, 0);  // r(b): symbols smaller than byte b
     uint32_t sigma = 0;
@@ -1603,10 +1616,14 @@ struct Engine {
     if (rle != lastRle) throw InputError{CMSBWT_EARG, "merge was run with a different output format"};
     auto t0 = std::chrono::steady_clock::now();
     const std::string path = outname + (rle ? ".rl_bwt" : ".bwt");
-    int fd = open(path.c_str(), O_WRONLY | O_CREAT | O_TRUNC, 0644);
+    // no O_TRUNC: rewriting an existing output in place and cutting it to
+    // size afterwards avoids freeing and refaulting its page-cache pages
+    int fd = open(path.c_str(), O_WRONLY | O_CREAT, 0644);
     if (fd < 0) throw InputError{CMSBWT_EIO, "cannot open " + path};
+    uint64_t outBytes = 0;
     try {
       if (rle) {  // FN:1695-1777: the packed 9-byte records as they are in HBM
+        outBytes = nruns * 9;
         stream_out(fd, nruns * 9, [&](uint64_t off, uint64_t) { return runs.p + off; });
       } else {    // FN:1631-1694: the runs expanded on the device, chunk by chunk
         DBuf<unsigned long long> rlen, rstart;
@@ -1617,6 +1634,7 @@ struct Engine {
         launch_out_split(runs.p, nruns, rlen.p, rchr.p, st);
         exscan(rlen.p, rstart.p, 0ull, nruns);
         const uint64_t total = nruns ? read1(rstart.p + nruns - 1) + read1(rlen.p + nruns - 1) : 0;
+        outBytes = total;
         ensure_pinned(std::max(1u, std::min(64u, env_u32("CMSBWT_WRITE_THREADS", 8))),
                       (uint64_t)std::max(1u, env_u32("CMSBWT_READ_CHUNK_MB", 32)) << 20);
         const uint64_t CH = pinnedBytes;
@@ -1632,6 +1650,7 @@ struct Engine {
       close(fd);
       throw;
     }
+    if (ftruncate(fd, (off_t)outBytes) != 0) { close(fd); throw InputError{CMSBWT_EIO, "cannot size " + path}; }
     if (close(fd) != 0) throw InputError{CMSBWT_EIO, "cannot close " + path};
     if (R.n < 1000000 && !dm.on) {  // FN:919-924 small-reference side output (single-GPU merge)
       std::vector<unsigned long long> c((uint64_t)H + 1);

@@ -246,8 +246,8 @@ int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path
   log << "MS-walk kernel: " << s.ms_walk_kernel_ms << " ms; collection pass: " << ms(t1, now()) << " ms\n";
   if (stats_out) *stats_out = e.stats;
   if (a->verbose)
-    fprintf(stderr, "index %.3fs upload %.3fs walk %.3fs (kernel %.2fms) merge %.3fs write %.3fs runs %llu\n",
-            s.t_index_s, s.t_upload_s, s.t_ms_walk_s, s.ms_walk_kernel_ms, s.t_merge_s, s.t_write_s,
+    fprintf(stderr, "index %.3fs (sa %.3fs, tables %.3fs) upload %.3fs walk %.3fs (kernel %.2fms) merge %.3fs write %.3fs runs %llu\n",
+            s.t_index_s, e.hix.t_sa, e.hix.t_lcp, s.t_upload_s, s.t_ms_walk_s, s.ms_walk_kernel_ms, s.t_merge_s, s.t_write_s,
             (unsigned long long)s.runs);
   cmsbwt_ctx_destroy(ctx);
   return CMSBWT_OK;

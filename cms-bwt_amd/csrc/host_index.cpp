@@ -130,14 +130,25 @@ void augment_reference(const std::string& trimmed, HostIndex& ix) {
   x = trimmed;
   ix.ref_len = trimmed.size();
   // FN:231-237: append absent bytes 3..127, then \1 \0
-  bool seen[256] = {false};
-  for (unsigned char c : x) seen[c] = true;
-  for (int c = 3; c < 128; c++) if (!seen[c]) x.push_back((char)c);
+  // one histogram pass (4 interleaved counters) gives seen[], present[] and
+  // the symbol counts of the prefix-rank tables
+  uint64_t h4[4][256] = {{0}};
+  const unsigned char* p = (const unsigned char*)trimmed.data();
+  const size_t L = trimmed.size();
+  size_t i = 0;
+  for (; i + 4 <= L; i += 4) {
+    h4[0][p[i]]++;
+    h4[1][p[i + 1]]++;
+    h4[2][p[i + 2]]++;
+    h4[3][p[i + 3]]++;
+  }
+  for (; i < L; i++) h4[0][p[i]]++;
+  for (int c = 0; c < 256; c++) ix.hist[c] = h4[0][c] + h4[1][c] + h4[2][c] + h4[3][c];
+  for (int c = 3; c < 128; c++) if (!ix.hist[c]) x.push_back((char)c);
   x.push_back((char)1);
   x.push_back((char)0);
   ix.n = (uint32_t)x.size();
-  for (int c = 0; c < 256; c++) ix.present[c] = false;
-  for (uint32_t i = 0; i + 2 < ix.n; i++) ix.present[(uint8_t)x[i]] = true;
+  for (int c = 0; c < 256; c++) ix.present[c] = ix.hist[c] != 0 || (c >= 3 && c < 128);
 }
 
 void build_index(const std::string& trimmed, HostIndex& ix) {

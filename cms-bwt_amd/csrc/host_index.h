@@ -16,6 +16,7 @@ struct HostIndex {
   std::vector<int32_t> plcp;   // _PLCP after the max-neighbour redefinition (FN:272-274)
   std::vector<uint8_t> bwt;    // _BWT
   bool present[256];           // bytes occurring in x[0..n-3] (collection check)
+  uint64_t hist[256];          // byte counts of the trimmed reference
   double t_sa = 0, t_lcp = 0;
 };
 

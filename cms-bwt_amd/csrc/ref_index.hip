@@ -14,6 +14,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <algorithm>
+
 #include "kernels.h"
 
 namespace cmsbwt {
@@ -230,6 +232,43 @@ __global__ void k_ix_pfx_count(const uint8_t* __restrict__ x, uint32_t n, uint32
   atomicAdd(t ? &ct[c] : &cf[c], 1u);
 }
 
+// same, for short lengths (E1 <= kPfxLds): block-private histograms in LDS
+// (a few hundred bins would serialise 1e8 global atomics), flushed once
+constexpr uint32_t kPfxLds = 4097;
+__global__ void __launch_bounds__(256) k_ix_pfx_count_lds(const uint8_t* __restrict__ x, uint32_t n, uint32_t l,
+                                                          uint32_t B, const uint8_t* __restrict__ map,
+                                                          const uint32_t* __restrict__ below,
+                                                          uint32_t* __restrict__ cur, uint8_t* __restrict__ term,
+                                                          uint32_t* __restrict__ cf, uint32_t* __restrict__ ct,
+                                                          uint32_t E1) {
+  __shared__ uint32_t hf[kPfxLds], ht[kPfxLds];
+  for (uint32_t i = threadIdx.x; i < E1; i += blockDim.x) hf[i] = ht[i] = 0;
+  __syncthreads();
+  for (uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; p < n; p += (uint64_t)gridDim.x * blockDim.x) {
+    uint32_t sym = 0;
+    uint8_t t = term[p];
+    if (!t) {
+      const uint64_t at = p + l - 1;
+      if (at >= n) {
+        t = 1;
+      } else {
+        const uint8_t b = x[at];
+        if (map[b] == 0xff) { t = 1; sym = below[b]; }
+        else sym = map[b];
+      }
+      term[p] = t;
+    }
+    const uint32_t c = (cur[p] << B) + sym;
+    cur[p] = c;
+    atomicAdd(t ? &ht[c] : &hf[c], 1u);
+  }
+  __syncthreads();
+  for (uint32_t i = threadIdx.x; i < E1; i += blockDim.x) {
+    if (hf[i]) atomicAdd(&cf[i], hf[i]);
+    if (ht[i]) atomicAdd(&ct[i], ht[i]);
+  }
+}
+
 __global__ void k_ix_pfx_write(const uint32_t* __restrict__ cfEx, const uint32_t* __restrict__ ctIn,
                                const uint32_t* __restrict__ cf, uint64_t E1, uint32_t* __restrict__ o) {
   const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -258,7 +297,15 @@ void launch_ix_adjacency(const int32_t* sa, const uint32_t* isa, const int32_t* 
 void launch_ix_pfx_count(const uint8_t* x, uint32_t n, uint32_t l, uint32_t B, const uint8_t* map,
                          const uint32_t* below, uint32_t* cur, uint8_t* term, uint32_t* cf, uint32_t* ct,
                          hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_ix_pfx_count, gix(n), dim3(256), 0, st, x, n, l, B, map, below, cur, term, cf, ct);
+  if (!n) return;
+  const uint64_t E1 = (1ull << (B * l)) + 1;
+  if (E1 <= kPfxLds) {
+    const uint64_t blocks = std::min<uint64_t>((n + 255) / 256, 2048);
+    hipLaunchKernelGGL(k_ix_pfx_count_lds, dim3((unsigned)blocks), dim3(256), 0, st, x, n, l, B, map, below, cur,
+                       term, cf, ct, (uint32_t)E1);
+  } else {
+    hipLaunchKernelGGL(k_ix_pfx_count, gix(n), dim3(256), 0, st, x, n, l, B, map, below, cur, term, cf, ct);
+  }
 }
 void launch_ix_pfx_write(const uint32_t* cfEx, const uint32_t* ctIn, const uint32_t* cf, uint64_t E1, uint32_t* o,
                          hipStream_t st) {
