@@ -968,6 +968,7 @@ struct Engine {
     // (3 % at first) + one partial block per chunk; an overflow re-runs the
     // walk with the measured size, so only the first walk of a denser
     // workload pays twice (1 % SNP collections have ~10 % heads)
+    if (!densityLearned && !v1 && nch >= 4096) sample_density(nch);
     uint64_t cap = (uint64_t)nch + (uint64_t)((double)chars * poolDensity * 1.1) / kPoolB + 1024;
     DBuf<HeadRec> rec;
     DBuf<uint32_t> blkChunk, blkSeq;
@@ -993,7 +994,10 @@ struct Engine {
       if (usedBlocks <= cap) break;
       cap = (uint64_t)usedBlocks + (uint64_t)nch + 1024;
     }
-    if (chars) poolDensity = std::max(1.0 / 32, (double)usedBlocks * kPoolB / (double)chars);
+    if (chars) {
+      poolDensity = std::max(1.0 / 32, (double)usedBlocks * kPoolB / (double)chars);
+      densityLearned = true;
+    }
     if (w2stats.p) {
       static const char* names[32] = {"done", "next", "bs_text", "bs_sa", "bs_x", "fail_sa", "lce_sa", "lce",
                                        "skip1", "skip0", "gallop", "skipbs", "isa1", "conp", "ext1", "adj",
@@ -1510,6 +1514,39 @@ struct Engine {
     stats.t_merge_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   double poolDensity = 1.0 / 32;  // head-pool records per collection char (learned per engine)
+  bool densityLearned = false;
+  // First walk on this engine: walk every 32nd chunk into a scratch pool to
+  // estimate the head density, so a dense collection (1 % SNP: ~10 % heads)
+  // does not overflow the pool and re-run the whole walk.
+  void sample_density(uint32_t nch) {
+    std::vector<uint32_t> ids;
+    for (uint32_t c = 0; c < nch; c += 32) ids.push_back(c);
+    const uint32_t ns = (uint32_t)ids.size();
+    DBuf<uint32_t> order, bstart, cnt, used, next;
+    order.alloc(ns);
+    bstart.alloc(2);
+    cnt.alloc(nch);
+    used.alloc(1);
+    next.alloc(16 * 8);
+    const uint32_t bs[2] = {0, ns};
+    HIPCHK(hipMemcpyAsync(order.p, ids.data(), ns * 4, hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(bstart.p, bs, 8, hipMemcpyHostToDevice, st));
+    used.zero(st);
+    next.zero(st);
+    const uint64_t sampleChars = (uint64_t)ns * plan.C;
+    const uint64_t cap = ns + sampleChars / 2 / kPoolB + 1024;  // up to 50 % heads
+    DBuf<HeadRec> rec;
+    DBuf<uint32_t> blkChunk, blkSeq;
+    rec.alloc(cap * kPoolB);
+    blkChunk.alloc(cap);
+    blkSeq.alloc(cap);
+    Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
+    launch_ms_walk2(R, dtext.p, ddoc.p, plan.dch.p, nch, order.p, bstart.p, 1, next.p, pool, cnt.p,
+                    std::min<uint32_t>(walk_lanes(), ns), nullptr, st);
+    HIPCHK(hipGetLastError());
+    const uint32_t ub = read1(used.p);
+    if (sampleChars) poolDensity = std::max(1.0 / 32, 1.15 * (double)ub * kPoolB / (double)sampleChars);
+  }
   float counter_kernel_ms = 0;
   bool keptT = false;  // rank2head written by the last merge
   uint32_t windows = 0, crossings = 0;
