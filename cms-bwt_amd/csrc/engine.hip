@@ -197,7 +197,9 @@ int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path
   std::string out = a->outname;
   std::ofstream log(out + ".log");
   cmsbwt_ctx* ctx = nullptr;
+  auto tc0 = std::chrono::steady_clock::now();
   int rc = cmsbwt_ctx_create(a->device, &ctx);
+  const double tCtx = std::chrono::duration<double>(std::chrono::steady_clock::now() - tc0).count();
   if (rc) {
     log << "HIP device " << a->device << " unavailable\n";
     return rc;
@@ -245,11 +247,14 @@ int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path
   if (rc) { log << ctx->err << "\n"; cmsbwt_ctx_destroy(ctx); return rc; }
   log << "MS-walk kernel: " << s.ms_walk_kernel_ms << " ms; collection pass: " << ms(t1, now()) << " ms\n";
   if (stats_out) *stats_out = e.stats;
+  auto td0 = now();
+  if (a->verbose) fprintf(stderr, "context %.3fs ", tCtx);
   if (a->verbose)
-    fprintf(stderr, "index %.3fs (sa %.3fs, tables %.3fs) upload %.3fs walk %.3fs (kernel %.2fms) merge %.3fs write %.3fs runs %llu\n",
+    fprintf(stderr, "index %.3fs (sa %.3fs, tables %.3fs) upload %.3fs walk %.3fs (kernel %.2fms) merge %.3fs write %.3fs runs %llu ",
             s.t_index_s, e.hix.t_sa, e.hix.t_lcp, s.t_upload_s, s.t_ms_walk_s, s.ms_walk_kernel_ms, s.t_merge_s, s.t_write_s,
             (unsigned long long)s.runs);
   cmsbwt_ctx_destroy(ctx);
+  if (a->verbose) fprintf(stderr, "teardown %.3fs\n", std::chrono::duration<double>(now() - td0).count());
   return CMSBWT_OK;
 }
 
