@@ -87,6 +87,8 @@ struct DevAlloc {
     if (it != freeBlocks.end() && it->first <= bytes + bytes / 4 + (4u << 20)) {
       void* p = it->second;
       cached -= it->first;
+      live += it->first;
+      peak = std::max(peak, live);
       freeBlocks.erase(it);
       return p;
     }
@@ -94,14 +96,22 @@ struct DevAlloc {
     if (hipMalloc(&p, bytes) != hipSuccess) {
       (void)hipGetLastError();
       trim();
-      HIPCHK(hipMalloc(&p, bytes));
+      if (hipMalloc(&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        throw HipError{"device out of memory: request " + std::to_string(bytes >> 20) + " MiB with " +
+                       std::to_string(live >> 20) + " MiB live (peak " + std::to_string(peak >> 20) + " MiB)"};
+      }
     }
     sizes[p] = bytes;
+    live += bytes;
+    peak = std::max(peak, live);
     return p;
   }
+  uint64_t live = 0, peak = 0;  // bytes handed out by get() and not yet put() back
   void put(void* p) {
     auto s = sizes.find(p);
     if (s == sizes.end()) { (void)hipFree(p); return; }
+    live -= s->second;
     freeBlocks.emplace(s->second, p);
     cached += s->second;
     if (cached > limit) trim();
