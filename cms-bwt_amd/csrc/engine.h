@@ -1041,15 +1041,29 @@ struct Engine {
     docEnd.alloc(ndocs);
     launch_end_phrases(dtext.p, ddoc.p, (uint32_t)ndocs, plan.dLast.p, chunkCount.p, chunkBase.p, R.n, h, docEnd.p,
                        hDoc.p, st);
-    diff.alloc((uint64_t)R.n + 1);
-    diff.zero(st);
-    hasHead.alloc(R.n);
-    hasHead.zero(st);
     DBuf<uint32_t> errf;
     errf.alloc(1);
     errf.zero(st);
-    launch_finalize(R, h, H, docEnd.p, (uint32_t)ndocs, dtext.p, ddoc.p, diff.p, hasHead.p, errf.p, hDoc.p, st);
+    launch_finalize(R, h, H, docEnd.p, (uint32_t)ndocs, dtext.p, ddoc.p, errf.p, hDoc.p, st);
     HIPCHK(hipGetLastError());
+    // run buckets (diff, hasHead) through position bins, no random atomics
+    diff.alloc((uint64_t)R.n + 1);
+    hasHead.alloc(R.n);
+    {
+      const uint32_t nb = (R.n >> kRunBinShift) + 1;
+      DBuf<uint32_t> binCnt, binOff, binCur, vals;
+      binCnt.alloc((uint64_t)nb + 1);
+      binCnt.zero(st);
+      binOff.alloc((uint64_t)nb + 1);
+      binCur.alloc(nb);
+      vals.alloc(2ull * H + 1);
+      launch_run_bin_count(h, H, R.n, nb, binCnt.p, st);
+      exscan(binCnt.p, binOff.p, 0u, (uint64_t)nb + 1);
+      HIPCHK(hipMemcpyAsync(binCur.p, binOff.p, (uint64_t)nb * 4, hipMemcpyDeviceToDevice, st));
+      launch_run_bin_scatter(h, H, R.n, nb, binCur.p, vals.p, st);
+      launch_run_bin_emit(vals.p, binOff.p, R.n, nb, diff.p, hasHead.p, st);
+      HIPCHK(hipGetLastError());
+    }
     uint32_t ef = read1(errf.p);
     orderInvariant = (ef & 8u) == 0;
     if (ef & 1) throw InputError{CMSBWT_EINPUT, "internal: match ends not monotone inside a document"};

@@ -54,8 +54,18 @@ void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t nd
                         const unsigned long long* chunkBase, uint32_t n, const HeadsSoA& h, uint32_t* docEndIdx,
                         uint32_t* hdoc, hipStream_t st);
 void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint32_t* docEndIdx,
-                     uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, int32_t* diff, uint8_t* hasHead,
-                     uint32_t* errFlags, const uint32_t* hdoc, hipStream_t st);
+                     uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, uint32_t* errFlags,
+                     const uint32_t* hdoc, hipStream_t st);
+// run buckets: diff[0..n] and hasHead[0..n) from the heads' runs, through
+// nb = (n >> kRunBinShift) + 1 bins (count into zeroed binCnt[nb+1]; scatter
+// with binCur = exclusive prefix of the counts; emit with binOff = that prefix)
+constexpr uint32_t kRunBinShift = 13;
+constexpr uint32_t kRunBinLdsMax = 16384;
+void launch_run_bin_count(const HeadsSoA& h, uint32_t H, uint32_t n, uint32_t nb, uint32_t* binCnt, hipStream_t st);
+void launch_run_bin_scatter(const HeadsSoA& h, uint32_t H, uint32_t n, uint32_t nb, uint32_t* binCur,
+                            uint32_t* vals, hipStream_t st);
+void launch_run_bin_emit(const uint32_t* vals, const uint32_t* binOff, uint32_t n, uint32_t nb, int32_t* diff,
+                         uint8_t* hasHead, hipStream_t st);
 
 // coll_read.hip: the collection reader on the device (getline semantics of
 // FN:1138-1275 without -p) over raw file bytes in HBM, tiles of kRdTile bytes.

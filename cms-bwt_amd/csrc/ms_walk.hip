@@ -18,6 +18,8 @@
 //   * the singleton-interval extension compares 8 bytes per step (LCE).
 // Per-position bucket updates become one run (pos, length) per head, turned
 // into counts by a difference array (no per-character atomics).
+#include <algorithm>
+
 #include "device_common.h"
 #include "kernels.h"
 
@@ -331,7 +333,6 @@ __global__ void k_end_phrases(const uint8_t* __restrict__ text, const uint64_t* 
 // replaces the per-position bucket increments.
 __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __restrict__ docEndIdx,
                            uint32_t ndocs, const uint8_t* __restrict__ text, const uint64_t* __restrict__ docOff,
-                           int32_t* __restrict__ diff, uint8_t* __restrict__ hasHead,
                            uint32_t* __restrict__ errFlags, const uint32_t* __restrict__ hdoc) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= H) return;
@@ -340,9 +341,6 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
     h.isa[i] = 0;
     h.tonext[i] = 0;
     h.nexthead[i] = 0;
-    atomicAdd(&diff[R.n - 1], 1);  // bucket[n-1]-- per document (FN:1203)
-    atomicSub(&diff[R.n], 1);
-    hasHead[R.n - 1] = 1;
     return;
   }
   const uint32_t lo = hdoc[i];  // document of i (written by the scatter)
@@ -378,12 +376,94 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
     if (!(c == R.x[q] || (c == kSep && q == R.n - 1))) atomicOr(errFlags, 8u);
   }
   h.nexthead[i] = (uint16_t)(j - i);
-  const uint32_t p = h.pos[i];
-  const uint64_t endp = (uint64_t)p + (s1 - si);
-  if (endp > R.n) { atomicOr(errFlags, 4u); return; }
-  atomicAdd(&diff[p], 1);
-  atomicSub(&diff[endp], 1);
-  hasHead[p] = 1;
+  if ((uint64_t)h.pos[i] + (s1 - si) > R.n) atomicOr(errFlags, 4u);
+}
+
+// ------------------------------------------------------------ run buckets (FN:1162-1171, 1203)
+// Every head i covers the reference positions [pos_i, pos_i + start_{i+1} -
+// start_i) with one bucket increment each; an end phrase covers [n-1, n).
+// diff = (#runs starting at p) - (#runs ending at p) and hasHead[p] = (#runs
+// starting at p) > 0.  Instead of two random device-scope atomics and a random
+// byte store per head, the run endpoints (pos << 1 | isEnd) are scattered into
+// bins of 2^kRunBinShift positions (count, scan, scatter) and every bin is
+// counted in LDS and written out coalesced.
+__device__ __forceinline__ bool run_of(const HeadsSoA& h, uint32_t i, uint32_t n, uint32_t& p, uint32_t& e) {
+  if (h.len[i] == 0) { p = n - 1; e = n; return true; }
+  p = h.pos[i];
+  const uint64_t endp = (uint64_t)p + (h.start[i + 1] - h.start[i]);
+  if (endp > n) return false;  // flagged by k_finalize (errFlags 4)
+  e = (uint32_t)endp;
+  return true;
+}
+
+template <bool kLds>
+__global__ void k_run_bin_count(HeadsSoA h, uint32_t H, uint32_t n, uint32_t nb, uint32_t* __restrict__ binCnt) {
+  extern __shared__ uint32_t sh[];
+  if (kLds) {
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) sh[j] = 0;
+    __syncthreads();
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < H; i += gridDim.x * blockDim.x) {
+    uint32_t p, e;
+    if (!run_of(h, i, n, p, e)) continue;
+    atomicAdd(kLds ? &sh[p >> kRunBinShift] : &binCnt[p >> kRunBinShift], 1u);
+    atomicAdd(kLds ? &sh[e >> kRunBinShift] : &binCnt[e >> kRunBinShift], 1u);
+  }
+  if (kLds) {
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x)
+      if (sh[j]) atomicAdd(&binCnt[j], sh[j]);
+  }
+}
+
+// binCur = exclusive prefix of the counts on entry; each block visits the same
+// heads as in k_run_bin_count's launch (same grid), reserves its share of every
+// bin once, then places its endpoints through LDS cursors.
+template <bool kLds>
+__global__ void k_run_bin_scatter(HeadsSoA h, uint32_t H, uint32_t n, uint32_t nb, uint32_t* __restrict__ binCur,
+                                  uint32_t* __restrict__ vals) {
+  extern __shared__ uint32_t sh[];
+  if (kLds) {
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) sh[j] = 0;
+    __syncthreads();
+    for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < H; i += gridDim.x * blockDim.x) {
+      uint32_t p, e;
+      if (!run_of(h, i, n, p, e)) continue;
+      atomicAdd(&sh[p >> kRunBinShift], 1u);
+      atomicAdd(&sh[e >> kRunBinShift], 1u);
+    }
+    __syncthreads();
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x)
+      if (sh[j]) sh[j] = atomicAdd(&binCur[j], sh[j]);
+    __syncthreads();
+  }
+  for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < H; i += gridDim.x * blockDim.x) {
+    uint32_t p, e;
+    if (!run_of(h, i, n, p, e)) continue;
+    vals[atomicAdd(kLds ? &sh[p >> kRunBinShift] : &binCur[p >> kRunBinShift], 1u)] = p << 1;
+    vals[atomicAdd(kLds ? &sh[e >> kRunBinShift] : &binCur[e >> kRunBinShift], 1u)] = e << 1 | 1u;
+  }
+}
+
+__global__ __launch_bounds__(1024) void k_run_bin_emit(const uint32_t* __restrict__ vals,
+                                                       const uint32_t* __restrict__ binOff, uint32_t n,
+                                                       int32_t* __restrict__ diff, uint8_t* __restrict__ hasHead) {
+  constexpr uint32_t W = 1u << kRunBinShift;
+  __shared__ uint32_t cs[W], ce[W];
+  for (uint32_t j = threadIdx.x; j < W; j += blockDim.x) cs[j] = ce[j] = 0;
+  __syncthreads();
+  const uint32_t b = blockIdx.x, k1 = binOff[b + 1];
+  for (uint32_t k = binOff[b] + threadIdx.x; k < k1; k += blockDim.x) {
+    const uint32_t v = vals[k], j = (v >> 1) & (W - 1);
+    atomicAdd((v & 1u) ? &ce[j] : &cs[j], 1u);
+  }
+  __syncthreads();
+  const uint64_t base = (uint64_t)b << kRunBinShift;
+  for (uint32_t j = threadIdx.x; j < W; j += blockDim.x) {
+    const uint64_t q = base + j;
+    if (q <= n) diff[q] = (int32_t)(cs[j] - ce[j]);
+    if (q < n) hasHead[q] = cs[j] != 0;
+  }
 }
 
 // ------------------------------------------------------------ host launchers
@@ -419,11 +499,38 @@ void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t nd
 }
 
 void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint32_t* docEndIdx,
-                     uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, int32_t* diff, uint8_t* hasHead,
-                     uint32_t* errFlags, const uint32_t* hdoc, hipStream_t st) {
+                     uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, uint32_t* errFlags,
+                     const uint32_t* hdoc, hipStream_t st) {
   if (!H) return;
   hipLaunchKernelGGL(k_finalize, dim3((H + 255) / 256), dim3(256), 0, st, R, h, H, docEndIdx, ndocs, text, docOff,
-                     diff, hasHead, errFlags, hdoc);
+                     errFlags, hdoc);
+}
+
+static unsigned run_bin_grid(uint32_t H) { return std::max(1u, std::min((H + 255) / 256, 1024u)); }
+
+void launch_run_bin_count(const HeadsSoA& h, uint32_t H, uint32_t n, uint32_t nb, uint32_t* binCnt,
+                          hipStream_t st) {
+  if (!H) return;
+  if (nb <= kRunBinLdsMax)
+    hipLaunchKernelGGL(k_run_bin_count<true>, dim3(run_bin_grid(H)), dim3(256), nb * 4, st, h, H, n, nb, binCnt);
+  else
+    hipLaunchKernelGGL(k_run_bin_count<false>, dim3(run_bin_grid(H)), dim3(256), 0, st, h, H, n, nb, binCnt);
+}
+
+void launch_run_bin_scatter(const HeadsSoA& h, uint32_t H, uint32_t n, uint32_t nb, uint32_t* binCur,
+                            uint32_t* vals, hipStream_t st) {
+  if (!H) return;
+  if (nb <= kRunBinLdsMax)
+    hipLaunchKernelGGL(k_run_bin_scatter<true>, dim3(run_bin_grid(H)), dim3(256), nb * 4, st, h, H, n, nb, binCur,
+                       vals);
+  else
+    hipLaunchKernelGGL(k_run_bin_scatter<false>, dim3(run_bin_grid(H)), dim3(256), 0, st, h, H, n, nb, binCur,
+                       vals);
+}
+
+void launch_run_bin_emit(const uint32_t* vals, const uint32_t* binOff, uint32_t n, uint32_t nb, int32_t* diff,
+                         uint8_t* hasHead, hipStream_t st) {
+  if (nb) hipLaunchKernelGGL(k_run_bin_emit, dim3(nb), dim3(1024), 0, st, vals, binOff, n, diff, hasHead);
 }
 
 }  // namespace cmsbwt
