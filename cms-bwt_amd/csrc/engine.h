@@ -1050,18 +1050,22 @@ struct Engine {
     diff.alloc((uint64_t)R.n + 1);
     hasHead.alloc(R.n);
     {
-      const uint32_t nb = (R.n >> kRunBinShift) + 1;
+      // CMSBWT_RUN_BIN_SHIFT / CMSBWT_RUN_BIN_GLOBAL: smaller bins and the
+      // global-counter path, for the tests
+      const uint32_t sh = std::max(1u, std::min(kRunBinShift, env_u32("CMSBWT_RUN_BIN_SHIFT", kRunBinShift)));
+      const bool global = env_u32("CMSBWT_RUN_BIN_GLOBAL", 0) != 0;
+      const uint32_t nb = (R.n >> sh) + 1;
       DBuf<uint32_t> binCnt, binOff, binCur, vals;
       binCnt.alloc((uint64_t)nb + 1);
       binCnt.zero(st);
       binOff.alloc((uint64_t)nb + 1);
       binCur.alloc(nb);
       vals.alloc(2ull * H + 1);
-      launch_run_bin_count(h, H, R.n, nb, binCnt.p, st);
+      launch_run_bin_count(h, H, R.n, nb, sh, global, binCnt.p, st);
       exscan(binCnt.p, binOff.p, 0u, (uint64_t)nb + 1);
       HIPCHK(hipMemcpyAsync(binCur.p, binOff.p, (uint64_t)nb * 4, hipMemcpyDeviceToDevice, st));
-      launch_run_bin_scatter(h, H, R.n, nb, binCur.p, vals.p, st);
-      launch_run_bin_emit(vals.p, binOff.p, R.n, nb, diff.p, hasHead.p, st);
+      launch_run_bin_scatter(h, H, R.n, nb, sh, global, binCur.p, vals.p, st);
+      launch_run_bin_emit(vals.p, binOff.p, R.n, nb, sh, diff.p, hasHead.p, st);
       HIPCHK(hipGetLastError());
     }
     uint32_t ef = read1(errf.p);

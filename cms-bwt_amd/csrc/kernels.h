@@ -57,15 +57,18 @@ void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint3
                      uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, uint32_t* errFlags,
                      const uint32_t* hdoc, hipStream_t st);
 // run buckets: diff[0..n] and hasHead[0..n) from the heads' runs, through
-// nb = (n >> kRunBinShift) + 1 bins (count into zeroed binCnt[nb+1]; scatter
-// with binCur = exclusive prefix of the counts; emit with binOff = that prefix)
+// nb = (n >> sh) + 1 bins of 2^sh positions, sh <= kRunBinShift (count into
+// zeroed binCnt[nb+1]; scatter with binCur = exclusive prefix of the counts;
+// emit with binOff = that prefix).  Bin counters live in LDS up to
+// kRunBinLdsMax bins, in global memory beyond (or when `global`).
 constexpr uint32_t kRunBinShift = 13;
 constexpr uint32_t kRunBinLdsMax = 16384;
-void launch_run_bin_count(const HeadsSoA& h, uint32_t H, uint32_t n, uint32_t nb, uint32_t* binCnt, hipStream_t st);
-void launch_run_bin_scatter(const HeadsSoA& h, uint32_t H, uint32_t n, uint32_t nb, uint32_t* binCur,
-                            uint32_t* vals, hipStream_t st);
-void launch_run_bin_emit(const uint32_t* vals, const uint32_t* binOff, uint32_t n, uint32_t nb, int32_t* diff,
-                         uint8_t* hasHead, hipStream_t st);
+void launch_run_bin_count(const HeadsSoA& h, uint32_t H, uint32_t n, uint32_t nb, uint32_t sh, bool global,
+                          uint32_t* binCnt, hipStream_t st);
+void launch_run_bin_scatter(const HeadsSoA& h, uint32_t H, uint32_t n, uint32_t nb, uint32_t sh, bool global,
+                            uint32_t* binCur, uint32_t* vals, hipStream_t st);
+void launch_run_bin_emit(const uint32_t* vals, const uint32_t* binOff, uint32_t n, uint32_t nb, uint32_t sh,
+                         int32_t* diff, uint8_t* hasHead, hipStream_t st);
 
 // coll_read.hip: the collection reader on the device (getline semantics of
 // FN:1138-1275 without -p) over raw file bytes in HBM, tiles of kRdTile bytes.

@@ -387,6 +387,7 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
 // byte store per head, the run endpoints (pos << 1 | isEnd) are scattered into
 // bins of 2^kRunBinShift positions (count, scan, scatter) and every bin is
 // counted in LDS and written out coalesced.
+// bins are 2^sh positions, sh <= kRunBinShift (smaller only to test bin edges)
 __device__ __forceinline__ bool run_of(const HeadsSoA& h, uint32_t i, uint32_t n, uint32_t& p, uint32_t& e) {
   if (h.len[i] == 0) { p = n - 1; e = n; return true; }
   p = h.pos[i];
@@ -397,22 +398,23 @@ __device__ __forceinline__ bool run_of(const HeadsSoA& h, uint32_t i, uint32_t n
 }
 
 template <bool kLds>
-__global__ void k_run_bin_count(HeadsSoA h, uint32_t H, uint32_t n, uint32_t nb, uint32_t* __restrict__ binCnt) {
-  extern __shared__ uint32_t sh[];
+__global__ void k_run_bin_count(HeadsSoA h, uint32_t H, uint32_t n, uint32_t nb, uint32_t sh,
+                                uint32_t* __restrict__ binCnt) {
+  extern __shared__ uint32_t lds[];
   if (kLds) {
-    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) sh[j] = 0;
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) lds[j] = 0;
     __syncthreads();
   }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < H; i += gridDim.x * blockDim.x) {
     uint32_t p, e;
     if (!run_of(h, i, n, p, e)) continue;
-    atomicAdd(kLds ? &sh[p >> kRunBinShift] : &binCnt[p >> kRunBinShift], 1u);
-    atomicAdd(kLds ? &sh[e >> kRunBinShift] : &binCnt[e >> kRunBinShift], 1u);
+    atomicAdd(kLds ? &lds[p >> sh] : &binCnt[p >> sh], 1u);
+    atomicAdd(kLds ? &lds[e >> sh] : &binCnt[e >> sh], 1u);
   }
   if (kLds) {
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x)
-      if (sh[j]) atomicAdd(&binCnt[j], sh[j]);
+      if (lds[j]) atomicAdd(&binCnt[j], lds[j]);
   }
 }
 
@@ -420,36 +422,38 @@ __global__ void k_run_bin_count(HeadsSoA h, uint32_t H, uint32_t n, uint32_t nb,
 // heads as in k_run_bin_count's launch (same grid), reserves its share of every
 // bin once, then places its endpoints through LDS cursors.
 template <bool kLds>
-__global__ void k_run_bin_scatter(HeadsSoA h, uint32_t H, uint32_t n, uint32_t nb, uint32_t* __restrict__ binCur,
-                                  uint32_t* __restrict__ vals) {
-  extern __shared__ uint32_t sh[];
+__global__ void k_run_bin_scatter(HeadsSoA h, uint32_t H, uint32_t n, uint32_t nb, uint32_t sh,
+                                  uint32_t* __restrict__ binCur, uint32_t* __restrict__ vals) {
+  extern __shared__ uint32_t lds[];
   if (kLds) {
-    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) sh[j] = 0;
+    for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x) lds[j] = 0;
     __syncthreads();
     for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < H; i += gridDim.x * blockDim.x) {
       uint32_t p, e;
       if (!run_of(h, i, n, p, e)) continue;
-      atomicAdd(&sh[p >> kRunBinShift], 1u);
-      atomicAdd(&sh[e >> kRunBinShift], 1u);
+      atomicAdd(&lds[p >> sh], 1u);
+      atomicAdd(&lds[e >> sh], 1u);
     }
     __syncthreads();
     for (uint32_t j = threadIdx.x; j < nb; j += blockDim.x)
-      if (sh[j]) sh[j] = atomicAdd(&binCur[j], sh[j]);
+      if (lds[j]) lds[j] = atomicAdd(&binCur[j], lds[j]);
     __syncthreads();
   }
   for (uint32_t i = blockIdx.x * blockDim.x + threadIdx.x; i < H; i += gridDim.x * blockDim.x) {
     uint32_t p, e;
     if (!run_of(h, i, n, p, e)) continue;
-    vals[atomicAdd(kLds ? &sh[p >> kRunBinShift] : &binCur[p >> kRunBinShift], 1u)] = p << 1;
-    vals[atomicAdd(kLds ? &sh[e >> kRunBinShift] : &binCur[e >> kRunBinShift], 1u)] = e << 1 | 1u;
+    vals[atomicAdd(kLds ? &lds[p >> sh] : &binCur[p >> sh], 1u)] = p << 1;
+    vals[atomicAdd(kLds ? &lds[e >> sh] : &binCur[e >> sh], 1u)] = e << 1 | 1u;
   }
 }
 
 __global__ __launch_bounds__(1024) void k_run_bin_emit(const uint32_t* __restrict__ vals,
                                                        const uint32_t* __restrict__ binOff, uint32_t n,
-                                                       int32_t* __restrict__ diff, uint8_t* __restrict__ hasHead) {
-  constexpr uint32_t W = 1u << kRunBinShift;
-  __shared__ uint32_t cs[W], ce[W];
+                                                       uint32_t sh, int32_t* __restrict__ diff,
+                                                       uint8_t* __restrict__ hasHead) {
+  constexpr uint32_t kW = 1u << kRunBinShift;
+  __shared__ uint32_t cs[kW], ce[kW];
+  const uint32_t W = 1u << sh;
   for (uint32_t j = threadIdx.x; j < W; j += blockDim.x) cs[j] = ce[j] = 0;
   __syncthreads();
   const uint32_t b = blockIdx.x, k1 = binOff[b + 1];
@@ -458,7 +462,7 @@ __global__ __launch_bounds__(1024) void k_run_bin_emit(const uint32_t* __restric
     atomicAdd((v & 1u) ? &ce[j] : &cs[j], 1u);
   }
   __syncthreads();
-  const uint64_t base = (uint64_t)b << kRunBinShift;
+  const uint64_t base = (uint64_t)b << sh;
   for (uint32_t j = threadIdx.x; j < W; j += blockDim.x) {
     const uint64_t q = base + j;
     if (q <= n) diff[q] = (int32_t)(cs[j] - ce[j]);
@@ -508,29 +512,29 @@ void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint3
 
 static unsigned run_bin_grid(uint32_t H) { return std::max(1u, std::min((H + 255) / 256, 1024u)); }
 
-void launch_run_bin_count(const HeadsSoA& h, uint32_t H, uint32_t n, uint32_t nb, uint32_t* binCnt,
-                          hipStream_t st) {
+void launch_run_bin_count(const HeadsSoA& h, uint32_t H, uint32_t n, uint32_t nb, uint32_t sh, bool global,
+                          uint32_t* binCnt, hipStream_t st) {
   if (!H) return;
-  if (nb <= kRunBinLdsMax)
-    hipLaunchKernelGGL(k_run_bin_count<true>, dim3(run_bin_grid(H)), dim3(256), nb * 4, st, h, H, n, nb, binCnt);
+  if (nb <= kRunBinLdsMax && !global)
+    hipLaunchKernelGGL(k_run_bin_count<true>, dim3(run_bin_grid(H)), dim3(256), nb * 4, st, h, H, n, nb, sh, binCnt);
   else
-    hipLaunchKernelGGL(k_run_bin_count<false>, dim3(run_bin_grid(H)), dim3(256), 0, st, h, H, n, nb, binCnt);
+    hipLaunchKernelGGL(k_run_bin_count<false>, dim3(run_bin_grid(H)), dim3(256), 0, st, h, H, n, nb, sh, binCnt);
 }
 
-void launch_run_bin_scatter(const HeadsSoA& h, uint32_t H, uint32_t n, uint32_t nb, uint32_t* binCur,
-                            uint32_t* vals, hipStream_t st) {
+void launch_run_bin_scatter(const HeadsSoA& h, uint32_t H, uint32_t n, uint32_t nb, uint32_t sh, bool global,
+                            uint32_t* binCur, uint32_t* vals, hipStream_t st) {
   if (!H) return;
-  if (nb <= kRunBinLdsMax)
-    hipLaunchKernelGGL(k_run_bin_scatter<true>, dim3(run_bin_grid(H)), dim3(256), nb * 4, st, h, H, n, nb, binCur,
-                       vals);
+  if (nb <= kRunBinLdsMax && !global)
+    hipLaunchKernelGGL(k_run_bin_scatter<true>, dim3(run_bin_grid(H)), dim3(256), nb * 4, st, h, H, n, nb, sh,
+                       binCur, vals);
   else
-    hipLaunchKernelGGL(k_run_bin_scatter<false>, dim3(run_bin_grid(H)), dim3(256), 0, st, h, H, n, nb, binCur,
+    hipLaunchKernelGGL(k_run_bin_scatter<false>, dim3(run_bin_grid(H)), dim3(256), 0, st, h, H, n, nb, sh, binCur,
                        vals);
 }
 
-void launch_run_bin_emit(const uint32_t* vals, const uint32_t* binOff, uint32_t n, uint32_t nb, int32_t* diff,
-                         uint8_t* hasHead, hipStream_t st) {
-  if (nb) hipLaunchKernelGGL(k_run_bin_emit, dim3(nb), dim3(1024), 0, st, vals, binOff, n, diff, hasHead);
+void launch_run_bin_emit(const uint32_t* vals, const uint32_t* binOff, uint32_t n, uint32_t nb, uint32_t sh,
+                         int32_t* diff, uint8_t* hasHead, hipStream_t st) {
+  if (nb) hipLaunchKernelGGL(k_run_bin_emit, dim3(nb), dim3(1024), 0, st, vals, binOff, n, sh, diff, hasHead);
 }
 
 }  // namespace cmsbwt

@@ -103,6 +103,18 @@ def test_doubling_group_paths(engine, oracle, tmp_path, case, small):
     _compare(engine, oracle, tmp_path, case, env={"CMSBWT_DBL_SMALL": small})
 
 
+@pytest.mark.parametrize("geom", [{"CMSBWT_RUN_BIN_SHIFT": "3"},
+                                  {"CMSBWT_RUN_BIN_SHIFT": "5", "CMSBWT_RUN_BIN_GLOBAL": "1"},
+                                  {"CMSBWT_RUN_BIN_GLOBAL": "1"}],
+                         ids=["bins8_lds", "bins32_global", "bins8192_global"])
+@pytest.mark.parametrize("case", cases.small_cases(), ids=lambda c: c[0])
+def test_run_bucket_bins(engine, oracle, tmp_path, case, geom):
+    """Run buckets (FN:1162-1171, 1203) through position bins: many small bins
+    (runs crossing bin edges, endpoints at n) and the global-counter path used
+    above kRunBinLdsMax bins give the oracle's bucket array and output."""
+    _compare(engine, oracle, tmp_path, case, env=geom)
+
+
 @pytest.mark.parametrize("case", cases.large_cases(), ids=lambda c: c[0])
 def test_large_reference_path(engine, oracle, tmp_path, case):
     _compare(engine, oracle, tmp_path, case, rle=True)
@@ -276,3 +288,10 @@ def test_writer_streams_both_formats(engine, tmp_path, threads, chunk_mb):
         for k in env:
             os.environ.pop(k, None)
     assert os.path.getsize(pre + "_gpu.bwt") == g["bwt_bytes"]
+
+
+@pytest.mark.parametrize("case", cases.large_cases(), ids=lambda c: c[0])
+def test_large_reference_run_bins_beyond_lds(engine, oracle, tmp_path, case):
+    """1 M reference with 32-position bins: 31k bins exceed kRunBinLdsMax, so
+    the bin counters take the global path on their own."""
+    _compare(engine, oracle, tmp_path, case, rle=True, env={"CMSBWT_RUN_BIN_SHIFT": "5"})
