@@ -1453,7 +1453,11 @@ struct Engine {
     DBuf<uint32_t> nhr;
     nhr.alloc(H);
     {
-      mk_nhr_slot(Pm.p, headRank.p, hNext.p, H, nhr.p, st);
+      {
+        DBuf<uint32_t> nbi;
+        nbi.alloc(H);
+        mk_nhr_slot(Pm.p, headRank.p, hNext.p, H, nbi.p, nhr.p, st);
+      }
       sort_nhr_items(S, K, itemOfSlot.p, nhr.p, H);
     }
     headRank.release();

@@ -413,13 +413,20 @@ __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ ite
   // unresolved members (items with >= 2 heads): their sa positions
   actv[s] = it.count[q] >= 2 ? g + m : 0xffffffffu;
 }
-// next-head rank of each member, in slot order (FN:1480-1494)
-__global__ void k_nhr_slot(const uint32_t* __restrict__ Pm, const uint32_t* __restrict__ headRank,
-                           const uint16_t* __restrict__ nexthead, uint32_t H, uint32_t* __restrict__ nhr) {
+// next-head rank of each member, in slot order (FN:1480-1494): first per head
+// in document order (nexthead is small, so headRank[idx + nexthead] is read
+// almost sequentially), then one gather through the slot permutation
+__global__ void k_nhr_idx(const uint32_t* __restrict__ headRank, const uint16_t* __restrict__ nexthead, uint32_t H,
+                          uint32_t* __restrict__ nbi) {
+  uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= H) return;
+  nbi[idx] = headRank[idx + nexthead[idx]];
+}
+__global__ void k_nhr_slot(const uint32_t* __restrict__ Pm, const uint32_t* __restrict__ nbi, uint32_t H,
+                           uint32_t* __restrict__ nhr) {
   uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= H) return;
-  const uint32_t idx = Pm[s];
-  nhr[s] = headRank[idx + nexthead[idx]];
+  nhr[s] = nbi[Pm[s]];
 }
 // Sort each item's nhr segment: insertion sort in place for <= kSmallSeg
 // members; larger items are appended to a list (bigList[0] = their number)
@@ -1036,9 +1043,11 @@ void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_
     hipLaunchKernelGGL(k_ranks_slot, g1(H), dim3(256), 0, st, it, itemOfSlot, Pm, H, rankBase, gBase, n, T, sa, grp,
                        actv);
 }
-void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, const uint16_t* nexthead, uint32_t H, uint32_t* nhr,
-                 hipStream_t st) {
-  if (H) hipLaunchKernelGGL(k_nhr_slot, g1(H), dim3(256), 0, st, Pm, headRank, nexthead, H, nhr);
+void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, const uint16_t* nexthead, uint32_t H, uint32_t* nbi,
+                 uint32_t* nhr, hipStream_t st) {
+  if (!H) return;
+  hipLaunchKernelGGL(k_nhr_idx, g1(H), dim3(256), 0, st, headRank, nexthead, H, nbi);
+  hipLaunchKernelGGL(k_nhr_slot, g1(H), dim3(256), 0, st, Pm, nbi, H, nhr);
 }
 void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigList, hipStream_t st) {
   if (K) hipLaunchKernelGGL(k_nhr_sort_small, g1(K), dim3(256), 0, st, it, K, nhr, bigList);

@@ -46,8 +46,9 @@ void mk_pos_rank_base(const uint32_t* posBegin, const uint32_t* slot, const uint
 void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
                    const uint32_t* rankBase, const uint32_t* gBase, uint32_t n, int32_t* T, uint32_t* sa,
                    uint32_t* grp, uint32_t* actv, hipStream_t st);
-void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, const uint16_t* nexthead, uint32_t H, uint32_t* nhr,
-                 hipStream_t st);
+// nbi: H scratch words (next-head rank per head in document order)
+void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, const uint16_t* nexthead, uint32_t H, uint32_t* nbi,
+                 uint32_t* nhr, hipStream_t st);
 void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigList, hipStream_t st);
 void mk_nhr_big_fill(const uint32_t* items, const uint32_t* off, uint32_t nb, const ItemsSoA& it, const uint32_t* nhr,
                      unsigned long long* key, uint32_t* slots, hipStream_t st);
