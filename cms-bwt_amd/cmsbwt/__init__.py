@@ -32,6 +32,7 @@ CMSBWT_EINPUT = 3
 CMSBWT_EDEVICE = 4
 CMSBWT_ELIMIT = 5
 CMSBWT_EORDER = 6
+CMSBWT_EINTERNAL = 7
 UINT64_MAX = (1 << 64) - 1
 
 ARRAYS = {  # name -> numpy dtype, as dumped by the oracle

@@ -88,6 +88,11 @@ def gather_walk(local: dict, meta, device, root: int = 0):
     if ops:
         for req in dist.batch_isend_irecv(ops):
             req.wait()
+    # RCCL collectives and the root's slice copy are ordered on torch's current
+    # stream only; the engine reads the tensors from its own stream, so the
+    # host waits for them here (as Transport.sync does in the sharded merge).
+    if torch.device(device).type == "cuda":
+        torch.cuda.synchronize(device)
     return combined, totals
 
 

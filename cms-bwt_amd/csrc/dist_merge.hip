@@ -60,6 +60,8 @@ void Engine::dm_begin(uint32_t world, uint32_t rank, uint64_t heads_total, uint6
   if (!walked) throw InputError{CMSBWT_EARG, "run ms_walk first"};
   if (world < 1 || world > 64 || rank >= world) throw InputError{CMSBWT_EARG, "bad world/rank"};
   if (heads_total >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^31-1 heads (int32 ranks, FN:1436)"};
+  if (heads_total == 0)  // as Engine::merge: FN:1359-1385 is undefined without heads
+    throw InputError{CMSBWT_EINPUT, "collection has no documents (reference behaviour undefined, FN:1359-1385)"};
   if (!diffAll || !hashead) throw InputError{CMSBWT_EARG, "reduced diff/hashead arrays required"};
   const uint32_t n = R.n;
   merged = false;

@@ -961,6 +961,29 @@ struct Engine {
     walked = merged = false;
     ndocs = hdoc.size() - 1;  // walk_import may have replaced these with merged totals
     chars = collChars;
+    if (ndocs == 0) {
+      // No document (an empty file, or one unterminated line that getline().good()
+      // drops, FN:1138): no heads and no runs.  A rank of a sharded run may own
+      // no documents; a merge over zero heads in total is rejected in merge().
+      H = 0;
+      hStart.alloc(0); hPos.alloc(0); hLen.alloc(0); hIsa.alloc(0); hTonext.alloc(0);
+      hSmall.alloc(0); hChar.alloc(0); hNext.alloc(0);
+      diff.alloc((uint64_t)R.n + 1);
+      diff.zero(st);
+      hasHead.alloc(R.n);
+      hasHead.zero(st);
+      sync();
+      orderInvariant = true;
+      walked = true;
+      stats.order_invariant = 1;
+      stats.heads = 0;
+      stats.ndocs = 0;
+      stats.chars = chars;
+      stats.sn = sn;
+      stats.ms_walk_kernel_ms = 0;
+      stats.t_ms_walk_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+      return;
+    }
     const uint32_t C = chunk_size();
     if (!plan.valid || plan.C != C) build_plan(C);
     const uint32_t nch = plan.nch;
@@ -1321,6 +1344,9 @@ struct Engine {
 
   void merge(int rle) {
     if (!walked) throw InputError{CMSBWT_EARG, "run ms_walk first"};
+    // Zero heads: the j-scan's `phrasesVector.size() - 1` (FN:1359) wraps and
+    // FN:1385 writes phrasesVector[-1]; the reference's behaviour is undefined.
+    if (H == 0) throw InputError{CMSBWT_EINPUT, "collection has no documents (reference behaviour undefined, FN:1359-1385)"};
     auto t0 = std::chrono::steady_clock::now();
     dm.on = false;
     const uint32_t n = R.n;
@@ -1716,10 +1742,17 @@ struct Engine {
         });
       }
     } catch (...) {
+      // never leave new bytes over a previous run's tail: the reference's
+      // ofstream truncates, so a failed write leaves an empty file
+      if (ftruncate(fd, 0) != 0) (void)unlink(path.c_str());
       close(fd);
       throw;
     }
-    if (ftruncate(fd, (off_t)outBytes) != 0) { close(fd); throw InputError{CMSBWT_EIO, "cannot size " + path}; }
+    if (ftruncate(fd, (off_t)outBytes) != 0) {
+      (void)unlink(path.c_str());
+      close(fd);
+      throw InputError{CMSBWT_EIO, "cannot size " + path};
+    }
     if (close(fd) != 0) throw InputError{CMSBWT_EIO, "cannot close " + path};
     if (R.n < 1000000 && !dm.on) {  // FN:919-924 small-reference side output (single-GPU merge)
       std::vector<unsigned long long> c((uint64_t)H + 1);

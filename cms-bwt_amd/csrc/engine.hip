@@ -28,6 +28,12 @@ static int guard(cmsbwt_ctx* c, F&& f) {
   } catch (const std::bad_alloc&) {
     if (c) c->err = "host out of memory";
     return CMSBWT_ELIMIT;
+  } catch (const std::exception& ex) {  // std::system_error (threads), length_error, ...
+    if (c) c->err = std::string("internal error: ") + ex.what();
+    return CMSBWT_EINTERNAL;
+  } catch (...) {  // nothing may unwind through the C ABI
+    if (c) c->err = "internal error: unknown exception";
+    return CMSBWT_EINTERNAL;
   }
 }
 

@@ -27,6 +27,7 @@ extern "C" {
 #define CMSBWT_EDEVICE 4    /* HIP runtime error or HIP code object not loadable    */
 #define CMSBWT_ELIMIT 5     /* size limit (reference int32/uint32 limits)           */
 #define CMSBWT_EORDER 6     /* map comparator ambiguity (match.h:27-33) detected    */
+#define CMSBWT_EINTERNAL 7  /* unexpected host exception (thread creation, ...)     */
 
 /* utils.h:8-14 struct Args, plus engine knobs. */
 typedef struct cmsbwt_args {

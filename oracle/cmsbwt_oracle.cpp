@@ -496,6 +496,11 @@ struct Engine {
     if (!parse_collection(collFile)) { *log << error << "\n"; return false; }
     *log << "Finished parsing file of length: " << sn << "\n";
     const uint64_t H = V.size();
+    if (H == 0) {  // FN:1359 `size() - 1` wraps and FN:1385 writes V[-1]: undefined
+      error = "collection has no documents (reference behaviour undefined, FN:1359-1385)";
+      *log << error << "\n";
+      return false;
+    }
     if (!dumpdir.empty()) {
       std::vector<uint32_t> st(H);
       for (uint64_t i = 0; i < H; i++) st[i] = V[i].start;

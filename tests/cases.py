@@ -101,6 +101,17 @@ def small_cases():
     return cases
 
 
+def no_document_cases():
+    """Collections the reader turns into zero documents: an empty file and one
+    unterminated line (dropped by getline().good(), FN:1138).  With no heads the
+    reference's j-scan runs `size() - 1` wrapped and writes phrasesVector[-1]
+    (FN:1359-1385): undefined behaviour, rejected with CMSBWT_EINPUT here."""
+    rng = _rng(12)
+    ref = fasta([rand_dna(rng, 2000)])
+    return [("empty_file", ref, b"", UINT64_MAX),
+            ("single_unterminated_line", ref, rand_dna(rng, 300), UINT64_MAX)]
+
+
 def large_cases():
     """Large-reference path (_n >= 1e6, FN:1795)."""
     r, c = copies_case(9, 1_000_000, 3, 0.001)

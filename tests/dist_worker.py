@@ -11,10 +11,13 @@ sys.path.insert(0, os.path.join(ROOT, "cms-bwt_amd"))
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 
-def _init(rank, world, port):
+def _init(rank, world, port, backend="gloo"):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
-    dist.init_process_group("gloo", rank=rank, world_size=world)
+    if backend == "nccl":
+        import torch
+        torch.cuda.set_device(0)
+    dist.init_process_group(backend, rank=rank, world_size=world)
     return dist
 
 
@@ -71,6 +74,28 @@ def gpu_sharded(rank, world, port, work):
         cdist.gather_step(eng, "cpu", rle=True)
     if rank == 0:
         open(os.path.join(work, "runs.bin"), "wb").write(eng.runs_bytes())
+    eng.close()
+    dist.destroy_process_group()
+
+
+def gpu_gather_device(rank, world, port, work):
+    """gather_step on device tensors over RCCL (the bench's CMSBWT_DIST=gather
+    path): the reduce, the root's slice copy and the receives run on torch's
+    stream while the engine reads from its own, so gather_walk must wait for
+    them.  One rank (RCCL allows one rank per GPU); rank 0 writes its runs."""
+    import cmsbwt
+    import cmsbwt.dist as cdist
+    dist = _init(rank, world, port, backend="nccl")
+    cfg = json.load(open(os.path.join(work, "cfg.json")))
+    eng = cmsbwt.Engine(0)
+    eng.initialize_reference(cfg["ref"])
+    docs = cfg["docs"]
+    b, e = cdist.shard_range(len(docs), world, rank)
+    eng.load_collection([bytes.fromhex(d) for d in docs[b:e]])
+    for it in range(cfg.get("steps", 1)):
+        cdist.gather_step(eng, "cuda:0", rle=cfg["rle"])
+        if rank == 0:
+            open(os.path.join(work, f"runs{it}.bin"), "wb").write(eng.runs_bytes())
     eng.close()
     dist.destroy_process_group()
 

@@ -295,3 +295,30 @@ def test_large_reference_run_bins_beyond_lds(engine, oracle, tmp_path, case):
     """1 M reference with 32-position bins: 31k bins exceed kRunBinLdsMax, so
     the bin counters take the global path on their own."""
     _compare(engine, oracle, tmp_path, case, rle=True, env={"CMSBWT_RUN_BIN_SHIFT": "5"})
+
+
+@pytest.mark.parametrize("host_reader", [False, True], ids=["device_reader", "host_reader"])
+@pytest.mark.parametrize("case", cases.no_document_cases(), ids=lambda c: c[0])
+def test_collection_without_documents(engine, tmp_path, case, host_reader):
+    """Zero documents: the walk yields no heads (no chunk is read), and the merge
+    refuses with CMSBWT_EINPUT where the reference is undefined (FN:1359-1385),
+    as the oracle does (tests/test_oracle.py)."""
+    import cmsbwt
+    d, rp, cp, prefix = cases.materialise(tmp_path, case)
+    engine.initialize_reference(rp)
+    # a -p prefix above the file size keeps the host reader
+    engine.load_collection_file(cp, (1 << 62) if host_reader else prefix)
+    engine.ms_walk()
+    st = engine.stats()
+    assert (st.heads, st.ndocs) == (0, 0)
+    assert not engine.array("diff").any() and not engine.array("hashead").any()
+    with pytest.raises(cmsbwt.CmsBwtError) as ei:
+        engine.merge(True)
+    assert ei.value.code == cmsbwt.CMSBWT_EINPUT
+    # the engine stays usable afterwards
+    case2 = cases.small_cases()[0]
+    d2, rp2, cp2, _ = cases.materialise(tmp_path, case2)
+    engine.initialize_reference(rp2)
+    engine.load_collection_file(cp2)
+    engine.step(rle=True)
+    assert engine.stats().heads > 0

@@ -99,3 +99,39 @@ def test_sharded_world1_config3_golden(engine):
     assert (st.counter_bad, st.counter_good, st.counter_nothing) == \
         (g["t4"]["counterBad"], g["t4"]["counterGood"], g["t4"]["counterDoNothing"])
     assert hashlib.sha256(engine.runs_bytes()).hexdigest() == g["t4"]["rl_bwt_sha256"]
+
+
+def test_rank_without_documents(oracle, tmp_path):
+    """More ranks than documents: the last rank owns none (its walk yields no
+    heads, ms_walk returns without a chunk) and the position-sharded merge
+    still gives the oracle's bytes."""
+    rng = cases._rng(31)
+    ref = cases.rand_dna(rng, 3000)
+    coll = cases.mutate(rng, ref, 0.01) + b"\n\n" + cases.mutate(rng, ref, 0.01) + b"\n"  # blank line splits: 2 docs
+    case = ("two_docs", cases.fasta([ref]), coll, cases.UINT64_MAX)
+    d, rp, cp, prefix, ost, want = _oracle_files(oracle, tmp_path, case, True)
+    docs, _ = cases.py_read_docs(coll, prefix)
+    assert len(docs) == 2
+    work = str(tmp_path)
+    json.dump({"ref": rp, "docs": [x.hex() for x in docs], "rle": True, "steps": 1},
+              open(os.path.join(work, "cfg.json"), "w"))
+    spawn("gpu_position_sharded", 3, work)
+    assert open(os.path.join(work, "runs0.bin"), "rb").read() == want
+    st = json.load(open(os.path.join(work, "stats.json")))
+    assert (st["heads"], st["keys"], st["rank"]) == (ost["heads"], ost["keys"], ost["rank"])
+
+
+@pytest.mark.parametrize("case", [c for c in cases.small_cases() if c[0] in ("copies_5k_1pct", "tiny_docs")],
+                         ids=lambda c: c[0])
+def test_gather_step_device_tensors_rccl(oracle, tmp_path, case):
+    """gather_step with device tensors over RCCL (one rank: RCCL allows one rank
+    per GPU): the collectives and the root's copy are asynchronous on torch's
+    stream, the engine reads on its own; two repeated steps equal the oracle."""
+    d, rp, cp, prefix, ost, want = _oracle_files(oracle, tmp_path, case, True)
+    docs, _ = cases.py_read_docs(open(cp, "rb").read(), prefix)
+    work = str(tmp_path)
+    json.dump({"ref": rp, "docs": [x.hex() for x in docs], "rle": True, "steps": 2},
+              open(os.path.join(work, "cfg.json"), "w"))
+    spawn("gpu_gather_device", 1, work)
+    for it in range(2):
+        assert open(os.path.join(work, f"runs{it}.bin"), "rb").read() == want, f"step {it}"

@@ -37,6 +37,53 @@ def test_cli_exists_and_prints_help(built):
     assert r.returncode == 255 and "Usage:" in r.stdout and "-r" in r.stdout
 
 
+# Reader quirks, each restated from the reference line that causes it.  The
+# committed small goldens are oracle outputs (parity with the reference itself
+# is unpinned for them); these are the line-by-line cross-checks.
+READER_QUIRKS = [
+    # FN:1138 `while (getline(...).good())`: a last line without '\n' sets eof,
+    # good() is false and the line is dropped
+    ("unterminated_last_line_dropped", b">a\nACGT\nGG", [b"", b"ACGT"]),
+    # FN:1139 `line.empty() || line[0] == '>'` ends a document: a leading
+    # header closes an empty first document (FN:1140 appends the separator)
+    ("leading_header_empty_first_doc", b">a\nAC\n", [b"", b"AC"]),
+    # FN:1139 blank lines end documents like headers; consecutive ones give
+    # empty documents
+    ("blank_lines_split", b"AC\n\n\nGT\n", [b"AC", b"", b"GT"]),
+    # FN:1257-1266 `else if (!line.empty())` concatenates lines: headerless
+    # multi-line input is one document, closed as the tail (FN:1269-1275)
+    ("headerless_multiline_one_doc", b"AC\nGT\nTT\n", [b"ACGTTT"]),
+    # FN:1269 the tail document only exists when content is non-empty
+    ("no_tail_after_header", b"AC\n>b\n", [b"AC"]),
+    # '\r' is data: getline splits on '\n' only
+    ("crlf_kept", b">a\r\nAC\r\n", [b"", b"AC\r"]),
+]
+
+
+@pytest.mark.parametrize("name,body,docs", READER_QUIRKS, ids=[q[0] for q in READER_QUIRKS])
+def test_reader_quirks_restated_from_reference_lines(built, tmp_path, name, body, docs):
+    import cmsbwt
+    assert cases.py_read_docs(body)[0] == docs
+    p = str(tmp_path / "c.fa")
+    open(p, "wb").write(body)
+    assert cmsbwt.host_read_collection(p, cases.UINT64_MAX)[0] == docs
+
+
+def test_reader_prefix_cut_arithmetic(built, tmp_path):
+    """-p (FN:223 `_sn = min(file size, prefixLength)`, FN:1259-1262): the line at
+    which charactersRead reaches _sn - 1 is cut to `size - (read - _sn) - 1`
+    bytes and reading stops; the separator counted by a header is one of the
+    _sn symbols (`-p 1003` -> 1002 symbols)."""
+    import cmsbwt
+    body = b">a\n" + b"A" * 10 + b"\n>b\n" + b"C" * 10 + b"\n"
+    p = str(tmp_path / "c.fa")
+    open(p, "wb").write(body)
+    # read: '>a' -> 1, A*10 -> 11, '>b' -> 12, C*10 -> 22 >= sn-1 = 14 -> cut to 10 - (22-15) - 1 = 2
+    want = [b"", b"A" * 10, b"CC"]
+    assert cases.py_read_docs(body, 15)[0] == want
+    assert cmsbwt.host_read_collection(p, 15)[0] == want
+
+
 @pytest.mark.parametrize("case", cases.small_cases(), ids=lambda c: c[0])
 def test_reader_matches_reference_semantics(built, tmp_path, case):
     import cmsbwt

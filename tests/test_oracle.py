@@ -44,6 +44,16 @@ def test_oracle_rle_decodes_to_bwt_plus_quirk(oracle, tmp_path, case):
     assert int(lens.sum()) >= os.path.getsize(os.path.join(d, "o.bwt"))
 
 
+@pytest.mark.parametrize("case", cases.no_document_cases(), ids=lambda c: c[0])
+def test_oracle_rejects_collection_without_documents(oracle, tmp_path, case):
+    """Zero documents means zero heads, where FN:1359-1385 is undefined: the
+    oracle refuses (rc 3, "reference UB") instead of reading V[-1]."""
+    d, rp, cp, prefix = cases.materialise(tmp_path, case)
+    assert cases.py_read_docs(case[2], prefix)[0] == []
+    rc, st, _ = oracle.run(rp, cp, os.path.join(d, "o"), rle=True, prefix=prefix)
+    assert rc == 3 and st["heads"] == 0
+
+
 def _gen(tmp_path, key):
     import sys
     sys.path.insert(0, GOLD)
