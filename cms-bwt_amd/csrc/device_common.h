@@ -7,10 +7,16 @@ namespace cmsbwt {
 
 constexpr int kMaxLevels = 6;   // block-minima levels over LCP (64^6 > 2^32)
 constexpr uint32_t kPoolB = 16; // head records per pool block
+#ifndef CMSBWT_POOL_BATCH
+#define CMSBWT_POOL_BATCH 4
+#endif
+// pool blocks a lane of the uniform-step walk reserves per atomic (it keeps
+// unused ones for its next chunk; blocks never started keep blkChunk = ~0)
+constexpr uint32_t kPoolBatch = CMSBWT_POOL_BATCH;
 constexpr uint8_t kSep = 2;     // CMS-BWT.h:28
 // Readable tail after x and after the collection text: the cooperative LCE
-// of the walk reads up to 1 KiB (+16 B) past its current position.
-constexpr uint64_t kTextPad = 2048;
+// of the walk reads up to 4 KiB past its current position.
+constexpr uint64_t kTextPad = 8192;
 
 // Reference index staged in HBM; int32/uint32 arrays,
 // x as bytes with 64 bytes of padding so the LCE loop can read 16 B past n.
@@ -33,10 +39,23 @@ struct DevRef {
   // first l bytes (where P's SA interval starts, or P's insertion point when
   // it does not occur) and pfx[pfxOff[l] + 2c + 1] = the number of suffixes
   // starting with P.  pfx == nullptr disables them.
+  // A P that does not occur holds instead the walk's answer for any text
+  // starting with P (an "answer entry", word 1 has kPfxAns): the longest
+  // occurring prefix length l (< |P|) in the low byte, pos = SA[mm] in word 0
+  // with mm the insertion point of P[0..l] inside the interval of P[0..l)
+  // (FN:65-76: the interval's last index and smaller = false when P[0..l]
+  // sorts after all of it), kPfxSmaller = smaller, kPfxSingle = that
+  // interval holds one suffix.  Occurring entries keep (Start, Count).
   const uint32_t* pfx;
   uint32_t pfxOff[17];
   const uint8_t* kmap;  // 256 entries
   uint32_t kmerK, kmerB;
+  // 1 when no carried SA interval can be inexact: the reference holds no byte
+  // 0 or 1, so no text prefix can reach rank 0 and contractLeft never returns
+  // the root with len > 0 (FN:37-39).  The walk then trusts answer entries
+  // without re-reading the carried prefix's interval, and may drop a
+  // contraction whose result the next position's table probe supersedes.
+  uint32_t pfxExact;
   // Child table (walk only): ld[k] = min(LCP[k], 2^16-1) << 16 | D[k] << 8 | U[k]
   // with D[k] = x[SA[k]+LCP[k]] (where suffix k leaves suffix k-1) and
   // U[k] = x[SA[k]+LCP[k+1]] (where it leaves suffix k+1); nullptr disables
@@ -49,6 +68,10 @@ struct DevRef {
   const uint4* pr;
   const uint4* ir;
 };
+
+constexpr uint32_t kPfxAns = 0x80000000u;
+constexpr uint32_t kPfxSingle = 0x40000000u;
+constexpr uint32_t kPfxSmaller = 0x20000000u;
 
 // One restart chunk of the MS walk: positions [a, b) of document `doc`.
 struct Chunk {

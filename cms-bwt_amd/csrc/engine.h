@@ -557,6 +557,7 @@ struct Engine {
     R.pfx = nullptr;
     R.kmap = nullptr;
     R.kmerK = R.kmerB = 0;
+    R.pfxExact = 0;
     memset(R.pfxOff, 0, sizeof(R.pfxOff));
     if (!env_u32("CMSBWT_PFX", 1)) return;
     const uint32_t n = hix.n;
@@ -575,7 +576,10 @@ struct Engine {
     while ((1u << B) < sigma) B++;
     uint32_t lg = 1;
     while ((1ull << lg) < n) lg++;
-    const uint32_t maxBits = std::min<uint32_t>(env_u32("CMSBWT_KMER_BITS", 24), std::max<uint32_t>(lg + 1, 12));
+    // 2^(B K) ~ 16 n: a K-mer of the text that straddles a mutation then
+    // rarely occurs in the reference, and its answer entry ends the walk's
+    // search in one probe (10 MB DNA: K = 14, 2.9 GB of tables)
+    const uint32_t maxBits = std::min<uint32_t>(env_u32("CMSBWT_KMER_BITS", 28), std::max<uint32_t>(lg + 4, 12));
     const uint32_t K = std::min<uint32_t>(maxBits / B, 16);
     if (K < 3) return;
     uint64_t total = 0;
@@ -610,12 +614,16 @@ struct Engine {
         inscan(ct.p, ctIn.p, E1, rocprim::plus<uint32_t>());
         launch_ix_pfx_write(cfEx.p, ctIn.p, cf.p, E1, dpfx.p + R.pfxOff[l], st);
       }
+      for (uint32_t l = 1; l <= K; l++)  // answer entries, level by level (each reads the level below)
+        launch_ix_pfx_answer(dpfx.p + R.pfxOff[l], l > 1 ? dpfx.p + R.pfxOff[l - 1] : nullptr, 1ull << (B * l), B,
+                             dsa.p, n, l, st);
       HIPCHK(hipGetLastError());
       sync();  // map/below are pageable
       R.pfx = dpfx.p;
       R.kmap = dkmap.p;
       R.kmerK = K;
       R.kmerB = B;
+      R.pfxExact = (cnt[0] == 0 && cnt[1] == 0) ? 1u : 0u;
       return;
     }
     std::vector<uint32_t> tab(total + 4, 0);
@@ -650,6 +658,23 @@ struct Engine {
         o[2 * c + 1] = cf[c];
         sf += cf[c];
       }
+      // answer entries (k_ix_pfx_answer)
+      const uint32_t* par = l > 1 ? tab.data() + R.pfxOff[l - 1] : nullptr;
+      for (uint64_t c = 0; c < E; c++) {
+        if (o[2 * c + 1]) continue;
+        uint32_t S = 0, C = n;
+        if (par) {
+          const uint32_t p0 = par[2 * (c >> B)], p1 = par[2 * (c >> B) + 1];
+          if (p1 & kPfxAns) { o[2 * c] = p0; o[2 * c + 1] = p1; continue; }
+          S = p0;
+          C = p1;
+        }
+        uint32_t mm = o[2 * c], f = kPfxAns | kPfxSmaller;
+        if (mm >= S + C) { mm = S + C - 1; f = kPfxAns; }
+        if (C == 1) f |= kPfxSingle;
+        o[2 * c] = (uint32_t)hix.sa[mm];
+        o[2 * c + 1] = f | (l - 1);
+      }
     }
     dpfx.alloc(total + 4);
     HIPCHK(hipMemcpyAsync(dpfx.p, tab.data(), (total + 4) * 4, hipMemcpyHostToDevice, st));
@@ -660,6 +685,7 @@ struct Engine {
     R.kmap = dkmap.p;
     R.kmerK = K;
     R.kmerB = B;
+    R.pfxExact = (cnt[0] == 0 && cnt[1] == 0) ? 1u : 0u;
   }
 
   // Child table of the uniform-step walk: ld[k] packs LCP[k] (clipped to 16
@@ -1002,7 +1028,8 @@ struct Engine {
     // walk with the measured size, so only the first walk of a denser
     // workload pays twice (1 % SNP collections have ~10 % heads)
     if (!densityLearned && !v1 && nch >= 4096) sample_density(nch);
-    uint64_t cap = (uint64_t)nch + (uint64_t)((double)chars * poolDensity * 1.1) / kPoolB + 1024;
+    const uint64_t slack = v1 ? 0 : (uint64_t)std::min<uint32_t>(walk_lanes(), nch) * (kPoolBatch - 1);
+    uint64_t cap = (uint64_t)nch + slack + (uint64_t)((double)chars * poolDensity * 1.1) / kPoolB + 1024;
     DBuf<HeadRec> rec;
     DBuf<uint32_t> blkChunk, blkSeq;
     uint32_t usedBlocks = 0;
@@ -1013,6 +1040,7 @@ struct Engine {
       blkSeq.alloc(cap);
       used.zero(st);
       nextChunk.zero(st);
+      HIPCHK(hipMemsetAsync(blkChunk.p, 0xff, cap * 4, st));
       Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
       HIPCHK(hipEventRecord(ev0, st));
       if (v1) launch_ms_walk(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.laneChunk.p, pool, chunkCount.p, st);
@@ -1025,17 +1053,13 @@ struct Engine {
       HIPCHK(hipEventElapsedTime(&ms, ev0, ev1));
       stats.ms_walk_kernel_ms = ms;
       if (usedBlocks <= cap) break;
-      cap = (uint64_t)usedBlocks + (uint64_t)nch + 1024;
-    }
-    if (chars) {
-      poolDensity = std::max(1.0 / 32, (double)usedBlocks * kPoolB / (double)chars);
-      densityLearned = true;
+      cap = (uint64_t)usedBlocks + (uint64_t)nch + slack + 1024;
     }
     if (w2stats.p) {
       static const char* names[32] = {"done", "next", "bs_text", "bs_sa", "bs_x", "fail_sa", "lce_sa", "lce",
                                        "skip1", "skip0", "gallop", "skipbs", "isa1", "conp", "ext1", "adj",
-                                       "pfx_text", "pfx_probe", "ext_a", "ext_b", "lce_coop", "c_adj0", "c_adv",
-                                       "c_post", "c_char", "-", "scan0", "scan1", "scan2", "scan3", "wave_steps",
+                                       "pfx_text", "pfx_probe", "ext_a", "ext_b", "sktxt", "ivl", "lce_coop",
+                                       "c_adj0", "c_adv", "c_post", "scan0", "scan1", "scan2", "scan3", "wave_steps",
                                        "coop_steps"};
       std::vector<unsigned long long> h(32);
       HIPCHK(hipMemcpy(h.data(), w2stats.p, 32 * 8, hipMemcpyDeviceToHost));
@@ -1052,6 +1076,10 @@ struct Engine {
       const unsigned long long tot = read1(chunkBase.p + (nch - 1)) + read1(withEnd.p + (nch - 1));
       if (tot >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^31-1 heads (int32 ranks, FN:1436)"};
       H = (uint32_t)tot;
+    }
+    if (chars) {  // head density for the next walk's pool
+      poolDensity = std::max(1.0 / 32, (double)H / (double)chars);
+      densityLearned = true;
     }
     hStart.alloc(H); hPos.alloc(H); hLen.alloc(H); hIsa.alloc(H); hTonext.alloc(H);
     hSmall.alloc(H); hChar.alloc(H); hNext.alloc(H);
@@ -1592,18 +1620,25 @@ struct Engine {
     used.zero(st);
     next.zero(st);
     const uint64_t sampleChars = (uint64_t)ns * plan.C;
-    const uint64_t cap = ns + sampleChars / 2 / kPoolB + 1024;  // up to 50 % heads
+    const uint32_t sampleLanes = std::min<uint32_t>(walk_lanes(), ns);
+    const uint64_t cap = ns + (uint64_t)sampleLanes * (kPoolBatch - 1) + sampleChars / 2 / kPoolB + 1024;  // up to 50 % heads
     DBuf<HeadRec> rec;
     DBuf<uint32_t> blkChunk, blkSeq;
     rec.alloc(cap * kPoolB);
     blkChunk.alloc(cap);
     blkSeq.alloc(cap);
+    HIPCHK(hipMemsetAsync(blkChunk.p, 0xff, cap * 4, st));
     Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
     launch_ms_walk2(R, dtext.p, ddoc.p, plan.dch.p, nch, order.p, bstart.p, 1, next.p, pool, cnt.p,
-                    std::min<uint32_t>(walk_lanes(), ns), nullptr, st);
+                    sampleLanes, nullptr, st);
     HIPCHK(hipGetLastError());
-    const uint32_t ub = read1(used.p);
-    if (sampleChars) poolDensity = std::max(1.0 / 32, 1.15 * (double)ub * kPoolB / (double)sampleChars);
+    // heads of the sampled chunks (an overflowing sample still counts them all)
+    std::vector<uint32_t> hc(nch);
+    HIPCHK(hipMemcpyAsync(hc.data(), cnt.p, (uint64_t)nch * 4, hipMemcpyDeviceToHost, st));
+    sync();
+    uint64_t heads = 0;
+    for (uint32_t c : ids) heads += hc[c];
+    if (sampleChars) poolDensity = std::max(1.0 / 32, 1.15 * (double)heads / (double)sampleChars);
   }
   float counter_kernel_ms = 0;
   bool keptT = false;  // rank2head written by the last merge

@@ -46,6 +46,8 @@
 // bounds the walk; the issued instructions per step do.  Hence few, narrow
 // loads, compute written once, and long extensions moved to coalesced
 // wave-wide compares.
+#include <type_traits>
+
 #include "device_common.h"
 #include "kernels.h"
 
@@ -75,6 +77,8 @@ enum : uint32_t {
   PH_PFX_PROBE,
   PH_EXT_A,
   PH_EXT_B,
+  PH_SKTXT,
+  PH_IVL,
   PH_LCE_COOP,  // served by the whole wave (no lane load)
   // compute phases
   PC_ADJ0,
@@ -249,6 +253,15 @@ struct Walk2Args {
   unsigned long long* stats;  // STATS builds: per-phase lane-steps, wave-steps, ...
 };
 
+#ifndef CMSBWT_COOP_J
+#define CMSBWT_COOP_J 4
+#endif
+constexpr uint32_t kCoopJ = CMSBWT_COOP_J;  // 16-B pieces per thread per cooperative round
+#ifndef CMSBWT_COOP_ADAPT
+#define CMSBWT_COOP_ADAPT 1
+#endif
+constexpr bool kCoopAdapt = CMSBWT_COOP_ADAPT;  // first round 1 KiB per slot, then doubling
+
 #ifndef CMSBWT_W2_WAVES
 #define CMSBWT_W2_WAVES 6
 #endif
@@ -285,8 +298,14 @@ k_ms_walk2(Walk2Args A) {
   uint32_t i = 0, len = 0, pos = 0, prevPos = 0;
   int32_t lb = 0, rb = 0;
   bool smaller = false;
+  // text window of the prefix-table path: tw = t[twAt .. twAt+16), with the
+  // code of its first wm <= K symbols in wcode
+  uint4 tw = make_uint4(0, 0, 0, 0);
+  uint32_t twAt = 0xffffffffu, wcode = 0, wm = 0;
   // emission
-  uint32_t count = 0, blk = 0xffffffffu, fill = kPoolB, seq = 0;
+  // pool blocks are reserved kPoolBatch at a time (blk .. blkEnd) and kept
+  // across this lane's chunks; blocks never started keep blkChunk = ~0
+  uint32_t count = 0, blk = 0xffffffffu, blkEnd = 0, fill = kPoolB, seq = 0;
   uint32_t phase = PH_NEXT, use = 0;
   uintptr_t ad0 = X, ad2 = X;
   // phase-local slots
@@ -310,23 +329,85 @@ k_ms_walk2(Walk2Args A) {
     ad2 = SA + 4ull * (uint32_t)u3;
     use = U0B | U2D;
   };
-  // next character(s) over a large interval: prefix-rank tables below depth K
-  auto begin_search = [&]() {
-    if (R.pfx && len < R.kmerK) {
+  // a new text window at `at`: codes of its leading symbols (at most K)
+  auto set_window = [&](const uint4& v, uint32_t at) {
+    tw = v;
+    twAt = at;
+    const uint32_t K = R.kmerK, Bb = R.kmerB;
+    uint32_t code = 0, m = 0;
+    bool run = true;
+#pragma unroll
+    for (uint32_t d = 0; d < 16; d++) {
+      if (d < K && run) {
+        const uint32_t w = d < 4 ? v.x : d < 8 ? v.y : d < 12 ? v.z : v.w;
+        const uint32_t mp = kmapL[(w >> (8 * (d & 3))) & 0xff];
+        if (mp == 0xff) run = false;
+        else { code = (code << Bb) | mp; m = d + 1; }
+      }
+    }
+    wcode = code;
+    wm = m;
+  };
+  // probe of the prefix tables for t[i..i+m) (window at i): its interval, or
+  // the answer entry; without pfxExact also the carried prefix's entry (the
+  // interval must be exactly t[i..i+len)'s, not the root of FN:37-39); with
+  // it the window at i + 1 for the next position
+  auto pfx_probe = [&]() {
+    const uint32_t m = wm, code = wcode, Bb = R.kmerB;
+    // the next byte is no symbol (document end), or len = 0 away from the
+    // root: character by character
+    if (m <= len || (len == 0 && !(lb == 0 && rb == (int32_t)n - 1))) {
+      begin_bs();
+      return;
+    }
+    phase = PH_PFX_PROBE;
+    ad0 = (uintptr_t)(R.pfx + pfxL[m] + 2 * code);
+    use = U0E;
+    if (R.pfxExact) {
+      ad2 = T + i + 1;
+      use |= U2Q;
+    } else if (len > 0) {
+      ad2 = (uintptr_t)(R.pfx + pfxL[len] + 2 * (code >> (Bb * (m - len))));
+      use |= U2E;
+    }
+  };
+  auto begin_pfx = [&]() {
+    if (twAt == i) {
+      pfx_probe();
+    } else {
       phase = PH_PFX_TEXT;
       ad0 = T + i;
       use = U0Q;
-    } else {
-      begin_bs();
     }
+  };
+  // next character(s) over a large interval: prefix-rank tables below depth K
+  auto begin_search = [&]() {
+    if (R.pfx && len < R.kmerK) begin_pfx();
+    else begin_bs();
+  };
+  auto isa1 = [&]() {
+    phase = PH_ISA1;
+    if (R.ir) { ad0 = (uintptr_t)(R.ir + pos + 1); use = U0Q; }
+    else { ad0 = (uintptr_t)(R.isa + pos + 1); use = U0D; }
+  };
+  // the carried interval after a skip or a mismatch is not needed when the
+  // next position resolves by a table probe (pfxExact, len < K, K symbols
+  // ahead): it is marked unknown (lb < 0), the root when len = 0
+  auto virtual_interval = [&]() {
+    if (len == 0) { lb = 0; rb = (int32_t)n - 1; }
+    else { lb = -1; rb = -2; }
   };
   auto skip_done = [&](uint32_t s) {
     i += s;
     len -= s;
     pos += s;
-    phase = PH_ISA1;
-    if (R.ir) { ad0 = (uintptr_t)(R.ir + pos + 1); use = U0Q; }
-    else { ad0 = (uintptr_t)(R.isa + pos + 1); use = U0D; }
+    if (R.pfxExact && len < R.kmerK) {  // the window at i + 1 decides
+      phase = PH_SKTXT;
+      ad0 = T + i + 1;
+      use = U0Q;
+    } else {
+      isa1();
+    }
   };
   // adjustInterval(lo, hi, len) from the records of lo (PSV side: LCP[lo],
   // LCP[lo-1], ..) and of hi (NSV side: LCP[hi+1], ..); the general scan
@@ -428,6 +509,7 @@ k_ms_walk2(Walk2Args A) {
           rb = (int32_t)n - 1;
           prevPos = 0xfffffffeu;  // prevPos + 1 never equals a position
           smaller = false;
+          twAt = 0xffffffffu;
           if (R.pfx) {
             phase = PH_PFX_TEXT;
             ad0 = T + i;
@@ -443,7 +525,8 @@ k_ms_walk2(Walk2Args A) {
       use = 0;
     }
 
-    // ---- compute phases, in chain order (ADJ0 -> ADV -> CHAR; POST is terminal)
+    // ---- compute phases, in chain order (ADJ0 -> POST -> ADV -> CHAR; POST reaches ADV
+    // when the contraction is dropped)
     if (phase == PC_ADJ0) {  // adjustInterval(lo = u0, hi = u5, len) (FN:11-25)
       const int32_t lo = u0, hi = u5;
       uint32_t ls0;
@@ -452,21 +535,15 @@ k_ms_walk2(Walk2Args A) {
       u4 = (int32_t)ls0;
       adj_or_finish();
     }
-    if (phase == PC_ADV) {  // FN:1195-1196
-      i++;
-      prevPos = pos;
-      if (i >= b) {
-        A.chunkCount[cid] = count;
-        phase = PH_NEXT;
-        use = 0;
-      } else {
-        phase = PC_CHAR;
-      }
-    }
     if (phase == PC_POST) {  // head test and record (FN:1154-1171), then contraction
       if (i >= a && pos != prevPos + 1) {
         if (fill == kPoolB) {
-          blk = atomicAdd(A.pool.used, 1u);
+          if (blk + 1 < blkEnd) {
+            blk++;
+          } else {
+            blk = atomicAdd(A.pool.used, kPoolBatch);
+            blkEnd = blk + kPoolBatch;
+          }
           fill = 0;
           if (blk < A.pool.capBlocks) { A.pool.blkChunk[blk] = cid; A.pool.blkSeq[blk] = seq; }
           seq++;
@@ -491,6 +568,10 @@ k_ms_walk2(Walk2Args A) {
         const uint64_t TT = (uint64_t)pos + 1 + len;
         ad0 = P + 4ull * (TT >= 16 ? TT - 16 : 0);
         use = U0Q | U1Q | U4Q | U5Q;
+      } else if (lb < 0) {  // unknown interval: the next position's probe supersedes contractLeft
+        if (len == 0) { lb = 0; rb = (int32_t)n - 1; }
+        phase = PC_ADV;
+        use = 0;
       } else {  // FN:1190-1194: contractLeft from the psi records of lb and rb
         phase = PH_CONP;
         ad0 = (uintptr_t)(R.pr + (uint32_t)lb);
@@ -498,11 +579,24 @@ k_ms_walk2(Walk2Args A) {
         use = U0Q | U2Q;
       }
     }
+    if (phase == PC_ADV) {  // FN:1195-1196
+      i++;
+      prevPos = pos;
+      if (i >= b) {
+        A.chunkCount[cid] = count;
+        phase = PH_NEXT;
+        use = 0;
+      } else {
+        phase = PC_CHAR;
+      }
+    }
     if (phase == PC_CHAR) {  // next character of computeMSFactorAt at j = i + len
       if (lb == rb) {
         phase = PH_LCE_SA;
         ad0 = SA + 4ull * (uint32_t)lb;
         use = U0D;
+      } else if (R.pfxExact && len < R.kmerK) {  // (the only way on an unknown interval)
+        begin_pfx();
       } else if (R.ld && rb - lb < 16 && len < 0xffffu) {
         phase = PH_EXT1;
         ad0 = (uintptr_t)(R.ld + lb);
@@ -762,121 +856,149 @@ k_ms_walk2(Walk2Args A) {
         }
         break;
       }
-      case PH_PFX_TEXT: {  // codes of the longest symbol prefix t[i..i+m), m <= K
-        const uint32_t K = R.kmerK, Bb = R.kmerB;
-        uint32_t code = 0, m = 0;
-        bool run = true;
-#pragma unroll
-        for (uint32_t d = 0; d < 16; d++) {
-          if (d < K && run) {
-            const uint32_t w = d < 4 ? v0.x : d < 8 ? v0.y : d < 12 ? v0.z : v0.w;
-            const uint32_t mp = kmapL[(w >> (8 * (d & 3))) & 0xff];
-            if (mp == 0xff) run = false;
-            else { code = (code << Bb) | mp; m = d + 1; }
-          }
-        }
-        // the next byte is no symbol (document end), or len = 0 away from the
-        // root: character by character
-        if (m <= len || (len == 0 && !(lb == 0 && rb == (int32_t)n - 1))) {
-          begin_bs();
-          break;
-        }
-        u6 = (int32_t)code;
-        u7 = (int32_t)m;
-        u8 = 0;
-        phase = PH_PFX_PROBE;
-        ad0 = (uintptr_t)(R.pfx + pfxL[m] + 2 * code);
-        use = U0E;
-        if (len > 0) {  // the interval must be exactly t[i..i+len)'s (not the root of FN:37-39)
-          ad2 = (uintptr_t)(R.pfx + pfxL[len] + 2 * (code >> (Bb * (m - len))));
-          use |= U2E;
-        }
+      case PH_PFX_TEXT: {  // window at i, then the probe
+        set_window(v0, i);
+        pfx_probe();
         break;
       }
       case PH_PFX_PROBE: {
-        const uint32_t Bb = R.kmerB, m = (uint32_t)u7, code = (uint32_t)u6;
-        uint32_t lo, hi, ins;
-        if (!u8) {  // depth m (and the check of depth len)
-          if (len > 0 && (v2.x != (uint32_t)lb || v2.y != (uint32_t)(rb - lb) + 1)) {
-            begin_bs();
-            break;
-          }
-          if (v0.y) {  // t[i..i+m) occurs: its interval, depth m
-            lb = (int32_t)v0.x;
-            rb = (int32_t)(v0.x + v0.y) - 1;
-            len = m;
-            phase = PC_CHAR;
-            use = 0;
-            break;
-          }
-          lo = len;
-          hi = m;
-          ins = v0.x;
-        } else {
-          lo = (uint32_t)u1;
-          hi = (uint32_t)u2;
-          ins = (uint32_t)u3;
-          if (v0.y) {
-            lo = (uint32_t)u4;
-            lb = (int32_t)v0.x;
-            rb = (int32_t)(v0.x + v0.y) - 1;
-          } else {
-            hi = (uint32_t)u4;
-            ins = v0.x;
-          }
-        }
-        if (hi - lo > 1) {  // t[i..i+lo) occurs, t[i..i+hi) does not
-          const uint32_t mid = (lo + hi) >> 1;
-          u1 = (int32_t)lo;
-          u2 = (int32_t)hi;
-          u3 = (int32_t)ins;
-          u4 = (int32_t)mid;
-          u8 = 1;
-          ad0 = (uintptr_t)(R.pfx + pfxL[mid] + 2 * (code >> (Bb * (m - mid))));
-          use = U0E;
+        const uint32_t m = wm, code = wcode, Bb = R.kmerB;
+        if (!R.pfxExact && len > 0 && (v2.x != (uint32_t)lb || v2.y != (uint32_t)(rb - lb) + 1)) {
+          begin_bs();
           break;
         }
-        // depth lo matches and the symbol at lo does not: insertion point of
-        // t[i..i+lo+1) (FN:65-76)
-        len = lo;
-        int32_t mm = (int32_t)ins;
-        smaller = true;
-        if (mm == rb + 1) { mm = rb; smaller = false; }
-        phase = PH_FAIL_SA;
-        ad0 = SA + 4ull * (uint32_t)mm;
-        use = U0D;
+        if (R.pfxExact) set_window(v2, i + 1);
+        if (!(v0.y & kPfxAns)) {  // t[i..i+m) occurs: its interval, depth m
+          lb = (int32_t)v0.x;
+          rb = (int32_t)(v0.x + v0.y) - 1;
+          len = m;
+          phase = PC_CHAR;
+          use = 0;
+          break;
+        }
+        // answer entry: the longest occurring prefix t[i..i+l), the insertion
+        // point's SA value and `smaller` of FN:65-76, as the binary searches
+        // from the (exact) carried interval would find them
+        len = v0.y & 0xffu;
+        pos = v0.x;
+        smaller = (v0.y & kPfxSmaller) != 0;
+        use = 0;
+        phase = PC_POST;
+        if (v0.y & kPfxSingle) {
+          lb = rb = 0;  // a one-suffix interval: the skip of FN:1175-1189 follows
+        } else if (R.pfxExact && wm == R.kmerK) {
+          lb = -1;  // the next position resolves by its own probe
+          rb = -2;
+        } else if (len == 0) {
+          lb = 0;
+          rb = (int32_t)n - 1;
+        } else {  // contractLeft needs the interval of t[i..i+l)
+          phase = PH_IVL;
+          ad0 = (uintptr_t)(R.pfx + pfxL[len] + 2 * (code >> (Bb * (m - len))));
+          use = U0E;
+        }
+        break;
+      }
+      case PH_IVL: {
+        lb = (int32_t)v0.x;
+        rb = (int32_t)(v0.x + v0.y) - 1;
+        phase = PC_POST;
+        break;
+      }
+      case PH_SKTXT: {  // after a skip: K symbols at i + 1 make the interval unnecessary
+        set_window(v0, i + 1);
+        if (wm == R.kmerK) {
+          virtual_interval();
+          phase = PC_ADV;
+          use = 0;
+        } else {
+          isa1();
+        }
         break;
       }
       default:
         break;
     }
-    // ---- long extensions: the wave compares 1 KiB per step for one lane at
-    // a time, lane k loading bytes [16k, 16k+16) of x and of the text
+    // ---- long extensions, compared by the whole wave with coalesced loads.
+    // The pending lanes are served S = 1, 2 or 4 at a time (as many as are
+    // pending), each by a slot of W = 64 / S threads; a thread compares
+    // kCoopJ 16-byte pieces per round, piece j of thread k at byte
+    // 16 (k + W j), so a slot covers 16 W kCoopJ contiguous bytes per round
+    // (4 KiB for a single lane).  A slot ends at its first mismatch.
     uint64_t coop = __ballot(phase == PH_LCE_COOP);
     while (coop) {
-      const uint32_t L = (uint32_t)__builtin_ctzll(coop);
-      coop &= coop - 1;
-      const uintptr_t xa = ((uintptr_t)__shfl((uint32_t)(ad0 >> 32), L) << 32) | __shfl((uint32_t)ad0, L);
-      const uintptr_t ta = ((uintptr_t)__shfl((uint32_t)(ad2 >> 32), L) << 32) | __shfl((uint32_t)ad2, L);
-      uint32_t run = 0;
-      while (true) {
-        uint8_t xc = 0, tc = 0;
-        const uint4 xv = ldu16(xa + run + 16 * lane), tv = ldu16(ta + run + 16 * lane);
-        const uint32_t m = diff16(xv, tv, xc, tc);
-        const uint64_t mis = __ballot(m < 16);
-        if (STATS && lane == 0) atomicAdd(&sc[31], 1ull);
-        if (mis) {
-          const uint32_t f = (uint32_t)__builtin_ctzll(mis);
-          const uint32_t mm = (uint32_t)__shfl((int)m, f);
-          const uint32_t cc = (uint32_t)__shfl((int)((uint32_t)xc | ((uint32_t)tc << 8)), f);
-          if (lane == L) {
-            len += run + 16 * f + mm;
-            smaller = (int8_t)(uint8_t)cc > (int8_t)(uint8_t)(cc >> 8);  // FN:55
-            phase = PC_POST;
-          }
-          break;
+      const uint32_t P = (uint32_t)__popcll(coop);
+      const uint32_t S = P >= 4 ? 4u : P >= 2 ? 2u : 1u;
+      const uint32_t lgW = S == 4 ? 4u : S == 2 ? 5u : 6u;
+      const uint32_t W = 1u << lgW;
+      uint32_t Ls[4] = {0, 0, 0, 0};
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++)
+        if (q < S) {
+          Ls[q] = (uint32_t)__builtin_ctzll(coop);
+          coop &= coop - 1;
         }
-        run += 1024;
+      const uint32_t g = lane >> lgW, k = lane & (W - 1);
+      const uint32_t myL = g == 0 ? Ls[0] : g == 1 ? Ls[1] : g == 2 ? Ls[2] : Ls[3];
+      const uintptr_t xa = ((uintptr_t)__shfl((uint32_t)(ad0 >> 32), (int)myL) << 32) | __shfl((uint32_t)ad0, (int)myL);
+      const uintptr_t ta = ((uintptr_t)__shfl((uint32_t)(ad2 >> 32), (int)myL) << 32) | __shfl((uint32_t)ad2, (int)myL);
+      // pieces per thread: the first round reads 1 KiB per slot, later
+      // rounds double up to kCoopJ pieces (a lane's remaining match is
+      // usually shorter than 1 KiB: no over-read on the common case)
+      uint32_t run = 0, open = (1u << S) - 1;  // open: slots still comparing
+      uint32_t jr = kCoopAdapt ? (S < kCoopJ ? S : kCoopJ) : kCoopJ;
+      while (open) {
+        uint32_t mine = 16, mj = 0, cc = 0;  // this thread's first mismatch: piece, offset, chars
+        // one round of JR pieces (fixed-size arrays: no register spills)
+        auto cmp_round = [&](auto jrc) {
+          constexpr uint32_t JR = decltype(jrc)::value;
+          uint4 xv[JR], tv[JR];
+#pragma unroll
+          for (uint32_t j = 0; j < JR; j++) {
+            const uint32_t o = run + 16 * (k + (j << lgW));
+            xv[j] = ldu16(xa + o);
+            tv[j] = ldu16(ta + o);
+          }
+#pragma unroll
+          for (int j = (int)JR - 1; j >= 0; j--) {
+            uint8_t xc = 0, tc = 0;
+            const uint32_t m = diff16(xv[j], tv[j], xc, tc);
+            if (m < 16) { mine = m; mj = (uint32_t)j; cc = (uint32_t)xc | ((uint32_t)tc << 8); }
+          }
+        };
+        if ((open >> g) & 1) {
+          if (kCoopJ >= 4 && jr == 4) cmp_round(std::integral_constant<uint32_t, (kCoopJ >= 4 ? 4u : 1u)>{});
+          else if (kCoopJ >= 2 && jr == 2) cmp_round(std::integral_constant<uint32_t, (kCoopJ >= 2 ? 2u : 1u)>{});
+          else cmp_round(std::integral_constant<uint32_t, 1u>{});
+        }
+        if (STATS && lane == 0) atomicAdd(&sc[31], 1ull);
+        // per piece index j: threads whose first mismatch lies in piece j
+        uint64_t mask[kCoopJ];
+#pragma unroll
+        for (uint32_t j = 0; j < kCoopJ; j++) mask[j] = __ballot(mine < 16 && mj == j);
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+          if (q >= S || !((open >> q) & 1)) continue;
+          const uint64_t sm = (W == 64 ? ~0ull : ((1ull << W) - 1)) << (q << lgW);
+#pragma unroll
+          for (uint32_t j = 0; j < kCoopJ; j++) {
+            const uint64_t hit = mask[j] & sm;
+            if (hit) {  // first mismatching byte of slot q: piece j, thread f
+              const uint32_t f = (uint32_t)__builtin_ctzll(hit);
+              const uint32_t mm = (uint32_t)__shfl((int)mine, (int)f);
+              const uint32_t c2 = (uint32_t)__shfl((int)cc, (int)f);
+              if (lane == Ls[q]) {
+                len += run + 16 * ((f - (q << lgW)) + (j << lgW)) + mm;
+                smaller = (int8_t)(uint8_t)c2 > (int8_t)(uint8_t)(c2 >> 8);  // FN:55
+                phase = PC_POST;
+              }
+              open &= ~(1u << q);
+              break;
+            }
+          }
+        }
+        run += 16u * W * jr;
+        jr = 2 * jr < kCoopJ ? 2 * jr : kCoopJ;
       }
     }
   }

@@ -277,6 +277,31 @@ __global__ void k_ix_pfx_write(const uint32_t* __restrict__ cfEx, const uint32_t
   o[2 * c + 1] = cf[c];
 }
 
+// Answer entries of level l (device_common.h), from level l-1 (already
+// final) and level l's own insertion points: a P that does not occur either
+// inherits its parent's answer (the parent does not occur either) or, when
+// the parent P[0..l-1) occurs with interval [S, S+C), gets l-1, the insertion
+// point Start_l(P) of FN:65-76 and pos = SA of it.
+__global__ void k_ix_pfx_answer(uint32_t* __restrict__ tab, const uint32_t* __restrict__ par, uint64_t E,
+                                uint32_t B, const int32_t* __restrict__ sa, uint32_t n, uint32_t l) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= E) return;
+  const uint32_t cnt = tab[2 * c + 1];
+  if (cnt) return;  // occurs (counts never carry kPfxAns: n < 2^31)
+  uint32_t S = 0, C = n;
+  if (par) {
+    const uint32_t p0 = par[2 * (c >> B)], p1 = par[2 * (c >> B) + 1];
+    if (p1 & kPfxAns) { tab[2 * c] = p0; tab[2 * c + 1] = p1; return; }
+    S = p0;
+    C = p1;
+  }
+  uint32_t mm = tab[2 * c], f = kPfxAns | kPfxSmaller;
+  if (mm >= S + C) { mm = S + C - 1; f = kPfxAns; }
+  if (C == 1) f |= kPfxSingle;
+  tab[2 * c] = (uint32_t)sa[mm];
+  tab[2 * c + 1] = f | (l - 1);
+}
+
 static inline dim3 gix(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
 void launch_ix_plcp_check(const int32_t* plcp, uint32_t n, uint32_t* err, hipStream_t st) {
@@ -310,6 +335,11 @@ void launch_ix_pfx_count(const uint8_t* x, uint32_t n, uint32_t l, uint32_t B, c
 void launch_ix_pfx_write(const uint32_t* cfEx, const uint32_t* ctIn, const uint32_t* cf, uint64_t E1, uint32_t* o,
                          hipStream_t st) {
   if (E1) hipLaunchKernelGGL(k_ix_pfx_write, gix(E1), dim3(256), 0, st, cfEx, ctIn, cf, E1, o);
+}
+
+void launch_ix_pfx_answer(uint32_t* tab, const uint32_t* par, uint64_t E, uint32_t B, const int32_t* sa, uint32_t n,
+                          uint32_t l, hipStream_t st) {
+  if (E) hipLaunchKernelGGL(k_ix_pfx_answer, gix(E), dim3(256), 0, st, tab, par, E, B, sa, n, l);
 }
 
 }  // namespace cmsbwt

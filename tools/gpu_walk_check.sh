@@ -1,0 +1,12 @@
+# Walk change check (run through gpurun from the repo root): index tables,
+# parity suites that exercise the walk, the headline golden, stats and bench.
+set -e
+cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests -x -q -m gpu --timeout 300 --timeout-method thread -p no:cacheprovider \
+    -k "${TESTSEL:-gpu_index or small_cases or chunk_restarts or large_reference or config1 or config3_full or smoke or config2}" > gpurun_out/t_walk.log 2>&1 || { tail -40 gpurun_out/t_walk.log; exit 1; }
+tail -1 gpurun_out/t_walk.log
+CMSBWT_W2_STATS=1 timeout -k 10 300 python bench.py --steps 1 --warmup 0 --no-cpu > gpurun_out/b_st.log 2> gpurun_out/w2stats.log || { tail -20 gpurun_out/b_st.log gpurun_out/w2stats.log; exit 1; }
+grep w2stats gpurun_out/w2stats.log
+timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-cpu > gpurun_out/bench.log 2>&1 || { tail -20 gpurun_out/bench.log; exit 1; }
+python3 -c "import json; d=json.loads(open('gpurun_out/bench.log').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'], d['stages_ms'], d['roofline']['frac'])"
