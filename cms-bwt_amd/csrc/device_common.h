@@ -8,7 +8,7 @@ namespace cmsbwt {
 constexpr int kMaxLevels = 6;   // block-minima levels over LCP (64^6 > 2^32)
 constexpr uint32_t kPoolB = 16; // head records per pool block
 #ifndef CMSBWT_POOL_BATCH
-#define CMSBWT_POOL_BATCH 4
+#define CMSBWT_POOL_BATCH 16
 #endif
 // pool blocks a lane of the uniform-step walk reserves per atomic (it keeps
 // unused ones for its next chunk; blocks never started keep blkChunk = ~0)
@@ -56,6 +56,7 @@ struct DevRef {
   // without re-reading the carried prefix's interval, and may drop a
   // contraction whose result the next position's table probe supersedes.
   uint32_t pfxExact;
+  uint32_t pfxDna;  // the symbols are exactly A, C, G, T (codes 0..3)
   // Child table (walk only): ld[k] = min(LCP[k], 2^16-1) << 16 | D[k] << 8 | U[k]
   // with D[k] = x[SA[k]+LCP[k]] (where suffix k leaves suffix k-1) and
   // U[k] = x[SA[k]+LCP[k+1]] (where it leaves suffix k+1); nullptr disables

@@ -557,7 +557,7 @@ struct Engine {
     R.pfx = nullptr;
     R.kmap = nullptr;
     R.kmerK = R.kmerB = 0;
-    R.pfxExact = 0;
+    R.pfxExact = R.pfxDna = 0;
     memset(R.pfxOff, 0, sizeof(R.pfxOff));
     if (!env_u32("CMSBWT_PFX", 1)) return;
     const uint32_t n = hix.n;
@@ -624,6 +624,7 @@ struct Engine {
       R.kmerK = K;
       R.kmerB = B;
       R.pfxExact = (cnt[0] == 0 && cnt[1] == 0) ? 1u : 0u;
+      R.pfxDna = (sigma == 4 && cnt['A'] && cnt['C'] && cnt['G'] && cnt['T'] && !env_u32("CMSBWT_PFX_GENERIC", 0)) ? 1u : 0u;
       return;
     }
     std::vector<uint32_t> tab(total + 4, 0);
@@ -686,6 +687,7 @@ struct Engine {
     R.kmerK = K;
     R.kmerB = B;
     R.pfxExact = (cnt[0] == 0 && cnt[1] == 0) ? 1u : 0u;
+      R.pfxDna = (sigma == 4 && cnt['A'] && cnt['C'] && cnt['G'] && cnt['T'] && !env_u32("CMSBWT_PFX_GENERIC", 0)) ? 1u : 0u;
   }
 
   // Child table of the uniform-step walk: ld[k] packs LCP[k] (clipped to 16

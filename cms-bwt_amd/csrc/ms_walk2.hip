@@ -330,10 +330,25 @@ k_ms_walk2(Walk2Args A) {
     use = U0B | U2D;
   };
   // a new text window at `at`: codes of its leading symbols (at most K)
-  auto set_window = [&](const uint4& v, uint32_t at) {
+  auto set_window = [&](const uint4 v, uint32_t at) {
     tw = v;
     twAt = at;
     const uint32_t K = R.kmerK, Bb = R.kmerB;
+    if (R.pfxDna) {  // alphabet ACGT: 2-bit codes of 4 bytes at a time
+      const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
+      uint32_t full = 0, bad = 16;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        // A C G T (0x41 43 47 54) -> 0 1 2 3 in bits 1..2 xor 2..3 of each byte
+        const uint32_t c = ((w4[q] >> 1) ^ (w4[q] >> 2)) & 0x03030303u;
+        const uint32_t x = __builtin_amdgcn_perm(0u, 0x54474341u, c) ^ w4[q];  // zero byte: a symbol
+        if (bad == 16 && x) bad = 4 * q + ((uint32_t)__builtin_ctz(x) >> 3);
+        full |= (((c & 3u) << 6) | ((c >> 4) & 0x30u) | ((c >> 14) & 0xcu) | ((c >> 24) & 3u)) << (24 - 8 * q);
+      }
+      wm = bad < K ? bad : K;
+      wcode = wm ? full >> (32 - 2 * wm) : 0u;
+      return;
+    }
     uint32_t code = 0, m = 0;
     bool run = true;
 #pragma unroll
@@ -361,6 +376,8 @@ k_ms_walk2(Walk2Args A) {
       return;
     }
     phase = PH_PFX_PROBE;
+    u6 = (int32_t)code;  // kept: the probe step replaces the window
+    u7 = (int32_t)m;
     ad0 = (uintptr_t)(R.pfx + pfxL[m] + 2 * code);
     use = U0E;
     if (R.pfxExact) {
@@ -536,14 +553,24 @@ k_ms_walk2(Walk2Args A) {
       adj_or_finish();
     }
     if (phase == PC_POST) {  // head test and record (FN:1154-1171), then contraction
-      if (i >= a && pos != prevPos + 1) {
+      const bool head = i >= a && pos != prevPos + 1;
+      // new pool blocks: one atomic per wave for every lane whose reserved
+      // blocks ran out (a single counter takes every reservation of the grid)
+      const bool refill = head && fill == kPoolB && blk + 1 >= blkEnd;
+      const uint64_t rq = __ballot(refill);
+      if (rq) {
+        const uint32_t leader = (uint32_t)__builtin_ctzll(rq);
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(A.pool.used, kPoolBatch * (uint32_t)__popcll(rq));
+        base = __shfl(base, (int)leader);
+        if (refill) {
+          blk = base + kPoolBatch * (uint32_t)__popcll(rq & ((1ull << lane) - 1)) - 1;  // blk++ below
+          blkEnd = blk + 1 + kPoolBatch;
+        }
+      }
+      if (head) {
         if (fill == kPoolB) {
-          if (blk + 1 < blkEnd) {
-            blk++;
-          } else {
-            blk = atomicAdd(A.pool.used, kPoolBatch);
-            blkEnd = blk + kPoolBatch;
-          }
+          blk++;
           fill = 0;
           if (blk < A.pool.capBlocks) { A.pool.blkChunk[blk] = cid; A.pool.blkSeq[blk] = seq; }
           seq++;
@@ -630,6 +657,14 @@ k_ms_walk2(Walk2Args A) {
     if (use & U5Q) v5 = ldu16(ad0 + 48);
     if (use & U0E) { const uint2 w = ld8(ad0); v0.x = w.x; v0.y = w.y; }
     if (use & U2E) { const uint2 w = ld8(ad2); v2.x = w.x; v2.y = w.y; }
+    // the text window this step loaded (one call site: the code is emitted once)
+    {
+      const bool wa = phase == PH_PFX_TEXT || phase == PH_SKTXT;
+      if (wa || (phase == PH_PFX_PROBE && R.pfxExact)) {
+        const uint4 vv = make_uint4(wa ? v0.x : v2.x, wa ? v0.y : v2.y, wa ? v0.z : v2.z, wa ? v0.w : v2.w);
+        set_window(vv, phase == PH_PFX_TEXT ? i : i + 1);
+      }
+    }
     // ---- one state-machine step (load phases)
     switch (phase) {
       case PH_BS_TEXT: {  // c = t[j]; the first probe's SA value is in slot 2
@@ -856,18 +891,16 @@ k_ms_walk2(Walk2Args A) {
         }
         break;
       }
-      case PH_PFX_TEXT: {  // window at i, then the probe
-        set_window(v0, i);
+      case PH_PFX_TEXT: {  // window at i (set above), then the probe
         pfx_probe();
         break;
       }
-      case PH_PFX_PROBE: {
-        const uint32_t m = wm, code = wcode, Bb = R.kmerB;
+      case PH_PFX_PROBE: {  // (wm/wcode already describe the window at i + 1)
+        const uint32_t m = (uint32_t)u7, code = (uint32_t)u6, Bb = R.kmerB;
         if (!R.pfxExact && len > 0 && (v2.x != (uint32_t)lb || v2.y != (uint32_t)(rb - lb) + 1)) {
           begin_bs();
           break;
         }
-        if (R.pfxExact) set_window(v2, i + 1);
         if (!(v0.y & kPfxAns)) {  // t[i..i+m) occurs: its interval, depth m
           lb = (int32_t)v0.x;
           rb = (int32_t)(v0.x + v0.y) - 1;
@@ -905,8 +938,7 @@ k_ms_walk2(Walk2Args A) {
         phase = PC_POST;
         break;
       }
-      case PH_SKTXT: {  // after a skip: K symbols at i + 1 make the interval unnecessary
-        set_window(v0, i + 1);
+      case PH_SKTXT: {  // after a skip: K symbols at i + 1 (window set above) make the interval unnecessary
         if (wm == R.kmerK) {
           virtual_interval();
           phase = PC_ADV;
