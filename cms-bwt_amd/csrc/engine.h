@@ -1335,7 +1335,7 @@ struct Engine {
     wflag.alloc(n);
     wincl.alloc(n);
     const uint32_t winPos = std::min(1024u, env_u32("CMSBWT_WINPOS", 1024)),
-                   slotCap = std::min(4096u, env_u32("CMSBWT_WINSLOTS", 4096));
+                   slotCap = std::min(3584u, env_u32("CMSBWT_WINSLOTS", 3584));  // kWinSlots (merge.hip)
     mk_win_flags(posBegin, S.slot, n, P0, P1, std::max(1u, winPos), slotCap, wflag.p, st);
     inscan(wflag.p, wincl.p, n, rocprim::plus<uint32_t>());
     const uint32_t nw = P1 > P0 ? read1(wincl.p + (n - 1)) : 0;
@@ -1540,8 +1540,8 @@ struct Engine {
     HIPCHK(hipMemcpyAsync(cs, cstats.p, sizeof(cs), hipMemcpyDeviceToHost, st));
     sync();
     if (env_u32("CMSBWT_COUNTER_STATS", 0))
-      fprintf(stderr, "[counter] bad %llu good %llu nothing %llu windows %u crossings %u\n", cs[0], cs[1], cs[2],
-              windows, crossings);
+      fprintf(stderr, "[counter] bad %llu good %llu nothing %llu windows %u crossings %u searched %llu\n", cs[0], cs[1],
+              cs[2], windows, crossings, cs[5]);
     stats.counter_bad = cs[0];
     stats.counter_good = cs[1];
     stats.counter_nothing = cs[2];

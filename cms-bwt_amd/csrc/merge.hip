@@ -491,7 +491,7 @@ __global__ void k_low32(const uint64_t* __restrict__ key, uint32_t* __restrict__
 // is sorted by one 64-bit search key sk and `item < query` is `sk < qk`
 // inside the query's class.  CHECK adds the ambiguity tests of DESIGN.md §5
 // (only needed when k_finalize's order invariant failed).
-constexpr uint32_t kWinSlots = 4096;  // slot cap of an LDS window (see kWinItems)
+constexpr uint32_t kWinSlots = 3584;  // slot cap of an LDS window (see kWinItems)
 
 struct CounterArgs {
   ItemsSoA it;
@@ -508,7 +508,7 @@ struct CounterArgs {
 };
 
 struct QueryStats {  // per lane; a lane serves far fewer than 2^32 queries per window
-  uint32_t bad = 0, good = 0, nothing = 0, viol = 0;
+  uint32_t bad = 0, good = 0, nothing = 0, viol = 0, slow = 0;
 };
 
 __device__ __forceinline__ uint32_t d_upper_u32(const uint32_t* a, uint32_t lo, uint32_t hi, uint32_t v) {
@@ -609,26 +609,35 @@ struct LdsView {  // items and positions rebased to the window
   const unsigned long long* skL;
   const uint32_t* slotL;
   const uint32_t* pbL;
-  const uint32_t* pfL;
+  const uint32_t* fmL;
   const uint32_t* nhr;
   uint32_t iBeg, T0;
   __device__ uint32_t begin(uint32_t t) const { return pbL[t - T0] ; }
-  __device__ uint32_t fbeg(uint32_t t) const { return pfL[t - T0]; }
+  __device__ uint32_t fbeg(uint32_t t) const { return pbL[t - T0] + (fmL[t - T0] >> 16); }
   __device__ unsigned long long sk(uint32_t q) const { return skL[q - iBeg]; }
   __device__ uint32_t slot(uint32_t q) const { return slotL[q - iBeg]; }
 };
 
-constexpr uint32_t kWinItems = 4096;  // staged items (= max slots) per window
+constexpr uint32_t kWinItems = kWinSlots;  // staged items (= max slots) per window
 constexpr uint32_t kWinPositions = 1024;
 
 template <bool CHECK>
 __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
-  __shared__ uint32_t cnt[kWinItems];                   // 16 KB; per target the adds sum to <= H < 2^31
-  __shared__ unsigned long long skL[kWinItems];         // 32 KB
-  __shared__ uint32_t slotL[kWinItems + 1];             // 16 KB
-  __shared__ uint32_t pbL[kWinPositions + 1], pfL[kWinPositions];  // 8 KB
+  __shared__ uint32_t cnt[kWinItems + 64];              // 14 KB (+ one dummy per lane); per target the adds sum to <= H < 2^31
+  __shared__ unsigned long long skL[kWinItems];         // 28 KB
+  __shared__ uint32_t slotL[kWinItems + 1];             // 14 KB
+  // per target: its first item (pbL) and, packed in fmL, the offset of its
+  // first smaller=false item (bits 16..31) and its longest item len (bits
+  // 0..15, 0xffff = that long or longer)
+  __shared__ uint32_t pbL[kWinPositions + 1], fmL[kWinPositions];  // 8 KB
+  // fast test per target: x = bit 31 no items, bit 30 no smaller=false item,
+  // bits 0..11 the first smaller=false item's slot (window-relative);
+  // y = the longest smaller=true len (bits 0..15) and the first (longest)
+  // smaller=false len (bits 16..31), 0xffff: that long or longer
+  __shared__ uint2 fastL[kWinPositions];                            // 8 KB
+  __shared__ uint32_t qL[8][64];                                     // 2 KB: per-wave query queues
   __shared__ uint32_t s_next;
-  __shared__ unsigned long long red[4];
+  __shared__ unsigned long long red[6];
   const ItemsSoA& it = A.it;
   const uint32_t w = blockIdx.x;
   const uint32_t T0 = A.winStart[w], T1 = A.winStart[w + 1];
@@ -641,17 +650,34 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
     for (uint32_t i = threadIdx.x; i < iEnd - iBeg; i += blockDim.x) skL[i] = it.sk[iBeg + i];
     for (uint32_t i = threadIdx.x; i <= iEnd - iBeg; i += blockDim.x) slotL[i] = it.slot[iBeg + i];
     for (uint32_t i = threadIdx.x; i <= T1 - T0; i += blockDim.x) pbL[i] = A.posBegin[T0 + i];
-    for (uint32_t i = threadIdx.x; i < T1 - T0; i += blockDim.x) pfL[i] = A.posF[T0 + i];
   }
   if (threadIdx.x == 0) s_next = 0;
-  if (threadIdx.x < 4) red[threadIdx.x] = 0;
+  if (threadIdx.x < 6) red[threadIdx.x] = 0;
   __syncthreads();
+  if (lds) {
+    for (uint32_t t = threadIdx.x; t < T1 - T0; t += blockDim.x) {
+      const uint32_t b0 = pbL[t] - iBeg, b1 = pbL[t + 1] - iBeg, f = A.posF[T0 + t] - iBeg;
+      uint32_t m = 0;
+      for (uint32_t q = b0; q < b1; q++) {
+        const uint32_t hi = (uint32_t)(skL[q] >> 32);
+        m = max(m, q < f ? hi : ~hi);
+      }
+      fmL[t] = ((f - b0) << 16) | min(m, 0xffffu);
+      // S items ascend by len, F items descend: the class maxima are the
+      // last S item and the first F item
+      const uint32_t mS = f > b0 ? (uint32_t)(skL[f - 1] >> 32) : 0u;
+      const uint32_t mF = f < b1 ? ~(uint32_t)(skL[f] >> 32) : 0u;
+      fastL[t] = make_uint2(b0 == b1 ? 0x80000000u : (f < b1 ? slotL[f] - sb : 0x40000000u),
+                            min(mS, 0xffffu) | (min(mF, 0xffffu) << 16));
+    }
+    __syncthreads();
+  }
   const uint32_t c0 = A.crossOff[w];
   const uint32_t nCross = A.crossOff[w + 1] - c0;
   const uint32_t nItems = nCross + (iEnd - iBeg);
-  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   QueryStats qs;
-  const LdsView LV{skL, slotL, pbL, pfL, A.nhr, iBeg, T0};
+  const LdsView LV{skL, slotL, pbL, fmL, A.nhr, iBeg, T0};
   const GlobalView GV{&A.it, A.posBegin, A.posF, A.nhr};
   auto addLds = [&](uint32_t s, uint32_t v) { atomicAdd(&cnt[s - sb], v); };
   auto addGlb = [&](uint32_t s, uint32_t v) { atomicAdd(&A.counter[s], (unsigned long long)v); };
@@ -676,25 +702,90 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
       bs = it.slot[q];
       bS = it.smaller[q];
     }
-    for (uint32_t e = 0; e < nb; e++) {
-      const uint32_t u = __builtin_amdgcn_readlane(bu, e);
-      if (!u) continue;
-      const uint32_t p = __builtin_amdgcn_readlane(bp, e);
-      const uint32_t ql = __builtin_amdgcn_readlane(bl, e), qi = __builtin_amdgcn_readlane(bi, e);
-      const uint32_t cq = __builtin_amdgcn_readlane(bc, e), slq = __builtin_amdgcn_readlane(bs, e);
-      const bool S = __builtin_amdgcn_readlane(bS, e) != 0;
-      // targets p+1 .. p+u inside [T0, T1) (positions < 2^31: 32-bit is exact)
-      const uint32_t lo = max(p + 1, T0);
-      const uint32_t hi = (uint32_t)min((uint64_t)p + u, (uint64_t)T1 - 1);
-      for (uint32_t t0 = lo; t0 <= hi; t0 += 64) {
-        const uint32_t t = t0 + lane;
-        if (t <= hi) {
-          const uint32_t k = t - p - 1;
-          if (lds) d_counter_query<CHECK>(LV, ql, qi, S, cq, slq, k, t, qs, addLds);
-          else d_counter_query<CHECK>(GV, ql, qi, S, cq, slq, k, t, qs, addGlb);
+    // queries the fast test cannot settle wait in the wave's queue and run
+    // 64 at a time (item fields by bpermute), so the binary searches do not
+    // diverge against the cheap lanes
+    uint32_t qn = 0;
+    auto drain = [&](uint32_t cntq) {
+      __builtin_amdgcn_wave_barrier();
+      const uint32_t en = lane < cntq ? qL[wv][lane] : 0u;
+      const int e = (int)(en & 63u);
+      const uint32_t p = __shfl(bp, e), ql = __shfl(bl, e), qi = __shfl(bi, e);
+      const uint32_t cq = __shfl(bc, e), slq = __shfl(bs, e), sS = __shfl(bS, e);
+      __builtin_amdgcn_wave_barrier();
+      if (lane < cntq) {
+        qs.slow++;
+        const uint32_t t = T0 + (en >> 6);
+        d_counter_query<false>(LV, ql, qi, sS != 0, cq, slq, t - p - 1, t, qs, addLds);
+      }
+    };
+    if (lds && !CHECK) {
+      for (uint32_t e = 0; e < nb; e++) {
+        const uint32_t u = __builtin_amdgcn_readlane(bu, e);
+        if (!u) continue;
+        const uint32_t p = __builtin_amdgcn_readlane(bp, e);
+        const uint32_t ql = __builtin_amdgcn_readlane(bl, e), cq = __builtin_amdgcn_readlane(bc, e);
+        const bool S = __builtin_amdgcn_readlane(bS, e) != 0;
+        // targets p+1 .. p+u inside [T0, T1) (positions < 2^31: 32-bit is exact)
+        const uint32_t lo = max(p + 1, T0);
+        const uint32_t hi = (uint32_t)min((uint64_t)p + u, (uint64_t)T1 - 1);
+        // the query len at t is ql - 1 - (t - p - 1) = E - t (uint32 wrap as FN:1532)
+        const uint32_t E = ql + p;
+        for (uint32_t t0 = lo; t0 <= hi; t0 += 64) {
+          const uint32_t t = t0 + lane;
+          const bool valid = t <= hi;
+          const uint2 fw = fastL[min(t, hi) - T0];
+          const uint32_t L = E - t;
+          const uint32_t mS = fw.y & 0xffffu, mF = fw.y >> 16;
+          // a query longer than every item of its class lands on the first
+          // smaller=false item (lower_bound past the smaller=true class, or
+          // the first of a class sorted by len descending); an S query there
+          // is equal to it (operator== ignores `smaller`) only at its len
+          const bool fast = S ? (mS != 0xffffu && mF != 0xffffu && L > mS && L != mF) : (mF != 0xffffu && L > mF);
+          const bool none = (fw.x & 0x80000000u) != 0;  // bucket >= 0: no heads at t (FN:1530)
+          const bool add = valid && !none && fast && !(fw.x & 0x40000000u);
+          const bool slow = valid && !none && !fast;
+          qs.nothing += (valid && none) ? 1u : 0u;
+          qs.good += add ? 1u : 0u;
+          // every lane adds: the non-adding ones to a private dummy counter
+          atomicAdd(&cnt[add ? fw.x : kWinItems + lane], cq);
+          const uint64_t sm = __ballot(slow);
+          if (sm) {
+            const uint32_t c = (uint32_t)__popcll(sm), r = (uint32_t)__popcll(sm & ((1ull << lane) - 1));
+            const uint32_t room = 64 - qn, en = e | ((t - T0) << 6);
+            if (slow && r < room) qL[wv][qn + r] = en;
+            if (c >= room) {
+              drain(64);
+              __builtin_amdgcn_wave_barrier();
+              if (slow && r >= room) qL[wv][r - room] = en;
+              qn = c - room;
+            } else {
+              qn += c;
+            }
+          }
+        }
+      }
+    } else {
+      for (uint32_t e = 0; e < nb; e++) {
+        const uint32_t u = __builtin_amdgcn_readlane(bu, e);
+        if (!u) continue;
+        const uint32_t p = __builtin_amdgcn_readlane(bp, e);
+        const uint32_t ql = __builtin_amdgcn_readlane(bl, e), qi = __builtin_amdgcn_readlane(bi, e);
+        const uint32_t cq = __builtin_amdgcn_readlane(bc, e), slq = __builtin_amdgcn_readlane(bs, e);
+        const bool S = __builtin_amdgcn_readlane(bS, e) != 0;
+        const uint32_t lo = max(p + 1, T0);
+        const uint32_t hi = (uint32_t)min((uint64_t)p + u, (uint64_t)T1 - 1);
+        for (uint32_t t0 = lo; t0 <= hi; t0 += 64) {
+          const uint32_t t = t0 + lane;
+          if (t <= hi) {
+            const uint32_t k = t - p - 1;
+            if (lds) d_counter_query<CHECK>(LV, ql, qi, S, cq, slq, k, t, qs, addLds);
+            else d_counter_query<CHECK>(GV, ql, qi, S, cq, slq, k, t, qs, addGlb);
+          }
         }
       }
     }
+    if (qn) drain(qn);
   }
   __syncthreads();
   if (lds)
@@ -703,8 +794,9 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
   if (qs.good) atomicAdd(&red[1], (unsigned long long)qs.good);
   if (qs.nothing) atomicAdd(&red[2], (unsigned long long)qs.nothing);
   if (qs.viol) atomicAdd(&red[3], (unsigned long long)qs.viol);
+  if (qs.slow) atomicAdd(&red[5], (unsigned long long)qs.slow);
   __syncthreads();
-  if (threadIdx.x < 4 && red[threadIdx.x]) atomicAdd(&A.stats[threadIdx.x], red[threadIdx.x]);
+  if (threadIdx.x < 6 && threadIdx.x != 4 && red[threadIdx.x]) atomicAdd(&A.stats[threadIdx.x], red[threadIdx.x]);
 }
 
 __global__ void k_item_sk(ItemsSoA it, uint32_t K) {
