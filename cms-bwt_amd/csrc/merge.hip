@@ -609,32 +609,36 @@ struct LdsView {  // items and positions rebased to the window
   const unsigned long long* skL;
   const uint32_t* slotL;
   const uint32_t* pbL;
-  const uint32_t* fmL;
+  const uint4* fastL;
   const uint32_t* nhr;
   uint32_t iBeg, T0;
   __device__ uint32_t begin(uint32_t t) const { return pbL[t - T0] ; }
-  __device__ uint32_t fbeg(uint32_t t) const { return pbL[t - T0] + (fmL[t - T0] >> 16); }
+  __device__ uint32_t fbeg(uint32_t t) const { return pbL[t - T0] + ((fastL[t - T0].x >> 16) & 0x1fffu); }
   __device__ unsigned long long sk(uint32_t q) const { return skL[q - iBeg]; }
   __device__ uint32_t slot(uint32_t q) const { return slotL[q - iBeg]; }
 };
 
 constexpr uint32_t kWinItems = kWinSlots;  // staged items (= max slots) per window
 constexpr uint32_t kWinPositions = 1024;
+constexpr uint32_t kFsEnd = 0x40000000u, kFsSearch = 0x40000001u;
 
 template <bool CHECK>
 __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
   __shared__ uint32_t cnt[kWinItems + 64];              // 14 KB (+ one dummy per lane); per target the adds sum to <= H < 2^31
   __shared__ unsigned long long skL[kWinItems];         // 28 KB
   __shared__ uint32_t slotL[kWinItems + 1];             // 14 KB
-  // per target: its first item (pbL) and, packed in fmL, the offset of its
-  // first smaller=false item (bits 16..31) and its longest item len (bits
-  // 0..15, 0xffff = that long or longer)
-  __shared__ uint32_t pbL[kWinPositions + 1], fmL[kWinPositions];  // 8 KB
-  // fast test per target: x = bit 31 no items, bit 30 no smaller=false item,
-  // bits 0..11 the first smaller=false item's slot (window-relative);
-  // y = the longest smaller=true len (bits 0..15) and the first (longest)
-  // smaller=false len (bits 16..31), 0xffff: that long or longer
-  __shared__ uint2 fastL[kWinPositions];                            // 8 KB
+  // per target: its first item (pbL) and the fast-test record fastL:
+  //   x: bit 31 no items, bit 30 no smaller=false item, bit 29 no second
+  //      smaller=false item, bits 0..11 the first smaller=false item's slot
+  //      (window-relative), bits 16..28 its offset from the first item
+  //   y: the two longest smaller=true lens (the last two S items: bits 0..15
+  //      longest, 16..31 second), 0xffff: that long or longer
+  //   z: the two longest smaller=false lens (the first two F items: bits 0..15
+  //      first, 16..31 second)
+  //   w: slots (window-relative) of the last S item (bits 0..11) and of the
+  //      second F item (bits 16..27)
+  __shared__ uint32_t pbL[kWinPositions + 1];                       // 4 KB
+  __shared__ uint4 fastL[kWinPositions];                            // 16 KB
   __shared__ uint32_t qL[8][64];                                     // 2 KB: per-wave query queues
   __shared__ uint32_t s_next;
   __shared__ unsigned long long red[6];
@@ -657,18 +661,17 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
   if (lds) {
     for (uint32_t t = threadIdx.x; t < T1 - T0; t += blockDim.x) {
       const uint32_t b0 = pbL[t] - iBeg, b1 = pbL[t + 1] - iBeg, f = A.posF[T0 + t] - iBeg;
-      uint32_t m = 0;
-      for (uint32_t q = b0; q < b1; q++) {
-        const uint32_t hi = (uint32_t)(skL[q] >> 32);
-        m = max(m, q < f ? hi : ~hi);
-      }
-      fmL[t] = ((f - b0) << 16) | min(m, 0xffffu);
       // S items ascend by len, F items descend: the class maxima are the
-      // last S item and the first F item
-      const uint32_t mS = f > b0 ? (uint32_t)(skL[f - 1] >> 32) : 0u;
-      const uint32_t mF = f < b1 ? ~(uint32_t)(skL[f] >> 32) : 0u;
-      fastL[t] = make_uint2(b0 == b1 ? 0x80000000u : (f < b1 ? slotL[f] - sb : 0x40000000u),
-                            min(mS, 0xffffu) | (min(mF, 0xffffu) << 16));
+      // last S items and the first F items
+      auto sat = [](uint32_t v) { return min(v, 0xffffu); };
+      const uint32_t mS = f > b0 ? sat((uint32_t)(skL[f - 1] >> 32)) : 0u;
+      const uint32_t mS2 = f > b0 + 1 ? sat((uint32_t)(skL[f - 2] >> 32)) : 0u;
+      const uint32_t mF = f < b1 ? sat(~(uint32_t)(skL[f] >> 32)) : 0u;
+      const uint32_t mF2 = f + 1 < b1 ? sat(~(uint32_t)(skL[f + 1] >> 32)) : 0u;
+      const uint32_t x = (b0 == b1 ? 0x80000000u : 0u) | (f < b1 ? slotL[f] - sb : 0x40000000u) |
+                         (f + 1 < b1 ? 0u : 0x20000000u) | ((f - b0) << 16);
+      const uint32_t wv2 = (f > b0 ? slotL[f - 1] - sb : 0u) | (f + 1 < b1 ? (slotL[f + 1] - sb) << 16 : 0u);
+      fastL[t] = make_uint4(x, mS | (mS2 << 16), mF | (mF2 << 16), wv2);
     }
     __syncthreads();
   }
@@ -677,7 +680,7 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
   const uint32_t nItems = nCross + (iEnd - iBeg);
   const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   QueryStats qs;
-  const LdsView LV{skL, slotL, pbL, fmL, A.nhr, iBeg, T0};
+  const LdsView LV{skL, slotL, pbL, fastL, A.nhr, iBeg, T0};
   const GlobalView GV{&A.it, A.posBegin, A.posF, A.nhr};
   auto addLds = [&](uint32_t s, uint32_t v) { atomicAdd(&cnt[s - sb], v); };
   auto addGlb = [&](uint32_t s, uint32_t v) { atomicAdd(&A.counter[s], (unsigned long long)v); };
@@ -734,21 +737,32 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
         for (uint32_t t0 = lo; t0 <= hi; t0 += 64) {
           const uint32_t t = t0 + lane;
           const bool valid = t <= hi;
-          const uint2 fw = fastL[min(t, hi) - T0];
+          const uint4 fw = fastL[min(t, hi) - T0];
           const uint32_t L = E - t;
-          const uint32_t mS = fw.y & 0xffffu, mF = fw.y >> 16;
-          // a query longer than every item of its class lands on the first
+          const uint32_t mS = fw.y & 0xffffu, mS2 = fw.y >> 16, mF = fw.z & 0xffffu, mF2 = fw.z >> 16;
+          // A query longer than every item of its class lands on the first
           // smaller=false item (lower_bound past the smaller=true class, or
           // the first of a class sorted by len descending); an S query there
-          // is equal to it (operator== ignores `smaller`) only at its len
-          const bool fast = S ? (mS != 0xffffu && mF != 0xffffu && L > mS && L != mF) : (mF != 0xffffu && L > mF);
+          // is equal to it (operator== ignores `smaller`) only at its len.
+          // One between the two longest of its class lands on the longest S
+          // item (S) or on the second F item (F), equal to neither.
+          uint32_t dst = kFsEnd;  // kFsEnd: lower_bound == end (no add); kFsSearch: undecided
+          if (S) {
+            if (mS != 0xffffu && mF != 0xffffu && L > mS && L != mF) dst = fw.x & 0x40000fffu;
+            else if (mS != 0xffffu && L < mS && L > mS2) dst = fw.w & 0xfffu;
+            else dst = kFsSearch;
+          } else {
+            if (mF != 0xffffu && L > mF) dst = fw.x & 0x40000fffu;
+            else if (mF != 0xffffu && L < mF && L > mF2) dst = (fw.x & 0x20000000u) ? 0x40000000u : fw.w >> 16;
+            else dst = kFsSearch;
+          }
           const bool none = (fw.x & 0x80000000u) != 0;  // bucket >= 0: no heads at t (FN:1530)
-          const bool add = valid && !none && fast && !(fw.x & 0x40000000u);
-          const bool slow = valid && !none && !fast;
+          const bool add = valid && !none && dst < 0x40000000u;
+          const bool slow = valid && !none && dst == kFsSearch;
           qs.nothing += (valid && none) ? 1u : 0u;
           qs.good += add ? 1u : 0u;
           // every lane adds: the non-adding ones to a private dummy counter
-          atomicAdd(&cnt[add ? fw.x : kWinItems + lane], cq);
+          atomicAdd(&cnt[add ? dst : kWinItems + lane], cq);
           const uint64_t sm = __ballot(slow);
           if (sm) {
             const uint32_t c = (uint32_t)__popcll(sm), r = (uint32_t)__popcll(sm & ((1ull << lane) - 1));
