@@ -73,6 +73,9 @@ struct DevRef {
 constexpr uint32_t kPfxAns = 0x80000000u;
 constexpr uint32_t kPfxSingle = 0x40000000u;
 constexpr uint32_t kPfxSmaller = 0x20000000u;
+// an occurring P with one suffix holds (SA of it, kPfxOne | 1) instead of
+// (Start, 1): the walk's singleton extension starts at the reference position
+constexpr uint32_t kPfxOne = 0x40000000u;
 
 // One restart chunk of the MS walk: positions [a, b) of document `doc`.
 struct Chunk {

@@ -617,6 +617,7 @@ struct Engine {
       for (uint32_t l = 1; l <= K; l++)  // answer entries, level by level (each reads the level below)
         launch_ix_pfx_answer(dpfx.p + R.pfxOff[l], l > 1 ? dpfx.p + R.pfxOff[l - 1] : nullptr, 1ull << (B * l), B,
                              dsa.p, n, l, st);
+      for (uint32_t l = 1; l <= K; l++) launch_ix_pfx_one(dpfx.p + R.pfxOff[l], 1ull << (B * l), dsa.p, st);
       HIPCHK(hipGetLastError());
       sync();  // map/below are pageable
       R.pfx = dpfx.p;
@@ -676,6 +677,11 @@ struct Engine {
         o[2 * c] = (uint32_t)hix.sa[mm];
         o[2 * c + 1] = f | (l - 1);
       }
+    }
+    for (uint32_t l = 1; l <= K; l++) {  // k_ix_pfx_one
+      uint32_t* o = tab.data() + R.pfxOff[l];
+      for (uint64_t c = 0; c < (1ull << (B * l)); c++)
+        if (o[2 * c + 1] == 1u) { o[2 * c] = (uint32_t)hix.sa[o[2 * c]]; o[2 * c + 1] = kPfxOne | 1u; }
     }
     dpfx.alloc(total + 4);
     HIPCHK(hipMemcpyAsync(dpfx.p, tab.data(), (total + 4) * 4, hipMemcpyHostToDevice, st));
@@ -1485,6 +1491,7 @@ struct Engine {
         mk_dbl_small(gs.p, G, U, act.p, k64.p, val.p, saT.p, grp.p, keep.p, big.p, maxSmall, st);
         origB.alloc(U);
         const uint32_t B = select_flagged(io.p, big.p, origB.p, U);
+        if (env_u32("CMSBWT_DBL_STATS", 0)) fprintf(stderr, "[dbl] h %llu U %u groups %u big %u\n", (unsigned long long)hstep, U, G, B);
         if (B) {
           actB.alloc(B); valB.alloc(B); keyB.alloc(B); keepB.alloc(B);
           mk_dbl_gather_big(origB.p, B, act.p, k64.p, val.p, actB.p, keyB.p, valB.p, st);

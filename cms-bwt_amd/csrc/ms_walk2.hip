@@ -414,6 +414,9 @@ k_ms_walk2(Walk2Args A) {
     if (len == 0) { lb = 0; rb = (int32_t)n - 1; }
     else { lb = -1; rb = -2; }
   };
+  // text index of the 32 bytes a skip step loads: the next position after an
+  // exit inside the PLCP window lies at offset 0..16 of them
+  auto skip_text_base = [&]() -> uint32_t { return i + len + 1 >= 16 ? i + len - 15 : 0u; };
   auto skip_done = [&](uint32_t s) {
     i += s;
     len -= s;
@@ -595,6 +598,10 @@ k_ms_walk2(Walk2Args A) {
         const uint64_t TT = (uint64_t)pos + 1 + len;
         ad0 = P + 4ull * (TT >= 16 ? TT - 16 : 0);
         use = U0Q | U1Q | U4Q | U5Q;
+        if (R.pfxExact && R.pfx) {  // and the 32 text bytes around the match end: the next window
+          ad2 = T + skip_text_base();
+          use |= U2Q | U3Q;
+        }
       } else if (lb < 0) {  // unknown interval: the next position's probe supersedes contractLeft
         if (len == 0) { lb = 0; rb = (int32_t)n - 1; }
         phase = PC_ADV;
@@ -657,12 +664,45 @@ k_ms_walk2(Walk2Args A) {
     if (use & U5Q) v5 = ldu16(ad0 + 48);
     if (use & U0E) { const uint2 w = ld8(ad0); v0.x = w.x; v0.y = w.y; }
     if (use & U2E) { const uint2 w = ld8(ad2); v2.x = w.x; v2.y = w.y; }
+    // PLCP skip (FN:1176-1185): the exit inside the 16-entry window below
+    // the match end, if it is there (skS = the skip, or ~0u)
+    uint32_t skS = 0xffffffffu;
+    if (phase == PH_SKIP1) {
+      // entries Wb..Wb+15 below TT; PLCP[q] + q is non-decreasing, so the
+      // window decides when it starts at or below pos+1 or below the exit
+      const int64_t TT = (int64_t)pos + 1 + len, q0 = (int64_t)pos + 1;
+      const int64_t Wb = TT >= 16 ? TT - 16 : 0;
+      const uint32_t e[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
+                              v4.x, v4.y, v4.z, v4.w, v5.x, v5.y, v5.z, v5.w};
+      if (Wb <= q0 || (int64_t)(int32_t)e[0] + Wb < TT) {
+        int64_t qc = TT;  // first crossing (TT itself always crosses)
+#pragma unroll
+        for (int k = 15; k >= 0; k--) {
+          const int64_t q = Wb + k;
+          if (q >= q0 && q < TT && (int64_t)(int32_t)e[k] + q >= TT) qc = q;
+        }
+        skS = (uint32_t)(qc - q0);
+      }
+    }
     // the text window this step loaded (one call site: the code is emitted once)
     {
       const bool wa = phase == PH_PFX_TEXT || phase == PH_SKTXT;
-      if (wa || (phase == PH_PFX_PROBE && R.pfxExact)) {
-        const uint4 vv = make_uint4(wa ? v0.x : v2.x, wa ? v0.y : v2.y, wa ? v0.z : v2.z, wa ? v0.w : v2.w);
-        set_window(vv, phase == PH_PFX_TEXT ? i : i + 1);
+      const bool ws = phase == PH_SKIP1 && skS != 0xffffffffu && R.pfxExact && R.pfx && len - skS < R.kmerK;
+      if (wa || ws || (phase == PH_PFX_PROBE && R.pfxExact)) {
+        uint4 vv = make_uint4(wa ? v0.x : v2.x, wa ? v0.y : v2.y, wa ? v0.z : v2.z, wa ? v0.w : v2.w);
+        uint32_t at = phase == PH_PFX_TEXT ? i : i + 1;
+        if (ws) {  // bytes o..o+15 of the 32 loaded (v2, v3), o = next position - base
+          at = i + skS + 1;
+          const uint32_t o = at - skip_text_base();
+          uint32_t d[8] = {v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+          if (o & 16) { d[0] = d[4]; d[1] = d[5]; d[2] = d[6]; d[3] = d[7]; d[4] = d[5] = d[6] = d[7] = 0; }
+          if (o & 8) { d[0] = d[2]; d[1] = d[3]; d[2] = d[4]; d[3] = d[5]; d[4] = d[6]; d[5] = d[7]; }
+          if (o & 4) { d[0] = d[1]; d[1] = d[2]; d[2] = d[3]; d[3] = d[4]; d[4] = d[5]; }
+          const uint32_t sh = o & 3;
+          vv = make_uint4(__builtin_amdgcn_alignbyte(d[1], d[0], sh), __builtin_amdgcn_alignbyte(d[2], d[1], sh),
+                          __builtin_amdgcn_alignbyte(d[3], d[2], sh), __builtin_amdgcn_alignbyte(d[4], d[3], sh));
+        }
+        set_window(vv, at);
       }
     }
     // ---- one state-machine step (load phases)
@@ -756,20 +796,23 @@ k_ms_walk2(Walk2Args A) {
         break;
       }
       case PH_SKIP1: {
-        // entries Wb..Wb+15 below TT; PLCP[q] + q is non-decreasing, so the
-        // window decides when it starts at or below pos+1 or below the exit
         const int64_t TT = (int64_t)pos + 1 + len, q0 = (int64_t)pos + 1;
         const int64_t Wb = TT >= 16 ? TT - 16 : 0;
-        const uint32_t e[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
-                                v4.x, v4.y, v4.z, v4.w, v5.x, v5.y, v5.z, v5.w};
-        if (Wb <= q0 || (int64_t)(int32_t)e[0] + Wb < TT) {
-          int64_t qc = TT;  // first crossing (TT itself always crosses)
-#pragma unroll
-          for (int k = 15; k >= 0; k--) {
-            const int64_t q = Wb + k;
-            if (q >= q0 && q < TT && (int64_t)(int32_t)e[k] + q >= TT) qc = q;
+        if (skS != 0xffffffffu) {  // exit inside the window (scanned above)
+          if (R.pfxExact && R.pfx && len - skS < R.kmerK) {  // the window of the next position is decoded
+            i += skS;
+            len -= skS;
+            pos += skS;
+            if (wm == R.kmerK) {
+              virtual_interval();
+              phase = PC_ADV;
+              use = 0;
+            } else {
+              isa1();
+            }
+          } else {
+            skip_done(skS);
           }
-          skip_done((uint32_t)(qc - q0));
         } else {  // exit at or below Wb: PLCP[pos+1] first, then gallop
           phase = PH_SKIP0;
           ad0 = P + 4ull * (pos + 1);
@@ -899,6 +942,16 @@ k_ms_walk2(Walk2Args A) {
         const uint32_t m = (uint32_t)u7, code = (uint32_t)u6, Bb = R.kmerB;
         if (!R.pfxExact && len > 0 && (v2.x != (uint32_t)lb || v2.y != (uint32_t)(rb - lb) + 1)) {
           begin_bs();
+          break;
+        }
+        if (v0.y == (kPfxOne | 1u)) {  // t[i..i+m) occurs once, at v0.x: extend there (FN:52-62)
+          lb = rb = 0;
+          len = m;
+          pos = v0.x;
+          phase = PH_LCE;
+          ad0 = X + pos + len;
+          ad2 = T + i + len;
+          use = U0Q | U2Q;
           break;
         }
         if (!(v0.y & kPfxAns)) {  // t[i..i+m) occurs: its interval, depth m

@@ -141,7 +141,6 @@ void launch_ix_lcp(const uint8_t* x, const int32_t* sa, uint32_t n, uint32_t* is
   hipLaunchKernelGGL(k_ix_lcp_bwt, gidx((uint64_t)n + 1), dim3(256), 0, st, x, sa, n, plcpRaw, lcp, bwt);
   hipLaunchKernelGGL(k_ix_plcp_max, gidx(n), dim3(256), 0, st, isa, lcp, n, plcp);
 }
-
 }  // namespace cmsbwt
 
 // ---------------------------------------------------------------- walk tables
@@ -302,6 +301,17 @@ __global__ void k_ix_pfx_answer(uint32_t* __restrict__ tab, const uint32_t* __re
   tab[2 * c + 1] = f | (l - 1);
 }
 
+// after every level's answers: occurring strings with one suffix store its
+// reference position (kPfxOne)
+__global__ void k_ix_pfx_one(uint32_t* __restrict__ tab, uint64_t E, const int32_t* __restrict__ sa) {
+  const uint64_t c = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= E) return;
+  if (tab[2 * c + 1] == 1u) {
+    tab[2 * c] = (uint32_t)sa[tab[2 * c]];
+    tab[2 * c + 1] = kPfxOne | 1u;
+  }
+}
+
 static inline dim3 gix(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
 void launch_ix_plcp_check(const int32_t* plcp, uint32_t n, uint32_t* err, hipStream_t st) {
@@ -340,6 +350,9 @@ void launch_ix_pfx_write(const uint32_t* cfEx, const uint32_t* ctIn, const uint3
 void launch_ix_pfx_answer(uint32_t* tab, const uint32_t* par, uint64_t E, uint32_t B, const int32_t* sa, uint32_t n,
                           uint32_t l, hipStream_t st) {
   if (E) hipLaunchKernelGGL(k_ix_pfx_answer, gix(E), dim3(256), 0, st, tab, par, E, B, sa, n, l);
+}
+void launch_ix_pfx_one(uint32_t* tab, uint64_t E, const int32_t* sa, hipStream_t st) {
+  if (E) hipLaunchKernelGGL(k_ix_pfx_one, gix(E), dim3(256), 0, st, tab, E, sa);
 }
 
 }  // namespace cmsbwt
