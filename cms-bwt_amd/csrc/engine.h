@@ -1437,15 +1437,13 @@ struct Engine {
       inscan(mark.p, itemOfSlot.p, H, rocprim::plus<uint32_t>());
     }
     mk_slot_members(S, itemOfSlot.p, P.p, H, Pm.p, st);
-    DBuf<uint32_t> actv;
-    actv.alloc(H);
     {
       DBuf<uint32_t> rankBase, gBase;
       rankBase.alloc(n);
       gBase.alloc(n);
       mk_pos_rank_base(posBegin.p, sSlot.p, disa.p, itemRankBase.p, headBase.p, n, E, keepT ? rankBase.p : nullptr,
                        gBase.p, st);
-      mk_ranks_slot(S, itemOfSlot.p, Pm.p, H, rankBase.p, gBase.p, n, keepT ? T.p : nullptr, saT.p, grp.p, actv.p,
+      mk_ranks_slot(S, itemOfSlot.p, Pm.p, H, rankBase.p, gBase.p, n, keepT ? T.p : nullptr, saT.p, grp.p, nullptr,
                     st);
     }
     itemRankBase.release();
@@ -1455,45 +1453,45 @@ struct Engine {
     // ---- suffix sort of the head string (libsais_int, FN:1455-1459)
     {
       const int bH = bits_for(H);
-      // unresolved members' sa positions (resolved ones are 0xffffffff and
-      // sort to the end); U of them
+      const bool dstats = env_u32("CMSBWT_DBL_STATS", 0) != 0;
+      // unresolved members' sa positions, ascending (= SA rank, then map
+      // order): every group is a contiguous range of act
       DBuf<uint32_t> act, act2, val, val2, lab, labMax, keep;
-      act.alloc(H); act2.alloc(H);
       uint32_t U = 0;
       {
-        DBuf<uint32_t> cntU;
-        cntU.alloc(1);
-        size_t bb = 0;
-        HIPCHK(rocprim::select(nullptr, bb, actv.p, act2.p, cntU.p, (size_t)H, IsActive(), st));
-        HIPCHK(rocprim::select(scratch(bb), bb, actv.p, act2.p, cntU.p, (size_t)H, IsActive(), st));
-        U = read1(cntU.p);
+        DBuf<uint32_t> cntR, offR;
+        cntR.alloc(n);
+        offR.alloc(n);
+        cntR.zero(st);
+        mk_act_count(posBegin.p, sCount.p, disa.p, n, cntR.p, st);
+        exscan(cntR.p, offR.p, 0u, n);
+        U = read1(offR.p + (n - 1)) + read1(cntR.p + (n - 1));
+        act.alloc(std::max<uint32_t>(U, 1)); act2.alloc(std::max<uint32_t>(U, 1));
+        mk_act_fill(posBegin.p, sSlot.p, sCount.p, disa.p, headBase.p, offR.p, n, act.p, st);
       }
-      actv.release();
-      sort_keys(act2.p, act.p, U, bH);
       DBuf<uint64_t> k64, k64b;
       val.alloc(U); val2.alloc(U); lab.alloc(U); labMax.alloc(U); keep.alloc(U);
       k64.alloc(U); k64b.alloc(U);
-      // groups are visited in suffix-array order (a group's members take its
-      // sa positions in key order): act is sorted above, so every group is a
-      // contiguous range of act.  Groups of <= 32 members are sorted by one
-      // thread each; the members of larger groups by one radix sort.
+      // Group leaders sort groups of <= 32 members by one thread each; the
+      // members of larger groups go to one radix sort.
       const uint32_t maxSmall = env_u32("CMSBWT_DBL_SMALL", 32);
-      DBuf<uint32_t> gflag, gs, big, io, origB, actB, valB, keepB;
+      DBuf<uint32_t> gflag, bigList, origB, actB, valB, keepB;
       DBuf<uint64_t> keyB;
-      gflag.alloc(U); gs.alloc(U); big.alloc(U); io.alloc(U);
-      mk_iota(io.p, U, st);
+      gflag.alloc(U); bigList.alloc((uint64_t)U + 1);
       for (uint64_t hstep = 1; U > 0; hstep <<= 1) {
         if (hstep > H) throw InputError{CMSBWT_EINPUT, "internal: head-string suffix sort did not converge"};
         mk_dbl_keys(act.p, saT.p, grp.p, (uint32_t)hstep, U, k64.p, val.p, st);
         mk_dbl_gstart(k64.p, U, gflag.p, st);
-        const uint32_t G = select_flagged(io.p, gflag.p, gs.p, U);
-        HIPCHK(hipMemsetAsync(big.p, 0, (size_t)U * 4, st));
-        mk_dbl_small(gs.p, G, U, act.p, k64.p, val.p, saT.p, grp.p, keep.p, big.p, maxSmall, st);
-        origB.alloc(U);
-        const uint32_t B = select_flagged(io.p, big.p, origB.p, U);
-        if (env_u32("CMSBWT_DBL_STATS", 0)) fprintf(stderr, "[dbl] h %llu U %u groups %u big %u\n", (unsigned long long)hstep, U, G, B);
+        HIPCHK(hipMemsetAsync(bigList.p, 0, 4, st));
+        mk_dbl_small2(gflag.p, U, act.p, k64.p, val.p, saT.p, grp.p, keep.p, bigList.p, maxSmall, st);
+        const uint32_t B = read1(bigList.p);
+        if (dstats) fprintf(stderr, "[dbl] h %llu U %u big %u\n", (unsigned long long)hstep, U, B);
         if (B) {
-          actB.alloc(B); valB.alloc(B); keyB.alloc(B); keepB.alloc(B);
+          // big members were appended group by group in any group order: put
+          // them back in act order (the radix path maps sorted members onto
+          // ascending sa positions)
+          origB.alloc(B); actB.alloc(B); valB.alloc(B); keyB.alloc(B); keepB.alloc(B);
+          sort_keys(bigList.p + 1, origB.p, B, bits_for(U));
           mk_dbl_gather_big(origB.p, B, act.p, k64.p, val.p, actB.p, keyB.p, valB.p, st);
           sort_pairs(keyB.p, k64b.p, valB.p, val2.p, B, 32 + bH);
           mk_dbl_apply(actB.p, k64b.p, val2.p, B, saT.p, lab.p, st);

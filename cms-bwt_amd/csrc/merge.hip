@@ -322,6 +322,78 @@ __global__ void k_dbl_small(const uint32_t* __restrict__ gs, uint32_t G, uint32_
     keep[u] = (rs == u && endRun) ? 0u : 1u;
   }
 }
+// Unresolved members (items with >= 2 heads, end phrases excluded) in sa
+// position order, without a sort: per position p its count at rank ISA[p],
+// then each position writes its members' sa positions at its rank's offset.
+__global__ void k_act_count(const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ count,
+                            const uint32_t* __restrict__ isaRef, uint32_t n, uint32_t* __restrict__ cntR) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p + 1 >= n) return;  // position n-1: end phrases, ranked one by one
+  const uint32_t b = posBegin[p], e = posBegin[p + 1];
+  uint32_t c = 0;
+  for (uint32_t q = b; q < e; q++) {
+    const uint32_t k = count[q];
+    c += k >= 2 ? k : 0u;
+  }
+  if (c) cntR[isaRef[p]] = c;
+}
+__global__ void k_act_fill(const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ slot,
+                           const uint32_t* __restrict__ count, const uint32_t* __restrict__ isaRef,
+                           const uint32_t* __restrict__ headBase, const uint32_t* __restrict__ offR, uint32_t n,
+                           uint32_t* __restrict__ act) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p + 1 >= n) return;
+  const uint32_t b = posBegin[p], e = posBegin[p + 1];
+  if (b == e) return;
+  const uint32_t r = isaRef[p];
+  uint32_t o = offR[r];
+  const uint32_t g0 = 1 + headBase[r] - slot[b];
+  for (uint32_t q = b; q < e; q++) {
+    const uint32_t k = count[q];
+    if (k < 2) continue;
+    const uint32_t g = g0 + slot[q];
+    for (uint32_t m = 0; m < k; m++) act[o++] = g + m;
+  }
+}
+
+// Group leaders (gflag) sort their group when it has <= maxSmall members;
+// members of larger groups are appended to bigList (group by group) for the
+// radix path (bigList[0] counts them).
+__global__ void k_dbl_small2(const uint32_t* __restrict__ gflag, uint32_t U, const uint32_t* __restrict__ act,
+                             uint64_t* __restrict__ key, uint32_t* __restrict__ val, uint32_t* __restrict__ sa,
+                             uint32_t* __restrict__ grp, uint32_t* __restrict__ keep, uint32_t* __restrict__ bigList,
+                             uint32_t maxSmall) {
+  const uint32_t u0 = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u0 >= U || !gflag[u0]) return;
+  uint32_t u1 = u0 + 1;
+  while (u1 < U && !gflag[u1]) u1++;
+  if (u1 - u0 > maxSmall) {
+    const uint32_t o = atomicAdd(bigList, u1 - u0);
+    for (uint32_t u = u0; u < u1; u++) bigList[1 + o + (u - u0)] = u;
+    return;
+  }
+  for (uint32_t a = u0 + 1; a < u1; a++) {  // insertion sort by (label, label of suffix + h)
+    const uint64_t kk = key[a];
+    const uint32_t vv = val[a];
+    uint32_t b = a;
+    while (b > u0 && key[b - 1] > kk) {
+      key[b] = key[b - 1];
+      val[b] = val[b - 1];
+      b--;
+    }
+    key[b] = kk;
+    val[b] = vv;
+  }
+  uint32_t rs = u0;
+  for (uint32_t u = u0; u < u1; u++) {
+    if (u > u0 && key[u] != key[u - 1]) rs = u;
+    const bool endRun = u + 1 == u1 || key[u + 1] != key[u];
+    sa[act[u]] = val[u];
+    grp[val[u]] = act[rs];
+    keep[u] = (rs == u && endRun) ? 0u : 1u;
+  }
+}
+
 __global__ void k_dbl_gather_big(const uint32_t* __restrict__ orig, uint32_t B, const uint32_t* __restrict__ act,
                                  const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
                                  uint32_t* __restrict__ actB, uint64_t* __restrict__ keyB, uint32_t* __restrict__ valB) {
@@ -403,7 +475,7 @@ __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ ite
     if (T) T[idx] = (int32_t)(1 + m);
     sa[1 + m] = idx;
     grp[idx] = 1 + m;
-    actv[s] = 0xffffffffu;
+    if (actv) actv[s] = 0xffffffffu;
     return;
   }
   const uint32_t g = gBase[p] + sq;
@@ -411,7 +483,7 @@ __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ ite
   sa[g + m] = idx;
   grp[idx] = g;
   // unresolved members (items with >= 2 heads): their sa positions
-  actv[s] = it.count[q] >= 2 ? g + m : 0xffffffffu;
+  if (actv) actv[s] = it.count[q] >= 2 ? g + m : 0xffffffffu;
 }
 // next-head rank of each member, in slot order (FN:1480-1494): first per head
 // in document order (nexthead is small, so headRank[idx + nexthead] is read
@@ -1227,6 +1299,18 @@ void mk_dbl_gstart(const uint64_t* key, uint32_t U, uint32_t* flag, hipStream_t 
 void mk_dbl_small(const uint32_t* gs, uint32_t G, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val,
                   uint32_t* sa, uint32_t* grp, uint32_t* keep, uint32_t* big, uint32_t maxSmall, hipStream_t st) {
   if (G) hipLaunchKernelGGL(k_dbl_small, g1(G), dim3(256), 0, st, gs, G, U, act, key, val, sa, grp, keep, big, maxSmall);
+}
+void mk_act_count(const uint32_t* posBegin, const uint32_t* count, const uint32_t* isaRef, uint32_t n, uint32_t* cntR,
+                  hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_act_count, g1(n), dim3(256), 0, st, posBegin, count, isaRef, n, cntR);
+}
+void mk_act_fill(const uint32_t* posBegin, const uint32_t* slot, const uint32_t* count, const uint32_t* isaRef,
+                 const uint32_t* headBase, const uint32_t* offR, uint32_t n, uint32_t* act, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_act_fill, g1(n), dim3(256), 0, st, posBegin, slot, count, isaRef, headBase, offR, n, act);
+}
+void mk_dbl_small2(const uint32_t* gflag, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val, uint32_t* sa,
+                   uint32_t* grp, uint32_t* keep, uint32_t* bigList, uint32_t maxSmall, hipStream_t st) {
+  if (U) hipLaunchKernelGGL(k_dbl_small2, g1(U), dim3(256), 0, st, gflag, U, act, key, val, sa, grp, keep, bigList, maxSmall);
 }
 void mk_dbl_gather_big(const uint32_t* orig, uint32_t B, const uint32_t* act, const uint64_t* key, const uint32_t* val,
                        uint32_t* actB, uint64_t* keyB, uint32_t* valB, hipStream_t st) {

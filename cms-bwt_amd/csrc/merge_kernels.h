@@ -82,6 +82,12 @@ void mk_head_ranks(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint32_
 void mk_map_order(const uint32_t* posBegin, const uint32_t* len, const uint8_t* sm, uint32_t n, uint32_t* order,
                   hipStream_t st);
 // per-group doubling round (small groups sorted by one thread each)
+void mk_act_count(const uint32_t* posBegin, const uint32_t* count, const uint32_t* isaRef, uint32_t n, uint32_t* cntR,
+                  hipStream_t st);
+void mk_act_fill(const uint32_t* posBegin, const uint32_t* slot, const uint32_t* count, const uint32_t* isaRef,
+                 const uint32_t* headBase, const uint32_t* offR, uint32_t n, uint32_t* act, hipStream_t st);
+void mk_dbl_small2(const uint32_t* gflag, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val, uint32_t* sa,
+                   uint32_t* grp, uint32_t* keep, uint32_t* bigList, uint32_t maxSmall, hipStream_t st);
 void mk_dbl_gstart(const uint64_t* key, uint32_t U, uint32_t* flag, hipStream_t st);
 void mk_dbl_small(const uint32_t* gs, uint32_t G, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val,
                   uint32_t* sa, uint32_t* grp, uint32_t* keep, uint32_t* big, uint32_t maxSmall, hipStream_t st);
