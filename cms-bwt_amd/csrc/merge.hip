@@ -372,6 +372,37 @@ __global__ void k_dbl_small2(const uint32_t* __restrict__ gflag, uint32_t U, con
     for (uint32_t u = u0; u < u1; u++) bigList[1 + o + (u - u0)] = u;
     return;
   }
+  if (u1 - u0 <= 4) {  // the common case: a sorting network in registers
+    uint64_t k[4];
+    uint32_t v[4], a4[4];
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      const bool in = u0 + j < u1;
+      k[j] = in ? key[u0 + j] : ~0ull;
+      v[j] = in ? val[u0 + j] : 0u;
+      a4[j] = in ? act[u0 + j] : 0u;
+    }
+    auto cs = [&](int x, int y) {
+      if (k[y] < k[x]) {
+        const uint64_t tk = k[x]; k[x] = k[y]; k[y] = tk;
+        const uint32_t tv = v[x]; v[x] = v[y]; v[y] = tv;
+      }
+    };
+    cs(0, 1); cs(2, 3); cs(0, 2); cs(1, 3); cs(1, 2);
+    // (equal keys stay in one group: their order is settled by later rounds)
+    uint32_t rs = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < 4; j++) {
+      if (u0 + j < u1) {
+        if (j > 0 && k[j] != k[j - 1]) rs = j;
+        const bool endRun = u0 + j + 1 == u1 || k[j + 1 < 4 ? j + 1 : 3] != k[j];
+        sa[a4[j]] = v[j];
+        grp[v[j]] = a4[rs];
+        keep[u0 + j] = (rs == j && endRun) ? 0u : 1u;
+      }
+    }
+    return;
+  }
   for (uint32_t a = u0 + 1; a < u1; a++) {  // insertion sort by (label, label of suffix + h)
     const uint64_t kk = key[a];
     const uint32_t vv = val[a];
