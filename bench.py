@@ -62,7 +62,10 @@ def cpu_baseline(ref_len, copies, p, seed, rle=True):
             "seconds": round(t_coll, 3)}
 
 
-def pmc_traffic(args):
+PMC_FILE = "r02_pmc.json"  # tools/gpu_prof_r.sh + tools/pmc_main.py
+
+
+def pmc_traffic(args, kernel="k_ms_walk2"):
     """Beyond-L2 bytes per launch of the walk kernel from the committed PMC
     summary (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes, KiB
     units; tools/gpu_prof.sh), for the default workload only.  Per
@@ -70,14 +73,14 @@ def pmc_traffic(args):
     the bytes of 128-B requests on gfx950, so it is doubled; both counters
     include Infinity-Cache hits."""
     default = (args.ref_len, args.copies, args.p, args.seed) == (10_000_000, 1000, 0.001, 4)
-    path = os.path.join(ROOT, "profiles", "r01_pmc.json")
+    path = os.path.join(ROOT, "profiles", PMC_FILE)
     if not default or not os.path.exists(path):
         return None, None
     try:
-        d = json.load(open(path))["k_ms_walk2"]
-        b = (2 * d["FETCH_SIZE"]["per_launch"] + d["WRITE_SIZE"]["per_launch"]) * 1024.0
-        return int(b), "profiles/r01_pmc.json (2 x FETCH_SIZE + WRITE_SIZE per launch)"
-    except (KeyError, ValueError):
+        d = json.load(open(path))[kernel]
+        b = (2 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
+        return int(b), f"profiles/{PMC_FILE} (2 x FETCH_SIZE + WRITE_SIZE of the launch)"
+    except (KeyError, ValueError, TypeError):
         return None, None
 
 
@@ -164,6 +167,8 @@ def main():
     t_ms = st.ms_walk_kernel_ms / 1e3
     achieved = b_ms / t_ms / 1e9 if t_ms > 0 else 0.0
     traffic, traffic_src = pmc_traffic(args) if world == 1 else (None, None)
+    ctraffic, _ = pmc_traffic(args, "k_counter_win") if world == 1 else (None, None)
+    c_ms = st.counter_kernel_ms
     out = {
         "metric": ("collection MB/s to .bwt" if args.plain else
                    "collection MB/s to .rl_bwt (10 MB ref + 1000 copies @0.1% SNP)"),
@@ -184,7 +189,16 @@ def main():
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
                      "algorithmic_bytes": b_ms, "kernel_ms": round(st.ms_walk_kernel_ms, 3),
-                     "bytes_model": "22 B/char + 24 B/head (SURVEY.md §8d)"},
+                     "bytes_model": "22 B/char + 24 B/head (SURVEY.md §8d); the walk skips the "
+                                    "reference's per-character streams, so achieved can exceed the peak",
+                     "traffic_GBps": round(traffic / t_ms / 1e9, 1) if traffic and t_ms > 0 else None,
+                     "traffic_frac": round(traffic / t_ms / 1e9 / HBM_PEAK_GBS, 4) if traffic and t_ms > 0 else None},
+        # the merge's largest kernel (counterSmallerThanHead, FN:1523-1603):
+        # LDS- and VALU-bound, measured HBM traffic for reference
+        "counter_kernel": {"kernel": "k_counter_win", "kernel_ms": round(c_ms, 3),
+                           "queries": int(st.counter_good + st.counter_bad + st.counter_nothing),
+                           "traffic": ctraffic,
+                           "traffic_GBps": round(ctraffic / (c_ms / 1e3) / 1e9, 1) if ctraffic and c_ms > 0 else None},
         "stages_ms": {"ms_walk": round(st.t_ms_walk_s * 1e3, 2), "merge": round(st.t_merge_s * 1e3, 2),
                       "ms_walk_kernel": round(st.ms_walk_kernel_ms, 2),
                       "counter_kernel": round(st.counter_kernel_ms, 2)},
