@@ -54,6 +54,9 @@ struct LastNonEmpty {  // scan operator: the later non-empty unit's (has, last, 
 struct WidenU64 {
   __host__ __device__ uint64_t operator()(uint32_t v) const { return (uint64_t)v; }
 };
+struct PlusOneU64 {
+  __host__ __device__ unsigned long long operator()(unsigned long long v) const { return v + 1; }
+};
 
 struct HipError {
   std::string msg;
@@ -1378,6 +1381,32 @@ struct Engine {
     crossings = ncross;
   }
 
+  // per-SA-rank writer (one thread per unit), kept for A/B (CMSBWT_UNIT_WRITER=1)
+  void unit_writer(int rle, uint32_t E, DBuf<uint32_t>& posBegin, DBuf<uint32_t>& sSlot, DBuf<uint32_t>& sCount,
+                   DBuf<uint32_t>& headBase, uint64_t& Rn, uint64_t& symbols, DBuf<unsigned long long>& runStart,
+                   DBuf<uint8_t>& runChar) {
+    const uint32_t n = R.n;
+    WriterIn wi{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, sCount.p, headBase.p, bwtHeads.p, counter.p,
+                n, E, rle};
+    // units: the E end phrases, then SA ranks 1..n-1; runs counted per unit,
+    // joined across unit boundaries, emitted as (start, char) and packed
+    const uint64_t U64 = (uint64_t)E + n - 1;
+    if (U64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer units"};
+    const uint32_t Uw = (uint32_t)U64;
+    DBuf<uint32_t> wruns, whl, wprev;
+    DBuf<unsigned long long> wsym, wrunOff, wsymOff;
+    wruns.alloc(Uw); whl.alloc(Uw); wprev.alloc(Uw); wsym.alloc(Uw); wrunOff.alloc(Uw); wsymOff.alloc(Uw);
+    mk_wr_count(wi, Uw, wruns.p, wsym.p, whl.p, st);
+    exscan(whl.p, wprev.p, 0u, Uw, LastNonEmpty());
+    mk_wr_adjust(whl.p, wprev.p, Uw, wruns.p, st);
+    auto runs64 = rocprim::make_transform_iterator(wruns.p, WidenU64());
+    exscan(runs64, wrunOff.p, 0ull, Uw);
+    exscan(wsym.p, wsymOff.p, 0ull, Uw);
+    Rn = read1(wrunOff.p + (Uw - 1)) + read1(wruns.p + (Uw - 1));
+    symbols = read1(wsymOff.p + (Uw - 1)) + read1(wsym.p + (Uw - 1));
+    runStart.alloc(std::max<uint64_t>(Rn, 1)); runChar.alloc(std::max<uint64_t>(Rn, 1));
+    mk_wr_emit(wi, Uw, wrunOff.p, wsymOff.p, wprev.p, runStart.p, runChar.p, st);
+  }
   void merge(int rle) {
     if (!walked) throw InputError{CMSBWT_EARG, "run ms_walk first"};
     // Zero heads: the j-scan's `phrasesVector.size() - 1` (FN:1359) wraps and
@@ -1523,7 +1552,6 @@ struct Engine {
     }
     headRank.release();
     Pm.release();
-    itemOfSlot.release();
 
     // ---- counterSmallerThanHead (FN:1523-1603)
     counter.alloc((uint64_t)H + 1);
@@ -1570,28 +1598,45 @@ struct Engine {
     }
 
     // ---- writer (FN:1631-1777) as segments + run-length merge
-    WriterIn wi{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, sCount.p, headBase.p, bwtHeads.p, counter.p,
-                n, E, rle};
-    // units: the E end phrases, then SA ranks 1..n-1; runs counted per unit,
-    // joined across unit boundaries, emitted as (start, char) and packed
-    const uint64_t U64 = (uint64_t)E + n - 1;
-    if (U64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer units"};
-    const uint32_t Uw = (uint32_t)U64;
-    DBuf<uint32_t> wruns, whl, wprev;
-    DBuf<unsigned long long> wsym, wrunOff, wsymOff;
-    wruns.alloc(Uw); whl.alloc(Uw); wprev.alloc(Uw); wsym.alloc(Uw); wrunOff.alloc(Uw); wsymOff.alloc(Uw);
-    mk_wr_count(wi, Uw, wruns.p, wsym.p, whl.p, st);
-    exscan(whl.p, wprev.p, 0u, Uw, LastNonEmpty());
-    mk_wr_adjust(whl.p, wprev.p, Uw, wruns.p, st);
-    auto runs64 = rocprim::make_transform_iterator(wruns.p, WidenU64());
-    exscan(runs64, wrunOff.p, 0ull, Uw);
-    exscan(wsym.p, wsymOff.p, 0ull, Uw);
-    const uint64_t Rn = read1(wrunOff.p + (Uw - 1)) + read1(wruns.p + (Uw - 1));
-    const uint64_t symbols = read1(wsymOff.p + (Uw - 1)) + read1(wsym.p + (Uw - 1));
+    uint64_t Rn = 0, symbols = 0;
     DBuf<unsigned long long> runStart;
     DBuf<uint8_t> runChar;
-    runStart.alloc(std::max<uint64_t>(Rn, 1)); runChar.alloc(std::max<uint64_t>(Rn, 1));
-    mk_wr_emit(wi, Uw, wrunOff.p, wsymOff.p, wprev.p, runStart.p, runChar.p, st);
+    if (env_u32("CMSBWT_UNIT_WRITER", 0)) {
+      itemOfSlot.release();
+      unit_writer(rle, E, posBegin, sSlot, sCount, headBase, Rn, symbols, runStart, runChar);
+    } else {
+      // elements: end phrases, then per SA rank its heads (or one element)
+      DBuf<uint32_t> m, eBase;
+      m.alloc(n); eBase.alloc(n);
+      mk_el_count(headBase.p, n, E, H, m.p, st);
+      exscan(m.p, eBase.p, 0u, n);
+      const uint64_t V64 = (uint64_t)read1(eBase.p + (n - 1)) + read1(m.p + (n - 1));
+      if (V64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer elements"};
+      const uint32_t V = (uint32_t)V64;
+      DBuf<uint32_t> rOf;
+      rOf.alloc(V);
+      mk_el_rof(eBase.p, m.p, n, rOf.p, st);
+      m.release();
+      DBuf<unsigned long long> cum;
+      cum.alloc(H);
+      inscan(rocprim::make_transform_iterator(counter.p, PlusOneU64()), cum.p, H, rocprim::plus<unsigned long long>());
+      ElemIn ei{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, itemOfSlot.p, headBase.p, eBase.p, rOf.p, bwtHeads.p,
+                counter.p, cum.p, n, E, H, rle};
+      DBuf<uint32_t> wruns, whl, wprev;
+      DBuf<unsigned long long> wsym, wrunOff, wsymOff;
+      wruns.alloc(V); whl.alloc(V); wprev.alloc(V); wsym.alloc(V); wrunOff.alloc(V); wsymOff.alloc(V);
+      mk_el_wr_count(ei, V, wruns.p, wsym.p, whl.p, st);
+      exscan(whl.p, wprev.p, 0u, V, LastNonEmpty());
+      mk_wr_adjust(whl.p, wprev.p, V, wruns.p, st);
+      auto runs64 = rocprim::make_transform_iterator(wruns.p, WidenU64());
+      exscan(runs64, wrunOff.p, 0ull, V);
+      exscan(wsym.p, wsymOff.p, 0ull, V);
+      Rn = read1(wrunOff.p + (V - 1)) + read1(wruns.p + (V - 1));
+      symbols = read1(wsymOff.p + (V - 1)) + read1(wsym.p + (V - 1));
+      runStart.alloc(std::max<uint64_t>(Rn, 1)); runChar.alloc(std::max<uint64_t>(Rn, 1));
+      mk_el_wr_emit(ei, V, wrunOff.p, wsymOff.p, wprev.p, runStart.p, runChar.p, st);
+      itemOfSlot.release();
+    }
     runs.alloc(Rn * 9);
     mk_wr_records(runStart.p, runChar.p, Rn, symbols, runs.p, st);
     HIPCHK(hipGetLastError());

@@ -1142,6 +1142,109 @@ __global__ void k_wr_records(const unsigned long long* __restrict__ runStart, co
   o[8] = runChar[j];
 }
 
+// ---- element writer (one GPU): the same segments as d_unit_segments, one
+// thread per writer element instead of per SA rank.  Elements in output
+// order: the E end phrases (rank 0), then per SA rank r >= 1 its heads in
+// head-rank order (= slot order of its position), or one element when it has
+// none.  A rank's heads are contiguous in every array the thread reads
+// (counter and cum by slot, bwtHeads by head rank), so a wave reads
+// contiguous memory whatever the head count of its ranks; the per-rank loops
+// of k_wr_count/k_wr_emit diverged over 1..1000+ heads per thread.
+struct ElemArgs {
+  const int32_t* sa;
+  const uint8_t* bwt;
+  const int64_t* bucket;
+  const uint32_t* posBegin;
+  const uint32_t* slot;
+  const uint32_t* itemOfSlot;
+  const uint32_t* headBase;            // per SA rank (n), exclusive head counts
+  const uint32_t* elemBase;            // per SA rank (n), exclusive element counts
+  const uint32_t* rOf;                 // per element: its SA rank
+  const uint8_t* bwtHeads;
+  const unsigned long long* counter;   // by slot
+  const unsigned long long* cum;       // by slot: inclusive sum of counter + 1
+  uint32_t n, E, H;
+  int rle;
+};
+
+template <class F>
+__device__ __forceinline__ void d_elem_segments(const ElemArgs& A, uint32_t e, F&& f) {
+  const uint32_t r = A.rOf[e];
+  const uint32_t k = e - A.elemBase[r];
+  if (r == 0) { f(A.bwtHeads[k], 1ull); return; }  // end phrases (units u < E)
+  const uint32_t p = (uint32_t)A.sa[r];
+  const uint8_t c = A.bwt[r];
+  const int64_t b = A.bucket[p];
+  if (b > 0) { if (k == 0) f(c, (unsigned long long)b); return; }
+  if (b == 0) return;
+  const uint32_t hb = A.headBase[r];
+  const uint32_t nh = (r + 1 < A.n ? A.headBase[r + 1] : A.H) - hb;
+  if (nh == 0) {  // no items: the item loop is empty (FN:1761-1770 / 1678-1686)
+    if (!A.rle) f(c, (unsigned long long)(-b));
+    return;
+  }
+  const uint32_t s0 = A.slot[A.posBegin[p]], s = s0 + k;
+  const unsigned long long cs = A.counter[s];
+  if (cs) f(c, cs);
+  f(A.bwtHeads[hb + k], 1ull);
+  const bool last = A.rle ? (s + 1 >= A.H || A.itemOfSlot[s + 1] != A.itemOfSlot[s]) : k + 1 == nh;
+  if (last) {
+    const int64_t acc = b + (int64_t)(A.cum[s] - (s0 ? A.cum[s0 - 1] : 0ull));
+    if (A.rle ? acc != 0 : acc < 0) f(c, (unsigned long long)(-acc));
+  }
+}
+
+// elements per SA rank: E at rank 0, otherwise max(heads, 1)
+__global__ void k_el_count(const uint32_t* __restrict__ headBase, uint32_t n, uint32_t E, uint32_t H,
+                           uint32_t* __restrict__ m) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint32_t nh = (r + 1 < n ? headBase[r + 1] : H) - headBase[r];
+  m[r] = r == 0 ? E : max(nh, 1u);
+}
+__global__ void k_el_rof(const uint32_t* __restrict__ elemBase, const uint32_t* __restrict__ m, uint32_t n,
+                         uint32_t* __restrict__ rOf) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint32_t b = elemBase[r], c = m[r];
+  for (uint32_t k = 0; k < c; k++) rOf[b + k] = r;
+}
+__global__ void k_el_wr_count(ElemArgs A, uint32_t V, uint32_t* __restrict__ runs, unsigned long long* __restrict__ sym,
+                              uint32_t* __restrict__ hl) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= V) return;
+  int prev = -1, first = -1;
+  uint32_t nr = 0;
+  unsigned long long ns = 0;
+  d_elem_segments(A, e, [&](uint8_t c, unsigned long long cnt) {
+    if (first < 0) first = c;
+    if ((int)c != prev) nr++;
+    prev = c;
+    ns += cnt;
+  });
+  runs[e] = nr;
+  sym[e] = ns;
+  hl[e] = first < 0 ? 0u : (1u << 16) | ((uint32_t)prev << 8) | (uint32_t)first;
+}
+__global__ void k_el_wr_emit(ElemArgs A, uint32_t V, const unsigned long long* __restrict__ runOff,
+                             const unsigned long long* __restrict__ symOff, const uint32_t* __restrict__ prevHL,
+                             unsigned long long* __restrict__ runStart, uint8_t* __restrict__ runChar) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= V) return;
+  const uint32_t pv = prevHL[e];
+  int prev = (pv >> 16) ? (int)((pv >> 8) & 0xff) : -1;
+  unsigned long long j = runOff[e], pos = symOff[e];
+  d_elem_segments(A, e, [&](uint8_t c, unsigned long long cnt) {
+    if ((int)c != prev) {
+      runStart[j] = pos;
+      runChar[j] = c;
+      j++;
+    }
+    prev = c;
+    pos += cnt;
+  });
+}
+
 __global__ void k_seg_count(WriterArgs A, unsigned long long* __restrict__ segN) {
   uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r >= A.n) return;
@@ -1419,6 +1522,25 @@ void mk_wr_adjust(const uint32_t* hl, const uint32_t* prevHL, uint32_t U, uint32
 void mk_wr_emit(const WriterIn& w, uint32_t U, const unsigned long long* runOff, const unsigned long long* symOff,
                 const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st) {
   if (U) hipLaunchKernelGGL(k_wr_emit, g1(U), dim3(256), 0, st, writer_args(w), U, runOff, symOff, prevHL, runStart,
+                            runChar);
+}
+static ElemArgs elem_args(const ElemIn& w) {
+  return ElemArgs{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.itemOfSlot, w.headBase, w.elemBase, w.rOf,
+                  w.bwtHeads, w.counter, w.cum, w.n, w.E, w.H, w.rle};
+}
+void mk_el_count(const uint32_t* headBase, uint32_t n, uint32_t E, uint32_t H, uint32_t* m, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_el_count, g1(n), dim3(256), 0, st, headBase, n, E, H, m);
+}
+void mk_el_rof(const uint32_t* elemBase, const uint32_t* m, uint32_t n, uint32_t* rOf, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_el_rof, g1(n), dim3(256), 0, st, elemBase, m, n, rOf);
+}
+void mk_el_wr_count(const ElemIn& w, uint32_t V, uint32_t* runs, unsigned long long* sym, uint32_t* hl,
+                    hipStream_t st) {
+  if (V) hipLaunchKernelGGL(k_el_wr_count, g1(V), dim3(256), 0, st, elem_args(w), V, runs, sym, hl);
+}
+void mk_el_wr_emit(const ElemIn& w, uint32_t V, const unsigned long long* runOff, const unsigned long long* symOff,
+                   const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st) {
+  if (V) hipLaunchKernelGGL(k_el_wr_emit, g1(V), dim3(256), 0, st, elem_args(w), V, runOff, symOff, prevHL, runStart,
                             runChar);
 }
 void mk_wr_records(const unsigned long long* runStart, const uint8_t* runChar, uint64_t R, unsigned long long total,

@@ -118,6 +118,29 @@ void mk_wr_emit(const WriterIn& w, uint32_t U, const unsigned long long* runOff,
                 const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st);
 void mk_wr_records(const unsigned long long* runStart, const uint8_t* runChar, uint64_t R, unsigned long long total,
                    uint8_t* out, hipStream_t st);
+// element writer (one GPU): one thread per end phrase / head / head-less SA rank
+struct ElemIn {
+  const int32_t* sa;
+  const uint8_t* bwt;
+  const int64_t* bucket;
+  const uint32_t* posBegin;
+  const uint32_t* slot;
+  const uint32_t* itemOfSlot;
+  const uint32_t* headBase;
+  const uint32_t* elemBase;
+  const uint32_t* rOf;
+  const uint8_t* bwtHeads;
+  const unsigned long long* counter;
+  const unsigned long long* cum;  // inclusive scan of counter + 1 over slots
+  uint32_t n, E, H;
+  int rle;
+};
+void mk_el_count(const uint32_t* headBase, uint32_t n, uint32_t E, uint32_t H, uint32_t* m, hipStream_t st);
+void mk_el_rof(const uint32_t* elemBase, const uint32_t* m, uint32_t n, uint32_t* rOf, hipStream_t st);
+void mk_el_wr_count(const ElemIn& w, uint32_t V, uint32_t* runs, unsigned long long* sym, uint32_t* hl,
+                    hipStream_t st);
+void mk_el_wr_emit(const ElemIn& w, uint32_t V, const unsigned long long* runOff, const unsigned long long* symOff,
+                   const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st);
 void mk_seg_count(const WriterIn& w, unsigned long long* segN, hipStream_t st);
 void mk_seg_emit(const WriterIn& w, const unsigned long long* segOff, uint8_t* sc, unsigned long long* sn,
                  hipStream_t st);
