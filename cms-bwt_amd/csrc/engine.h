@@ -54,6 +54,11 @@ struct LastNonEmpty {  // scan operator: the later non-empty unit's (has, last, 
 struct WidenU64 {
   __host__ __device__ uint64_t operator()(uint32_t v) const { return (uint64_t)v; }
 };
+struct MakeHeadKV {  // head idx -> its grouping fields
+  const uint32_t* len;
+  const uint32_t* isa;
+  __host__ __device__ HeadKV operator()(uint32_t i) const { return HeadKV{i, len[i], isa[i]}; }
+};
 struct PlusOneU64 {
   __host__ __device__ unsigned long long operator()(unsigned long long v) const { return v + 1; }
 };
@@ -1244,8 +1249,47 @@ struct Engine {
     DBuf<uint32_t>& perm2 = S.P;
     perm.alloc(H); perm2.alloc(H); key.alloc(H); key2.alloc(H);
     DBuf<unsigned long long> gk, gk2;
-    mk_iota(perm.p, H, st);
-    if (packed) {  // one sort on the composite key
+    const bool posFirst = packed && !env_u32("CMSBWT_GROUP64", 0);
+    if (!posFirst) mk_iota(perm.p, H, st);
+    if (posFirst) {
+      // position first: one stable radix sort by pos (3 passes of 8 bits at
+      // n = 1e7) carrying (idx, len, isaNext), then each position's segment
+      // (~10 heads) sorted by (len, isaNext); long segments by a radix sort
+      gk2.alloc(H);
+      {
+        DBuf<uint32_t> posS, hb;
+        DBuf<HeadKV> kv;
+        posS.alloc(H); kv.alloc(H); hb.alloc((uint64_t)n + 1);
+        auto kvIn = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint32_t>(0u),
+                                                     MakeHeadKV{h.len, h.isa});
+        size_t b = 0;
+        HIPCHK(rocprim::radix_sort_pairs(nullptr, b, h.pos, posS.p, kvIn, kv.p, (size_t)H, 0u, (unsigned)bN, st));
+        HIPCHK(rocprim::radix_sort_pairs(scratch(b), b, h.pos, posS.p, kvIn, kv.p, (size_t)H, 0u, (unsigned)bN, st));
+        mk_pos_begin(posS.p, H, n, hb.p, st);
+        DBuf<uint32_t> bigList;
+        bigList.alloc((uint64_t)n + 1);
+        HIPCHK(hipMemsetAsync(bigList.p, 0, 4, st));
+        mk_grp_seg(posS.p, hb.p, kv.p, H, bN, bL, gk2.p, perm2.p, bigList.p, env_u32("CMSBWT_GROUP_SMALL", 64), st);
+        kv.release();
+        posS.release();
+        const uint32_t nb = read1(bigList.p);
+        if (nb) {
+          DBuf<uint32_t> bpos, sz, off;
+          bpos.alloc(nb); sz.alloc(nb); off.alloc(nb);
+          sort_keys(bigList.p + 1, bpos.p, nb, bN);
+          mk_grp_big_sizes(bpos.p, nb, hb.p, sz.p, st);
+          exscan(sz.p, off.p, 0u, nb);
+          const uint32_t B = read1(off.p + (nb - 1)) + read1(sz.p + (nb - 1));
+          DBuf<uint32_t> bidx, pB, pB2;
+          DBuf<unsigned long long> kB, kB2;
+          bidx.alloc(B); pB.alloc(B); pB2.alloc(B); kB.alloc(B); kB2.alloc(B);
+          mk_grp_big_expand(bpos.p, nb, hb.p, off.p, bidx.p, st);
+          mk_gather_kp(bidx.p, B, gk2.p, perm2.p, kB.p, pB.p, st);
+          sort_pairs(kB.p, kB2.p, pB.p, pB2.p, B, 2 * bN + bL);  // stable: idx order kept per key
+          mk_scatter_kp(bidx.p, B, kB2.p, pB2.p, gk2.p, perm2.p, st);
+        }
+      }
+    } else if (packed) {  // one sort on the composite key
       gk.alloc(H); gk2.alloc(H);
       mk_group_key(h, H, bN, bL, gk.p, st);
       sort_pairs(gk.p, gk2.p, perm.p, perm2.p, H, 2 * bN + bL);

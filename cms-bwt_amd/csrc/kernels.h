@@ -18,6 +18,11 @@ struct HeadsSoA {
   uint16_t* nexthead;
 };
 
+// A head's grouping fields carried through the position radix sort (12 B).
+struct HeadKV {
+  uint32_t idx, len, isa;
+};
+
 // Items (distinct (pos, len, isaNext) keys) in map order: pos ascending, then
 // the MatchInSet order of match.h:27-33 — the order of the reference's slots.
 struct ItemsSoA {

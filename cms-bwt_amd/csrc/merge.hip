@@ -52,6 +52,81 @@ __global__ void k_group_key(const HeadsSoA h, uint64_t H, int bN, int bL, unsign
   if (i >= H) return;
   key[i] = ((unsigned long long)h.pos[i] << (bN + bL)) | ((unsigned long long)h.len[i] << bN) | h.isa[i];
 }
+// ---- grouping, position first: after a stable radix sort of the heads by
+// pos (HeadKV values in idx order within a position), each position's
+// segment is sorted by (len, isaNext) here.  Output: the composite key
+// pos|len|isaNext of every sorted head (what the one-sort path produces) and
+// its idx.  Segments longer than maxSmall are listed for a radix sort.
+constexpr uint32_t kGrpBlock = 256, kGrpHalo = 64;  // segments of <= kGrpHalo heads are ranked in LDS
+__global__ void __launch_bounds__(256) k_grp_seg(const uint32_t* __restrict__ posS, const uint32_t* __restrict__ hb,
+                                                 const HeadKV* __restrict__ kv, uint32_t H, int bN, int bL,
+                                                 unsigned long long* __restrict__ key, uint32_t* __restrict__ perm,
+                                                 uint32_t* __restrict__ bigList, uint32_t maxSmall) {
+  // one thread per sorted head: its rank inside its position's segment by
+  // counting over the segment, staged in LDS with a halo either side
+  __shared__ unsigned long long lk[kGrpBlock + 2 * kGrpHalo];
+  const uint32_t k0 = blockIdx.x * kGrpBlock;
+  const int64_t base = (int64_t)k0 - kGrpHalo;
+  for (uint32_t i = threadIdx.x; i < kGrpBlock + 2 * kGrpHalo; i += blockDim.x) {
+    const int64_t j = base + i;
+    if (j >= 0 && j < (int64_t)H) {
+      const HeadKV w = kv[j];
+      lk[i] = ((unsigned long long)w.len << bN) | w.isa;
+    }
+  }
+  __syncthreads();
+  const uint32_t k = k0 + threadIdx.x;
+  if (k >= H) return;
+  const uint32_t p = posS[k];
+  const uint32_t b = hb[p], e = hb[p + 1];
+  const unsigned long long hp = (unsigned long long)p << (bN + bL);
+  const HeadKV v = kv[k];
+  const unsigned long long me = lk[threadIdx.x + kGrpHalo];
+  if (e - b > min(maxSmall, kGrpHalo)) {
+    key[k] = hp | me;
+    perm[k] = v.idx;
+    if (k == b) bigList[1 + atomicAdd(bigList, 1u)] = p;
+    return;
+  }
+  // (len, isa) order; equal keys keep idx order (kv is idx-ascending per position)
+  uint32_t r = 0;
+  for (uint32_t j = b; j < e; j++) {
+    const unsigned long long lj = lk[j - base];
+    r += (lj < me || (lj == me && j < k)) ? 1u : 0u;
+  }
+  key[b + r] = hp | me;
+  perm[b + r] = v.idx;
+}
+// big segments: sizes, then their element indices (positions ascending)
+__global__ void k_grp_big_sizes(const uint32_t* __restrict__ pos, uint32_t nb, const uint32_t* __restrict__ hb,
+                                uint32_t* __restrict__ sz) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < nb) sz[i] = hb[pos[i] + 1] - hb[pos[i]];
+}
+__global__ void k_grp_big_expand(const uint32_t* __restrict__ pos, uint32_t nb, const uint32_t* __restrict__ hb,
+                                 const uint32_t* __restrict__ off, uint32_t* __restrict__ idx) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= nb) return;
+  const uint32_t b = hb[pos[i]], e = hb[pos[i] + 1], o = off[i];
+  for (uint32_t k = b; k < e; k++) idx[o + (k - b)] = k;
+}
+__global__ void k_gather_kp(const uint32_t* __restrict__ idx, uint32_t B, const unsigned long long* __restrict__ key,
+                            const uint32_t* __restrict__ perm, unsigned long long* __restrict__ keyB,
+                            uint32_t* __restrict__ permB) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  keyB[i] = key[idx[i]];
+  permB[i] = perm[idx[i]];
+}
+__global__ void k_scatter_kp(const uint32_t* __restrict__ idx, uint32_t B, const unsigned long long* __restrict__ keyB,
+                             const uint32_t* __restrict__ permB, unsigned long long* __restrict__ key,
+                             uint32_t* __restrict__ perm) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  key[idx[i]] = keyB[i];
+  perm[idx[i]] = permB[i];
+}
+
 __global__ void k_item_flags64(const unsigned long long* __restrict__ key, uint32_t* __restrict__ flag, uint64_t H) {
   uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= H) return;
@@ -1542,6 +1617,25 @@ void mk_el_wr_emit(const ElemIn& w, uint32_t V, const unsigned long long* runOff
                    const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st) {
   if (V) hipLaunchKernelGGL(k_el_wr_emit, g1(V), dim3(256), 0, st, elem_args(w), V, runOff, symOff, prevHL, runStart,
                             runChar);
+}
+void mk_grp_seg(const uint32_t* posS, const uint32_t* hb, const HeadKV* kv, uint32_t H, int bN, int bL,
+                unsigned long long* key, uint32_t* perm, uint32_t* bigList, uint32_t maxSmall, hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_grp_seg, dim3((H + kGrpBlock - 1) / kGrpBlock), dim3(kGrpBlock), 0, st, posS, hb, kv, H, bN, bL, key, perm, bigList, maxSmall);
+}
+void mk_grp_big_sizes(const uint32_t* pos, uint32_t nb, const uint32_t* hb, uint32_t* sz, hipStream_t st) {
+  if (nb) hipLaunchKernelGGL(k_grp_big_sizes, g1(nb), dim3(256), 0, st, pos, nb, hb, sz);
+}
+void mk_grp_big_expand(const uint32_t* pos, uint32_t nb, const uint32_t* hb, const uint32_t* off, uint32_t* idx,
+                       hipStream_t st) {
+  if (nb) hipLaunchKernelGGL(k_grp_big_expand, g1(nb), dim3(256), 0, st, pos, nb, hb, off, idx);
+}
+void mk_gather_kp(const uint32_t* idx, uint32_t B, const unsigned long long* key, const uint32_t* perm,
+                  unsigned long long* keyB, uint32_t* permB, hipStream_t st) {
+  if (B) hipLaunchKernelGGL(k_gather_kp, g1(B), dim3(256), 0, st, idx, B, key, perm, keyB, permB);
+}
+void mk_scatter_kp(const uint32_t* idx, uint32_t B, const unsigned long long* keyB, const uint32_t* permB,
+                   unsigned long long* key, uint32_t* perm, hipStream_t st) {
+  if (B) hipLaunchKernelGGL(k_scatter_kp, g1(B), dim3(256), 0, st, idx, B, keyB, permB, key, perm);
 }
 void mk_wr_records(const unsigned long long* runStart, const uint8_t* runChar, uint64_t R, unsigned long long total,
                    uint8_t* out, hipStream_t st) {

@@ -29,6 +29,16 @@ void mk_item_key(const uint32_t* len, const uint8_t* sm, const uint32_t* perm, u
                  hipStream_t st);
 void mk_item_flags(const uint32_t* perm, const HeadsSoA& h, uint32_t* flag, uint64_t H, hipStream_t st);
 void mk_group_key(const HeadsSoA& h, uint64_t H, int bN, int bL, unsigned long long* key, hipStream_t st);
+// grouping, position first (radix by pos, then per-position segments)
+void mk_grp_seg(const uint32_t* posS, const uint32_t* hb, const HeadKV* kv, uint32_t H, int bN, int bL,
+                unsigned long long* key, uint32_t* perm, uint32_t* bigList, uint32_t maxSmall, hipStream_t st);
+void mk_grp_big_sizes(const uint32_t* pos, uint32_t nb, const uint32_t* hb, uint32_t* sz, hipStream_t st);
+void mk_grp_big_expand(const uint32_t* pos, uint32_t nb, const uint32_t* hb, const uint32_t* off, uint32_t* idx,
+                       hipStream_t st);
+void mk_gather_kp(const uint32_t* idx, uint32_t B, const unsigned long long* key, const uint32_t* perm,
+                  unsigned long long* keyB, uint32_t* permB, hipStream_t st);
+void mk_scatter_kp(const uint32_t* idx, uint32_t B, const unsigned long long* keyB, const uint32_t* permB,
+                   unsigned long long* key, uint32_t* perm, hipStream_t st);
 void mk_item_flags64(const unsigned long long* key, uint32_t* flag, uint64_t H, hipStream_t st);
 void mk_item_fill64(const unsigned long long* key, const uint32_t* perm, const uint32_t* flag, const uint32_t* incl,
                     const HeadsSoA& h, uint64_t H, int bN, int bL, const ItemsSoA& it, hipStream_t st);

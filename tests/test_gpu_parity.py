@@ -95,6 +95,17 @@ def test_grouping_three_sorts(engine, oracle, tmp_path, case):
     _compare(engine, oracle, tmp_path, case, env={"CMSBWT_GROUP3": "1"})
 
 
+@pytest.mark.parametrize("env", [{"CMSBWT_GROUP64": "1"}, {"CMSBWT_GROUP_SMALL": "1"},
+                                 {"CMSBWT_GROUP_SMALL": "0"}],
+                         ids=["one_key_sort", "long_segments", "all_segments_radix"])
+@pytest.mark.parametrize("case", cases.small_cases()[:6], ids=lambda c: c[0])
+def test_grouping_position_first(engine, oracle, tmp_path, case, env):
+    """Grouping (FN:1387-1416) by a position radix sort plus per-position
+    segment sorts (default), by one sort of the composite key, and with every
+    segment longer than the per-thread limit (radix-sorted subset)."""
+    _compare(engine, oracle, tmp_path, case, env=env)
+
+
 @pytest.mark.parametrize("small", ["2", "1000000"], ids=["radix_groups", "thread_groups"])
 @pytest.mark.parametrize("case", cases.small_cases()[:4], ids=lambda c: c[0])
 def test_doubling_group_paths(engine, oracle, tmp_path, case, small):
