@@ -1387,9 +1387,14 @@ struct Engine {
     DBuf<uint32_t> wflag, wincl, winStart, crossCnt, crossOff, crossList;
     wflag.alloc(n);
     wincl.alloc(n);
-    const uint32_t winPos = std::min(1024u, env_u32("CMSBWT_WINPOS", 1024)),
+    // target-major kernel (default): windows of 256 targets, slots unbounded;
+    // k_counter_win (checked queries, or CMSBWT_COUNTER_WIN=1): windows cut
+    // by the LDS slot budget
+    const bool tgt = !check && !env_u32("CMSBWT_COUNTER_WIN", 0);
+    const uint32_t winPos = tgt ? std::max(1u, std::min(256u, env_u32("CMSBWT_TGTWIN", 256)))
+                                : std::min(1024u, env_u32("CMSBWT_WINPOS", 1024)),
                    slotCap = std::min(3584u, env_u32("CMSBWT_WINSLOTS", 3584));  // kWinSlots (merge.hip)
-    mk_win_flags(posBegin, S.slot, n, P0, P1, std::max(1u, winPos), slotCap, wflag.p, st);
+    mk_win_flags(posBegin, S.slot, n, P0, P1, std::max(1u, winPos), tgt ? 0xfffffffeu : slotCap, wflag.p, st);
     inscan(wflag.p, wincl.p, n, rocprim::plus<uint32_t>());
     const uint32_t nw = P1 > P0 ? read1(wincl.p + (n - 1)) : 0;
     winStart.alloc((uint64_t)nw + 1);
@@ -1413,8 +1418,11 @@ struct Engine {
     mk_win_cross_off(keyW2.p, ncross, nw, crossOff.p, st);
     wincl.release();
     HIPCHK(hipEventRecord(ev0, st));
-    mk_counter_win(S, posBegin, posF, nhrP, winStart.p, nw, crossOff.p, crossList.p, counterP, cstatsP, n,
-                   slotCap, check, st);
+    if (tgt)
+      mk_counter_tgt(S, posBegin, posF, nhrP, winStart.p, nw, crossOff.p, crossList.p, counterP, cstatsP, n, st);
+    else
+      mk_counter_win(S, posBegin, posF, nhrP, winStart.p, nw, crossOff.p, crossList.p, counterP, cstatsP, n,
+                     slotCap, check, st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev1, st));
     sync();

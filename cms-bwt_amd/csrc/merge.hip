@@ -8,6 +8,7 @@
 #include "merge_kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace cmsbwt {
 
@@ -710,13 +711,11 @@ __device__ __forceinline__ uint32_t d_lower_u64(const unsigned long long* a, uin
 // smaller, count and slot (wave-uniform).  V gives the target's items and
 // positions either from LDS (staged window) or from global memory.
 template <bool CHECK, class View, class AddFn>
-__device__ __forceinline__ void d_counter_query(const View& V, uint32_t ql, uint32_t qi, bool S, uint32_t cq,
-                                                uint32_t slq, uint32_t k, uint32_t t, QueryStats& qs,
-                                                AddFn add) {
+__device__ __forceinline__ void d_counter_query_L(const View& V, uint32_t L, uint32_t qi, bool S, uint32_t cq,
+                                                  uint32_t slq, uint32_t t, QueryStats& qs, AddFn add) {
   const uint32_t b0 = V.begin(t), b1 = V.begin(t + 1);
   if (b0 == b1) { qs.nothing++; return; }  // bucket >= 0: no heads at t (FN:1530)
   const uint32_t f = V.fbeg(t);
-  const uint32_t L = ql - 1 - k;  // uint32 wrap as FN:1532
   const unsigned long long kT = ((unsigned long long)L << 32) | qi;
   const unsigned long long kF = ((unsigned long long)(~L) << 32) | qi;
   auto lower = [&](uint32_t lo, uint32_t hi, unsigned long long v) {
@@ -770,6 +769,12 @@ __device__ __forceinline__ void d_counter_query(const View& V, uint32_t ql, uint
     add(so, cq);
     qs.good++;
   }
+}
+template <bool CHECK, class View, class AddFn>
+__device__ __forceinline__ void d_counter_query(const View& V, uint32_t ql, uint32_t qi, bool S, uint32_t cq,
+                                                uint32_t slq, uint32_t k, uint32_t t, QueryStats& qs,
+                                                AddFn add) {
+  d_counter_query_L<CHECK>(V, ql - 1 - k, qi, S, cq, slq, t, qs, add);  // uint32 wrap as FN:1532
 }
 
 // item/position views: global memory, or the block's staged window in LDS
@@ -989,6 +994,236 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
   if (qs.slow) atomicAdd(&red[5], (unsigned long long)qs.slow);
   __syncthreads();
   if (threadIdx.x < 6 && threadIdx.x != 4 && red[threadIdx.x]) atomicAdd(&A.stats[threadIdx.x], red[threadIdx.x]);
+}
+
+// ---- counterSmallerThanHead, target-major with register accumulators.
+// A block owns a window of <= 256 consecutive targets and a lane owns one of
+// them for the whole window (wave w: targets T0 + 64 w ..).  The items
+// covering the window (its crossing list, then the items starting inside it)
+// are staged in LDS as 16-byte records (match end E = pos + len, the
+// window-relative target range, count | smaller << 31, item), each copied to
+// the list of every wave whose 64 targets it reaches, and each wave walks its
+// list 64 records per LDS read + readlane.  Per (item, target) pair the fast
+// tests of k_counter_win compare the query len L = E - t (FN:1532, uint32
+// wrap) with the class maxima of the lane's target, held in registers, and a
+// decided query adds the item's count to one of the target's three
+// accumulators (first smaller=false item, last smaller=true item, second
+// smaller=false item): no memory traffic per pair.  Undecided queries are
+// appended to the wave's LDS list and searched 64 at a time when it fills
+// (items from global memory / L2, adds by global atomics); at the end each
+// accumulator is added to its slot.
+constexpr uint32_t kTgtRec = 256;   // item records staged per chunk (= threads per block)
+constexpr uint32_t kTgtQ = 256;     // undecided queries listed per wave before a search pass
+constexpr uint32_t kTgtS = 320;     // queries listed per wave for binary searches
+constexpr uint32_t kNoSlot = 0xffffffffu;
+
+__global__ void __launch_bounds__(256) k_counter_tgt(CounterArgs A) {
+  __shared__ uint4 recG[4][kTgtRec];  // 16 KB: per wave, the records reaching its targets
+  __shared__ uint32_t qL[4][kTgtQ];   // 8 KB
+  __shared__ uint32_t nG[8];  // per wave: smaller=true records (front), smaller=false (back)
+  __shared__ uint32_t accL[6][kTgtRec];  // 6 KB: adds settled in the search passes, per target
+  __shared__ uint32_t qS[4][kTgtS];       // 5 KB: queries left for binary searches
+  const ItemsSoA& it = A.it;
+  const uint32_t w = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const uint32_t T0 = A.winStart[w], T1 = A.winStart[w + 1];
+  const uint32_t iBeg = A.posBegin[T0], iEnd = A.posBegin[T1];
+  // the lane's target: presence of items, class maxima (S items ascend by
+  // len, F items descend) and the three destination slots
+  const uint32_t toff = tid, t = T0 + toff;
+  // the three longest items of each class: S items ascend by len (the last
+  // three, sl0 longest), F items descend (the first three, fl0 longest); a
+  // missing item has len 0 and slot kNoSlot
+  uint32_t sl0 = 0, sl1 = 0, sl2 = 0, fl0 = 0, fl1 = 0, fl2 = 0;
+  uint32_t ss0 = kNoSlot, ss1 = kNoSlot, ss2 = kNoSlot, fs0 = kNoSlot, fs1 = kNoSlot, fs2 = kNoSlot;
+  bool has = false, nS3 = false, nF3 = false;
+  if (t < T1) {
+    const uint32_t b0 = A.posBegin[t], b1 = A.posBegin[t + 1], f = A.posF[t];
+    has = b0 != b1;
+    const uint32_t nS = f - b0, nF = b1 - f;
+    if (nS >= 1) { sl0 = it.len[f - 1]; ss0 = it.slot[f - 1]; }
+    if (nS >= 2) { sl1 = it.len[f - 2]; ss1 = it.slot[f - 2]; }
+    if (nS >= 3) { sl2 = it.len[f - 3]; ss2 = it.slot[f - 3]; }
+    if (nF >= 1) { fl0 = it.len[f]; fs0 = it.slot[f]; }
+    if (nF >= 2) { fl1 = it.len[f + 1]; fs1 = it.slot[f + 1]; }
+    if (nF >= 3) { fl2 = it.len[f + 2]; fs2 = it.slot[f + 2]; }
+    nS3 = nS == 3;
+    nF3 = nF == 3;
+  }
+  const bool hasF0 = fs0 != kNoSlot, hasF1 = fs1 != kNoSlot, hasF2 = fs2 != kNoSlot;
+  const uint32_t flags = (hasF0 ? 1u : 0u) | (hasF1 ? 2u : 0u) | (hasF2 ? 4u : 0u) | (nS3 ? 8u : 0u) | (nF3 ? 16u : 0u);
+  for (uint32_t k = 0; k < 6; k++) accL[k][tid] = 0;
+  // accumulators: first F item (f), S items top 0..2, F items 1..2
+  uint32_t aF0 = 0, aS0 = 0, aS1 = 0, aS2 = 0, aF1 = 0, aF2 = 0, nGood = 0, nNothing = 0;
+  QueryStats qs;
+  const GlobalView GV{&A.it, A.posBegin, A.posF, A.nhr};
+  uint32_t* const myQ = qL[wv];
+  uint32_t* const myS = qS[wv];
+  const uint4* const myR = recG[wv];
+  const uint32_t c0 = A.crossOff[w], nCross = A.crossOff[w + 1] - c0;
+  const uint32_t nList = nCross + (iEnd - iBeg);
+  // binary searches of the wave's listed queries (FN:1534-1597 in full)
+  uint32_t nSearch = 0;
+  auto search = [&]() {
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t d = 0; d < nSearch; d += 64) {
+      if (d + lane < nSearch) {
+        const uint32_t en = myS[d + lane];
+        const uint4 rc = myR[en & 0xffffu];
+        const uint32_t tq = T0 + ((en >> 16) & 0xffu);
+        const uint32_t q = rc.w, L = rc.x - tq;
+        const bool S = (en >> 31) != 0;
+        qs.slow++;
+        auto addG = [&](uint32_t s, uint32_t v) { atomicAdd(&A.counter[s], (unsigned long long)v); };
+        d_counter_query_L<false>(GV, L, it.isa[q], S, rc.z & 0x7fffffffu, it.slot[q], tq, qs, addG);
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    nSearch = 0;
+  };
+  // one walk over a wave's records of one class (smaller=true records from
+  // the front of its list, smaller=false ones from the back)
+  auto walk = [&](auto cls, uint32_t rb, uint32_t re) {
+    constexpr bool S = decltype(cls)::value;
+    uint32_t r = rb;
+    for (;;) {
+      uint32_t qn = 0;  // listed undecided queries (wave-uniform)
+      while (r < re && qn <= kTgtQ - 64) {
+        const uint32_t nb = min(64u, re - r);
+        const uint4 my = lane < nb ? myR[r + lane] : make_uint4(0u, 0u, 0u, 0u);
+        uint32_t e = 0;
+        for (; e < nb && qn <= kTgtQ - 64; e++) {
+          const uint32_t ab = __builtin_amdgcn_readlane(my.y, e);
+          const uint32_t cq = __builtin_amdgcn_readlane(my.z, e) & 0x7fffffffu;
+          const uint32_t L = __builtin_amdgcn_readlane(my.x, e) - t;
+          const uint32_t aO = ab & 0xffffu, bO = ab >> 16;
+          const bool inr = (toff >= aO) & (toff <= bO);
+          // lower_bound (FN:1534) settled by the two longest items of the
+          // query's class (k_counter_win's fast tests, exact lens; bitwise
+          // & and | keep the body free of branches); the rest is listed
+          bool sl;
+          const bool vh = inr & has;
+          if (S) {  // smaller=true: S items ascending, then F items
+            const bool c1 = (L > sl0) & (L != fl0);  // past every S item: f (or end)
+            const bool c2 = (L < sl0) & (L > sl1);   // the longest S item
+            aF0 += (vh & c1 & hasF0) ? cq : 0u;
+            aS0 += (vh & c2) ? cq : 0u;
+            nGood += (vh & ((c1 & hasF0) | c2)) ? 1u : 0u;
+            sl = vh & !c1 & !c2;
+          } else {  // smaller=false: F items descending
+            const bool c1 = L > fl0;                 // f
+            const bool c2 = (L < fl0) & (L > fl1);   // the second F item (or end)
+            aF0 += (vh & c1 & hasF0) ? cq : 0u;
+            aF1 += (vh & c2 & hasF1) ? cq : 0u;
+            nGood += (vh & ((c1 & hasF0) | (c2 & hasF1))) ? 1u : 0u;
+            sl = vh & !c1 & !c2;
+          }
+          nNothing += (inr & !has) ? 1u : 0u;
+          const uint64_t sm = __ballot(sl);
+          if (sl) {
+            const uint32_t rk =
+                __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
+            myQ[qn + rk] = (r + e) | (toff << 16);
+          }
+          qn += (uint32_t)__popcll(sm);
+        }
+        r += e;
+      }
+      if (qn == 0) break;  // (the walk is done: an empty list never stops it)
+      if (A.slotCap & 2) continue;  // timing experiments only (CMSBWT_TGT_DEBUG): no searches
+      // search pass over the listed queries, 64 at a time: first the three
+      // longest items of the class, read from the target's owning lane
+      // (ds_bpermute); what they do not settle goes to the wave's search
+      // list, binary-searched 64 at a time
+      __builtin_amdgcn_wave_barrier();
+      for (uint32_t d = 0; d < qn; d += 64) {
+        const bool act = d + lane < qn;
+        const uint32_t en = act ? myQ[d + lane] : 0u;
+        const int own = (int)((en >> 16) & 63u);
+        const uint32_t o0 = __shfl(S ? sl0 : fl0, own), o1 = __shfl(S ? sl1 : fl1, own);
+        const uint32_t o2 = __shfl(S ? sl2 : fl2, own), of0 = __shfl(fl0, own);
+        const uint32_t fl = __shfl(flags, own);
+        uint32_t dst = 6;  // 0 f, 1..3 S top 0..2, 4..5 F items 1..2; 6 end / none; 7 search
+        uint32_t cq = 0;
+        if (act) {
+          const uint4 rc = myR[en & 0xffffu];
+          const uint32_t L = rc.x - (T0 + (en >> 16));
+          cq = rc.z & 0x7fffffffu;
+          const bool g0 = L < o0, g1 = L < o1, g2 = L < o2;
+          const bool ne = (L != o0) & (L != o1) & (L != o2);
+          dst = 7;
+          if (S) {
+            if (!g0 & ne) dst = (fl & 1u) ? ((L != of0) ? 0u : 7u) : 6u;
+            else if (g0 & !g1 & ne) dst = 1;
+            else if (g1 & !g2 & ne) dst = 2;
+            else if (g2 & ne & ((fl & 8u) != 0)) dst = 3;
+          } else {
+            if (!g0 & ne) dst = (fl & 1u) ? 0u : 6u;
+            else if (g0 & !g1 & ne) dst = (fl & 2u) ? 4u : 6u;
+            else if (g1 & !g2 & ne) dst = (fl & 4u) ? 5u : 6u;
+            else if (g2 & ne & ((fl & 16u) != 0)) dst = 6;
+          }
+          if (dst < 6) {
+            atomicAdd(&accL[dst][en >> 16], cq);
+            qs.good++;
+          }
+        }
+        const uint64_t smS = __ballot(dst == 7);
+        if (dst == 7) {
+          const uint32_t rk =
+              __builtin_amdgcn_mbcnt_hi((uint32_t)(smS >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)smS, 0u));
+          myS[nSearch + rk] = en | (S ? 0x80000000u : 0u);
+        }
+        nSearch += (uint32_t)__popcll(smS);
+        if (nSearch >= kTgtS - 64) search();
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  };
+  for (uint32_t ch = 0; ch < nList; ch += kTgtRec) {
+    const uint32_t nr = min(kTgtRec, nList - ch);
+    if (tid < 8) nG[tid] = 0;
+    __syncthreads();  // the previous chunk's lists are no longer read
+    if (tid < nr) {
+      const uint32_t j = ch + tid;
+      const uint32_t q = j < nCross ? A.crossList[c0 + j] : iBeg + (j - nCross);
+      const uint32_t p = it.pos[q], u = it.until[q];
+      if (u) {
+        const uint32_t lo = max(p + 1, T0);
+        const uint32_t hi = (uint32_t)min((uint64_t)p + u, (uint64_t)T1 - 1);
+        if (lo <= hi) {
+          const uint32_t aO = lo - T0, bO = hi - T0;
+          const bool sm = it.smaller[q] != 0;
+          const uint4 rec = make_uint4(it.len[q] + p, aO | (bO << 16), it.count[q] | (sm ? 0x80000000u : 0u), q);
+          for (uint32_t k = aO >> 6; k <= (bO >> 6); k++) {
+            const uint32_t o = atomicAdd(&nG[2 * k + (sm ? 0 : 1)], 1u);
+            recG[k][sm ? o : kTgtRec - 1 - o] = rec;
+          }
+        }
+      }
+    }
+    __syncthreads();
+    if (A.slotCap & 4) continue;  // timing experiments only: staging alone
+    const uint32_t nS = nG[2 * wv], nF = nG[2 * wv + 1];
+    walk(std::true_type{}, 0u, nS);
+    walk(std::false_type{}, kTgtRec - nF, kTgtRec);
+    if (nSearch) search();  // before the next chunk replaces the records
+  }
+  __syncthreads();
+  aF0 += accL[0][tid]; aS0 += accL[1][tid]; aS1 += accL[2][tid]; aS2 += accL[3][tid];
+  aF1 += accL[4][tid]; aF2 += accL[5][tid];
+  if (aF0) atomicAdd(&A.counter[fs0], (unsigned long long)aF0);
+  if (aF1) atomicAdd(&A.counter[fs1], (unsigned long long)aF1);
+  if (aF2) atomicAdd(&A.counter[fs2], (unsigned long long)aF2);
+  if (aS0) atomicAdd(&A.counter[ss0], (unsigned long long)aS0);
+  if (aS1) atomicAdd(&A.counter[ss1], (unsigned long long)aS1);
+  if (aS2) atomicAdd(&A.counter[ss2], (unsigned long long)aS2);
+  qs.good += nGood;
+  qs.nothing += nNothing;
+  if (qs.bad) atomicAdd(&A.stats[0], (unsigned long long)qs.bad);
+  if (qs.good) atomicAdd(&A.stats[1], (unsigned long long)qs.good);
+  if (qs.nothing) atomicAdd(&A.stats[2], (unsigned long long)qs.nothing);
+  if (qs.slow) atomicAdd(&A.stats[5], (unsigned long long)qs.slow);
 }
 
 __global__ void k_item_sk(ItemsSoA it, uint32_t K) {
@@ -1568,6 +1803,14 @@ void mk_counter_win(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t
                 std::min(slotCap, kWinSlots)};
   if (check) hipLaunchKernelGGL(k_counter_win<true>, dim3(nw), dim3(512), 0, st, A);
   else hipLaunchKernelGGL(k_counter_win<false>, dim3(nw), dim3(512), 0, st, A);
+}
+void mk_counter_tgt(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
+                    const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
+                    unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st) {
+  if (!nw) return;
+  CounterArgs A{it, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n,
+                (uint32_t)(getenv("CMSBWT_TGT_DEBUG") ? atoi(getenv("CMSBWT_TGT_DEBUG")) : 0)};
+  hipLaunchKernelGGL(k_counter_tgt, dim3(nw), dim3(256), 0, st, A);
 }
 void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st) {
   if (K) hipLaunchKernelGGL(k_count_distinct, dim3(std::min<unsigned>(2048, g1(K).x)), dim3(256), 0, st, v, K, out);

@@ -119,6 +119,10 @@ void mk_counter_win(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t
                     const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
                     unsigned long long* counter, unsigned long long* stats, uint32_t n, uint32_t slotCap, bool check,
                     hipStream_t st);
+// target-major counter: windows of <= 256 targets (winStart), register accumulators
+void mk_counter_tgt(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
+                    const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
+                    unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st);
 void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st);
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st);
 // run writer: units = E end phrases + SA ranks 1..n-1

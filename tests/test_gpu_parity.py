@@ -78,13 +78,16 @@ def test_chunk_restarts(engine, oracle, tmp_path, case, chunk):
     _compare(engine, oracle, tmp_path, case, chunk=chunk)
 
 
-@pytest.mark.parametrize("geom", [{"CMSBWT_WINPOS": "7"}, {"CMSBWT_WINPOS": "64", "CMSBWT_WINSLOTS": "16"},
-                                  {"CMSBWT_WINSLOTS": "1"}, {"CMSBWT_FORCE_CHECK": "1", "CMSBWT_WINPOS": "33"}],
+@pytest.mark.parametrize("geom", [{"CMSBWT_COUNTER_WIN": "1", "CMSBWT_WINPOS": "7"},
+                                  {"CMSBWT_COUNTER_WIN": "1", "CMSBWT_WINPOS": "64", "CMSBWT_WINSLOTS": "16"},
+                                  {"CMSBWT_COUNTER_WIN": "1", "CMSBWT_WINSLOTS": "1"},
+                                  {"CMSBWT_FORCE_CHECK": "1", "CMSBWT_WINPOS": "33"}],
                          ids=["tiny_windows", "small_lds", "global_atomics", "checked_queries"])
 @pytest.mark.parametrize("case", cases.small_cases()[:5], ids=lambda c: c[0])
 def test_counter_window_geometry(engine, oracle, tmp_path, case, geom):
-    """Tiny windows stress the crossing lists; slot caps below a position's
-    slot count force the global-atomic fallback of the counter kernel."""
+    """Slot-budget kernel (k_counter_win): tiny windows stress the crossing
+    lists; slot caps below a position's slot count force its global-atomic
+    fallback; checked queries always run here."""
     _compare(engine, oracle, tmp_path, case, env=geom)
 
 
@@ -93,6 +96,19 @@ def test_grouping_three_sorts(engine, oracle, tmp_path, case):
     """Grouping (FN:1387-1416) by three LSD sorts (the path for fields wider
     than one 64-bit key) gives the oracle's items, ranks and runs."""
     _compare(engine, oracle, tmp_path, case, env={"CMSBWT_GROUP3": "1"})
+
+
+@pytest.mark.parametrize("env", [{"CMSBWT_TGTWIN": "7"}, {"CMSBWT_TGTWIN": "1"}, {"CMSBWT_TGTWIN": "64"},
+                                 {"CMSBWT_TGTWIN": "200"}, {"CMSBWT_COUNTER_WIN": "1"}],
+                         ids=["tiny_windows", "one_target_windows", "one_wave_windows", "ragged_windows",
+                              "slot_windows_kernel"])
+@pytest.mark.parametrize("case", cases.small_cases()[:6], ids=lambda c: c[0])
+def test_counter_target_major(engine, oracle, tmp_path, case, env):
+    """counterSmallerThanHead (FN:1523-1603) target-major with per-lane
+    accumulators: tiny windows stress the crossing lists, windows of one wave
+    or not a multiple of 64 targets leave waves idle or partly filled; the
+    slot-budget kernel (k_counter_win) stays selectable."""
+    _compare(engine, oracle, tmp_path, case, env=env)
 
 
 @pytest.mark.parametrize("env", [{"CMSBWT_GROUP64": "1"}, {"CMSBWT_GROUP_SMALL": "1"},
