@@ -1556,15 +1556,21 @@ struct Engine {
       // Group leaders sort groups of <= 32 members by one thread each; the
       // members of larger groups go to one radix sort.
       const uint32_t maxSmall = env_u32("CMSBWT_DBL_SMALL", 32);
+      // one thread per member (default) or per group leader (CMSBWT_DBL_LEADERS=1)
+      const bool rankPath = !env_u32("CMSBWT_DBL_LEADERS", 0);
       DBuf<uint32_t> gflag, bigList, origB, actB, valB, keepB;
       DBuf<uint64_t> keyB;
       gflag.alloc(U); bigList.alloc((uint64_t)U + 1);
       for (uint64_t hstep = 1; U > 0; hstep <<= 1) {
         if (hstep > H) throw InputError{CMSBWT_EINPUT, "internal: head-string suffix sort did not converge"};
         mk_dbl_keys(act.p, saT.p, grp.p, (uint32_t)hstep, U, k64.p, val.p, st);
-        mk_dbl_gstart(k64.p, U, gflag.p, st);
         HIPCHK(hipMemsetAsync(bigList.p, 0, 4, st));
-        mk_dbl_small2(gflag.p, U, act.p, k64.p, val.p, saT.p, grp.p, keep.p, bigList.p, maxSmall, st);
+        if (rankPath) {
+          mk_dbl_rank(U, act.p, k64.p, val.p, saT.p, grp.p, keep.p, bigList.p, maxSmall, st);
+        } else {
+          mk_dbl_gstart(k64.p, U, gflag.p, st);
+          mk_dbl_small2(gflag.p, U, act.p, k64.p, val.p, saT.p, grp.p, keep.p, bigList.p, maxSmall, st);
+        }
         const uint32_t B = read1(bigList.p);
         if (dstats) fprintf(stderr, "[dbl] h %llu U %u big %u\n", (unsigned long long)hstep, U, B);
         if (B) {

@@ -435,6 +435,63 @@ __global__ void k_act_fill(const uint32_t* __restrict__ posBegin, const uint32_t
 // Group leaders (gflag) sort their group when it has <= maxSmall members;
 // members of larger groups are appended to bigList (group by group) for the
 // radix path (bigList[0] counts them).
+// One thread per unresolved member (act order): its group (a run of equal
+// labels = key high words, <= kDblHalo members, found in an LDS copy of the
+// keys around the block) is ranked by counting, as k_grp_seg does.  Member u
+// moves to sa position act[u0 + rank] (rank by (key, u)), its new label is
+// act[u0 + #smaller keys], and it stays unresolved when another member has
+// its key.  Members of longer groups are listed for the radix path.
+constexpr uint32_t kDblBlock = 256, kDblHalo = 64;
+__global__ void __launch_bounds__(256) k_dbl_rank(uint32_t U, const uint32_t* __restrict__ act,
+                                                  const uint64_t* __restrict__ key, const uint32_t* __restrict__ val,
+                                                  uint32_t* __restrict__ sa, uint32_t* __restrict__ grp,
+                                                  uint32_t* __restrict__ keep, uint32_t* __restrict__ bigList,
+                                                  uint32_t maxSmall) {
+  __shared__ uint64_t kL[kDblBlock + 2 * kDblHalo];
+  __shared__ uint32_t aL[kDblBlock + 2 * kDblHalo];
+  const uint32_t k0 = blockIdx.x * kDblBlock;
+  const int64_t base = (int64_t)k0 - kDblHalo;
+  for (uint32_t i = threadIdx.x; i < kDblBlock + 2 * kDblHalo; i += blockDim.x) {
+    const int64_t j = base + i;
+    if (j >= 0 && j < (int64_t)U) { kL[i] = key[j]; aL[i] = act[j]; }
+  }
+  __syncthreads();
+  const uint32_t u = k0 + threadIdx.x;
+  if (u >= U) return;
+  const uint32_t me = threadIdx.x + kDblHalo;
+  const uint64_t kk = kL[me];
+  const uint32_t lab = (uint32_t)(kk >> 32);
+  const uint32_t lim = min(maxSmall, kDblHalo - 1);
+  // group bounds [lo, hi) within lim + 1 steps either side
+  uint32_t lo = me, hi = me + 1;
+  while (lo > 0 && base + lo > 0 && (uint32_t)(kL[lo - 1] >> 32) == lab && me - lo <= lim) lo--;
+  while (hi < kDblBlock + 2 * kDblHalo && base + hi < (int64_t)U && (uint32_t)(kL[hi] >> 32) == lab &&
+         hi - me <= lim)
+    hi++;
+  if (hi - lo > lim) {  // a long group: radix path (wave-aggregated list append)
+    const uint64_t bm = __ballot(true);
+    const uint32_t lead = __builtin_amdgcn_readfirstlane((uint32_t)__builtin_ctzll(bm));
+    uint32_t o = 0;
+    if ((threadIdx.x & 63) == lead) o = atomicAdd(bigList, (uint32_t)__popcll(bm));
+    o = __shfl(o, (int)lead);
+    const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(bm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)bm, 0u));
+    bigList[1 + o + rk] = u;
+    return;
+  }
+  uint32_t r = 0, rs = 0, eq = 0;
+  for (uint32_t j = lo; j < hi; j++) {
+    const uint64_t kj = kL[j];
+    r += (kj < kk || (kj == kk && j < me)) ? 1u : 0u;
+    rs += kj < kk ? 1u : 0u;
+    eq += kj == kk ? 1u : 0u;
+  }
+  const uint32_t v = val[u];
+  if (lo + r != me) sa[aL[lo + r]] = v;  // moved by the sort
+  if (rs != 0) grp[v] = aL[lo + rs];     // a later part of the group: new label
+  // keep is indexed by act position (the member's new sa position): still
+  // unresolved while another member has its key
+  keep[(uint32_t)(base + lo + r)] = eq > 1 ? 1u : 0u;
+}
 __global__ void k_dbl_small2(const uint32_t* __restrict__ gflag, uint32_t U, const uint32_t* __restrict__ act,
                              uint64_t* __restrict__ key, uint32_t* __restrict__ val, uint32_t* __restrict__ sa,
                              uint32_t* __restrict__ grp, uint32_t* __restrict__ keep, uint32_t* __restrict__ bigList,
@@ -448,15 +505,19 @@ __global__ void k_dbl_small2(const uint32_t* __restrict__ gflag, uint32_t U, con
     for (uint32_t u = u0; u < u1; u++) bigList[1 + o + (u - u0)] = u;
     return;
   }
+  // Only changed entries are written: a member keeps its label (the group's
+  // first sa position) when it stays in the group's first part, and its sa
+  // entry when the sort did not move it (grp writes are random 4-byte stores).
   if (u1 - u0 <= 4) {  // the common case: a sorting network in registers
     uint64_t k[4];
-    uint32_t v[4], a4[4];
+    uint32_t v[4], a4[4], vo[4];
 #pragma unroll
     for (uint32_t j = 0; j < 4; j++) {
       const bool in = u0 + j < u1;
       k[j] = in ? key[u0 + j] : ~0ull;
       v[j] = in ? val[u0 + j] : 0u;
       a4[j] = in ? act[u0 + j] : 0u;
+      vo[j] = v[j];
     }
     auto cs = [&](int x, int y) {
       if (k[y] < k[x]) {
@@ -472,8 +533,8 @@ __global__ void k_dbl_small2(const uint32_t* __restrict__ gflag, uint32_t U, con
       if (u0 + j < u1) {
         if (j > 0 && k[j] != k[j - 1]) rs = j;
         const bool endRun = u0 + j + 1 == u1 || k[j + 1 < 4 ? j + 1 : 3] != k[j];
-        sa[a4[j]] = v[j];
-        grp[v[j]] = a4[rs];
+        if (v[j] != vo[j]) sa[a4[j]] = v[j];
+        if (rs != 0) grp[v[j]] = a4[rs];
         keep[u0 + j] = (rs == j && endRun) ? 0u : 1u;
       }
     }
@@ -496,7 +557,7 @@ __global__ void k_dbl_small2(const uint32_t* __restrict__ gflag, uint32_t U, con
     if (u > u0 && key[u] != key[u - 1]) rs = u;
     const bool endRun = u + 1 == u1 || key[u + 1] != key[u];
     sa[act[u]] = val[u];
-    grp[val[u]] = act[rs];
+    if (rs != u0) grp[val[u]] = act[rs];
     keep[u] = (rs == u && endRun) ? 0u : 1u;
   }
 }
@@ -1751,6 +1812,11 @@ void mk_act_count(const uint32_t* posBegin, const uint32_t* count, const uint32_
 void mk_act_fill(const uint32_t* posBegin, const uint32_t* slot, const uint32_t* count, const uint32_t* isaRef,
                  const uint32_t* headBase, const uint32_t* offR, uint32_t n, uint32_t* act, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_act_fill, g1(n), dim3(256), 0, st, posBegin, slot, count, isaRef, headBase, offR, n, act);
+}
+void mk_dbl_rank(uint32_t U, const uint32_t* act, const uint64_t* key, const uint32_t* val, uint32_t* sa,
+                 uint32_t* grp, uint32_t* keep, uint32_t* bigList, uint32_t maxSmall, hipStream_t st) {
+  if (U) hipLaunchKernelGGL(k_dbl_rank, dim3((U + kDblBlock - 1) / kDblBlock), dim3(kDblBlock), 0, st, U, act, key, val,
+                            sa, grp, keep, bigList, maxSmall);
 }
 void mk_dbl_small2(const uint32_t* gflag, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val, uint32_t* sa,
                    uint32_t* grp, uint32_t* keep, uint32_t* bigList, uint32_t maxSmall, hipStream_t st) {

@@ -98,6 +98,8 @@ void mk_act_fill(const uint32_t* posBegin, const uint32_t* slot, const uint32_t*
                  const uint32_t* headBase, const uint32_t* offR, uint32_t n, uint32_t* act, hipStream_t st);
 void mk_dbl_small2(const uint32_t* gflag, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val, uint32_t* sa,
                    uint32_t* grp, uint32_t* keep, uint32_t* bigList, uint32_t maxSmall, hipStream_t st);
+void mk_dbl_rank(uint32_t U, const uint32_t* act, const uint64_t* key, const uint32_t* val, uint32_t* sa,
+                 uint32_t* grp, uint32_t* keep, uint32_t* bigList, uint32_t maxSmall, hipStream_t st);
 void mk_dbl_gstart(const uint64_t* key, uint32_t U, uint32_t* flag, hipStream_t st);
 void mk_dbl_small(const uint32_t* gs, uint32_t G, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val,
                   uint32_t* sa, uint32_t* grp, uint32_t* keep, uint32_t* big, uint32_t maxSmall, hipStream_t st);
