@@ -57,7 +57,11 @@ struct WidenU64 {
 struct MakeHeadKV {  // head idx -> its grouping fields
   const uint32_t* len;
   const uint32_t* isa;
-  __host__ __device__ HeadKV operator()(uint32_t i) const { return HeadKV{i, len[i], isa[i]}; }
+  const uint8_t* smaller;
+  const uint32_t* tonext;
+  __host__ __device__ HeadKV operator()(uint32_t i) const {
+    return HeadKV{i, len[i] | (smaller[i] ? 0x80000000u : 0u), isa[i], tonext[i]};
+  }
 };
 struct PlusOneU64 {
   __host__ __device__ unsigned long long operator()(unsigned long long v) const { return v + 1; }
@@ -1249,6 +1253,8 @@ struct Engine {
     DBuf<uint32_t>& perm2 = S.P;
     perm.alloc(H); perm2.alloc(H); key.alloc(H); key2.alloc(H);
     DBuf<unsigned long long> gk, gk2;
+    DBuf<uint32_t> tsS;  // position-first path: tonext and smaller of each sorted head
+    DBuf<uint8_t> smS;
     const bool posFirst = packed && !env_u32("CMSBWT_GROUP64", 0);
     if (!posFirst) mk_iota(perm.p, H, st);
     if (posFirst) {
@@ -1261,7 +1267,7 @@ struct Engine {
         DBuf<HeadKV> kv;
         posS.alloc(H); kv.alloc(H); hb.alloc((uint64_t)n + 1);
         auto kvIn = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint32_t>(0u),
-                                                     MakeHeadKV{h.len, h.isa});
+                                                     MakeHeadKV{h.len, h.isa, h.smaller, h.tonext});
         size_t b = 0;
         HIPCHK(rocprim::radix_sort_pairs(nullptr, b, h.pos, posS.p, kvIn, kv.p, (size_t)H, 0u, (unsigned)bN, st));
         HIPCHK(rocprim::radix_sort_pairs(scratch(b), b, h.pos, posS.p, kvIn, kv.p, (size_t)H, 0u, (unsigned)bN, st));
@@ -1269,7 +1275,9 @@ struct Engine {
         DBuf<uint32_t> bigList;
         bigList.alloc((uint64_t)n + 1);
         HIPCHK(hipMemsetAsync(bigList.p, 0, 4, st));
-        mk_grp_seg(posS.p, hb.p, kv.p, H, bN, bL, gk2.p, perm2.p, bigList.p, env_u32("CMSBWT_GROUP_SMALL", 64), st);
+        tsS.alloc(H); smS.alloc(H);
+        mk_grp_seg(posS.p, hb.p, kv.p, H, bN, bL, gk2.p, perm2.p, tsS.p, smS.p, bigList.p,
+                   env_u32("CMSBWT_GROUP_SMALL", 64), st);
         kv.release();
         posS.release();
         const uint32_t nb = read1(bigList.p);
@@ -1287,6 +1295,7 @@ struct Engine {
           mk_gather_kp(bidx.p, B, gk2.p, perm2.p, kB.p, pB.p, st);
           sort_pairs(kB.p, kB2.p, pB.p, pB2.p, B, 2 * bN + bL);  // stable: idx order kept per key
           mk_scatter_kp(bidx.p, B, kB2.p, pB2.p, gk2.p, perm2.p, st);
+          mk_grp_big_fields(bidx.p, B, perm2.p, h, tsS.p, smS.p, st);
         }
       }
     } else if (packed) {  // one sort on the composite key
@@ -1318,9 +1327,10 @@ struct Engine {
     aPos.alloc(K); aLen.alloc(K); aIsa.alloc(K); aUntil.alloc(K); aCount.alloc(K); aFirst.alloc(K);
     aSmall.alloc(K);
     ItemsSoA A0{aPos.p, aLen.p, aIsa.p, aSmall.p, aUntil.p, aCount.p, aFirst.p, nullptr, nullptr, nullptr};
-    if (packed) mk_item_fill64(gk2.p, P.p, key.p, key2.p, h, H, bN, bL, A0, st);
+    if (packed) mk_item_fill64(gk2.p, P.p, key.p, key2.p, h, posFirst ? tsS.p : nullptr, smS.p, H, bN, bL, A0, st);
     else mk_item_fill(P.p, key.p, key2.p, h, H, A0, st);
     gk2.release();
+    tsS.release(); smS.release();
     mk_item_count(aFirst.p, aCount.p, K, H, st);
     key.release();
     key2.release();

@@ -18,9 +18,9 @@ struct HeadsSoA {
   uint16_t* nexthead;
 };
 
-// A head's grouping fields carried through the position radix sort (12 B).
+// A head's grouping fields carried through the position radix sort (16 B).
 struct HeadKV {
-  uint32_t idx, len, isa;
+  uint32_t idx, len, isa, tonext;  // len: bit 31 = smaller
 };
 
 // Items (distinct (pos, len, isaNext) keys) in map order: pos ascending, then

@@ -62,6 +62,7 @@ constexpr uint32_t kGrpBlock = 256, kGrpHalo = 64;  // segments of <= kGrpHalo h
 __global__ void __launch_bounds__(256) k_grp_seg(const uint32_t* __restrict__ posS, const uint32_t* __restrict__ hb,
                                                  const HeadKV* __restrict__ kv, uint32_t H, int bN, int bL,
                                                  unsigned long long* __restrict__ key, uint32_t* __restrict__ perm,
+                                                 uint32_t* __restrict__ tsOut, uint8_t* __restrict__ smOut,
                                                  uint32_t* __restrict__ bigList, uint32_t maxSmall) {
   // one thread per sorted head: its rank inside its position's segment by
   // counting over the segment, staged in LDS with a halo either side
@@ -72,7 +73,7 @@ __global__ void __launch_bounds__(256) k_grp_seg(const uint32_t* __restrict__ po
     const int64_t j = base + i;
     if (j >= 0 && j < (int64_t)H) {
       const HeadKV w = kv[j];
-      lk[i] = ((unsigned long long)w.len << bN) | w.isa;
+      lk[i] = ((unsigned long long)(w.len & 0x7fffffffu) << bN) | w.isa;
     }
   }
   __syncthreads();
@@ -85,7 +86,7 @@ __global__ void __launch_bounds__(256) k_grp_seg(const uint32_t* __restrict__ po
   const unsigned long long me = lk[threadIdx.x + kGrpHalo];
   if (e - b > min(maxSmall, kGrpHalo)) {
     key[k] = hp | me;
-    perm[k] = v.idx;
+    perm[k] = v.idx;  // (tonext / smaller of these follow the radix sort: k_grp_big_fields)
     if (k == b) bigList[1 + atomicAdd(bigList, 1u)] = p;
     return;
   }
@@ -97,6 +98,16 @@ __global__ void __launch_bounds__(256) k_grp_seg(const uint32_t* __restrict__ po
   }
   key[b + r] = hp | me;
   perm[b + r] = v.idx;
+  tsOut[b + r] = v.tonext;
+  smOut[b + r] = (uint8_t)(v.len >> 31);
+}
+__global__ void k_grp_big_fields(const uint32_t* __restrict__ idx, uint32_t B, const uint32_t* __restrict__ perm,
+                                 HeadsSoA h, uint32_t* __restrict__ tsOut, uint8_t* __restrict__ smOut) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= B) return;
+  const uint32_t k = idx[i], a = perm[k];
+  tsOut[k] = h.tonext[a];
+  smOut[k] = h.smaller[a];
 }
 // big segments: sizes, then their element indices (positions ascending)
 __global__ void k_grp_big_sizes(const uint32_t* __restrict__ pos, uint32_t nb, const uint32_t* __restrict__ hb,
@@ -135,6 +146,7 @@ __global__ void k_item_flags64(const unsigned long long* __restrict__ key, uint3
 }
 __global__ void k_item_fill64(const unsigned long long* __restrict__ key, const uint32_t* __restrict__ perm,
                               const uint32_t* __restrict__ flag, const uint32_t* __restrict__ itemIncl, HeadsSoA h,
+                              const uint32_t* __restrict__ tsS, const uint8_t* __restrict__ smS,
                               uint64_t H, int bN, int bL, ItemsSoA it) {
   uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (k >= H || !flag[k]) return;
@@ -144,8 +156,8 @@ __global__ void k_item_fill64(const unsigned long long* __restrict__ key, const 
   it.pos[q] = (uint32_t)(v >> (bN + bL));
   it.len[q] = (uint32_t)((v >> bN) & ((1ull << bL) - 1));
   it.isa[q] = (uint32_t)(v & ((1ull << bN) - 1));
-  it.smaller[q] = h.smaller[a];
-  it.until[q] = h.tonext[a];
+  it.smaller[q] = tsS ? smS[k] : h.smaller[a];  // the first member's (sorted order: no gather)
+  it.until[q] = tsS ? tsS[k] : h.tonext[a];
   it.first[q] = (uint32_t)k;
 }
 
@@ -1702,8 +1714,9 @@ void mk_item_flags64(const unsigned long long* key, uint32_t* flag, uint64_t H, 
   if (H) hipLaunchKernelGGL(k_item_flags64, g1(H), dim3(256), 0, st, key, flag, H);
 }
 void mk_item_fill64(const unsigned long long* key, const uint32_t* perm, const uint32_t* flag, const uint32_t* incl,
-                    const HeadsSoA& h, uint64_t H, int bN, int bL, const ItemsSoA& it, hipStream_t st) {
-  if (H) hipLaunchKernelGGL(k_item_fill64, g1(H), dim3(256), 0, st, key, perm, flag, incl, h, H, bN, bL, it);
+                    const HeadsSoA& h, const uint32_t* tsS,
+                    const uint8_t* smS, uint64_t H, int bN, int bL, const ItemsSoA& it, hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_item_fill64, g1(H), dim3(256), 0, st, key, perm, flag, incl, h, tsS, smS, H, bN, bL, it);
 }
 void mk_slot_mark(const uint32_t* slot, uint32_t K, uint32_t* mark, hipStream_t st) {
   if (K) hipLaunchKernelGGL(k_slot_mark, g1(K), dim3(256), 0, st, slot, K, mark);
@@ -1928,8 +1941,14 @@ void mk_el_wr_emit(const ElemIn& w, uint32_t V, const unsigned long long* runOff
                             runChar);
 }
 void mk_grp_seg(const uint32_t* posS, const uint32_t* hb, const HeadKV* kv, uint32_t H, int bN, int bL,
-                unsigned long long* key, uint32_t* perm, uint32_t* bigList, uint32_t maxSmall, hipStream_t st) {
-  if (H) hipLaunchKernelGGL(k_grp_seg, dim3((H + kGrpBlock - 1) / kGrpBlock), dim3(kGrpBlock), 0, st, posS, hb, kv, H, bN, bL, key, perm, bigList, maxSmall);
+                unsigned long long* key, uint32_t* perm, uint32_t* tsOut, uint8_t* smOut, uint32_t* bigList,
+                uint32_t maxSmall, hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_grp_seg, dim3((H + kGrpBlock - 1) / kGrpBlock), dim3(kGrpBlock), 0, st, posS, hb, kv, H, bN,
+                            bL, key, perm, tsOut, smOut, bigList, maxSmall);
+}
+void mk_grp_big_fields(const uint32_t* idx, uint32_t B, const uint32_t* perm, const HeadsSoA& h, uint32_t* tsOut,
+                       uint8_t* smOut, hipStream_t st) {
+  if (B) hipLaunchKernelGGL(k_grp_big_fields, g1(B), dim3(256), 0, st, idx, B, perm, h, tsOut, smOut);
 }
 void mk_grp_big_sizes(const uint32_t* pos, uint32_t nb, const uint32_t* hb, uint32_t* sz, hipStream_t st) {
   if (nb) hipLaunchKernelGGL(k_grp_big_sizes, g1(nb), dim3(256), 0, st, pos, nb, hb, sz);

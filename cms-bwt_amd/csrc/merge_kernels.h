@@ -31,7 +31,10 @@ void mk_item_flags(const uint32_t* perm, const HeadsSoA& h, uint32_t* flag, uint
 void mk_group_key(const HeadsSoA& h, uint64_t H, int bN, int bL, unsigned long long* key, hipStream_t st);
 // grouping, position first (radix by pos, then per-position segments)
 void mk_grp_seg(const uint32_t* posS, const uint32_t* hb, const HeadKV* kv, uint32_t H, int bN, int bL,
-                unsigned long long* key, uint32_t* perm, uint32_t* bigList, uint32_t maxSmall, hipStream_t st);
+                unsigned long long* key, uint32_t* perm, uint32_t* tsOut, uint8_t* smOut, uint32_t* bigList,
+                uint32_t maxSmall, hipStream_t st);
+void mk_grp_big_fields(const uint32_t* idx, uint32_t B, const uint32_t* perm, const HeadsSoA& h, uint32_t* tsOut,
+                       uint8_t* smOut, hipStream_t st);
 void mk_grp_big_sizes(const uint32_t* pos, uint32_t nb, const uint32_t* hb, uint32_t* sz, hipStream_t st);
 void mk_grp_big_expand(const uint32_t* pos, uint32_t nb, const uint32_t* hb, const uint32_t* off, uint32_t* idx,
                        hipStream_t st);
@@ -41,7 +44,8 @@ void mk_scatter_kp(const uint32_t* idx, uint32_t B, const unsigned long long* ke
                    unsigned long long* key, uint32_t* perm, hipStream_t st);
 void mk_item_flags64(const unsigned long long* key, uint32_t* flag, uint64_t H, hipStream_t st);
 void mk_item_fill64(const unsigned long long* key, const uint32_t* perm, const uint32_t* flag, const uint32_t* incl,
-                    const HeadsSoA& h, uint64_t H, int bN, int bL, const ItemsSoA& it, hipStream_t st);
+                    const HeadsSoA& h, const uint32_t* tsS, const uint8_t* smS, uint64_t H, int bN, int bL,
+                    const ItemsSoA& it, hipStream_t st);
 void mk_item_fill(const uint32_t* perm, const uint32_t* flag, const uint32_t* incl, const HeadsSoA& h,
                   uint64_t H, const ItemsSoA& it, hipStream_t st);
 void mk_item_count(const uint32_t* first, uint32_t* count, uint32_t K, uint32_t H, hipStream_t st);

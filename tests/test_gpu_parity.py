@@ -122,12 +122,15 @@ def test_grouping_position_first(engine, oracle, tmp_path, case, env):
     _compare(engine, oracle, tmp_path, case, env=env)
 
 
-@pytest.mark.parametrize("small", ["2", "1000000"], ids=["radix_groups", "thread_groups"])
+@pytest.mark.parametrize("env", [{"CMSBWT_DBL_SMALL": "2"}, {"CMSBWT_DBL_SMALL": "1000000"},
+                                 {"CMSBWT_DBL_LEADERS": "1"}, {"CMSBWT_DBL_LEADERS": "1", "CMSBWT_DBL_SMALL": "2"}],
+                         ids=["radix_groups", "member_ranks", "leader_sorts", "leader_radix"])
 @pytest.mark.parametrize("case", cases.small_cases()[:4], ids=lambda c: c[0])
-def test_doubling_group_paths(engine, oracle, tmp_path, case, small):
+def test_doubling_group_paths(engine, oracle, tmp_path, case, env):
     """Head-string suffix sort: groups above CMSBWT_DBL_SMALL members go through
-    the radix path, smaller ones are sorted per thread; both give the oracle's SA."""
-    _compare(engine, oracle, tmp_path, case, env={"CMSBWT_DBL_SMALL": small})
+    the radix path, smaller ones are ranked per member (default) or sorted by
+    their leader thread; all give the oracle's SA."""
+    _compare(engine, oracle, tmp_path, case, env=env)
 
 
 @pytest.mark.parametrize("geom", [{"CMSBWT_RUN_BIN_SHIFT": "3"},
