@@ -1600,11 +1600,11 @@ struct Engine {
         std::swap(act.p, act2.p);
       }
     }
-    grp.release();
-    DBuf<uint32_t> headRank;
-    headRank.alloc(H);
+    // Every group is a single head now, and a group's label is its first sa
+    // position: grp[idx] = 1 + rank of head idx (FN:1468-1471's rankToHead),
+    // so the inverse permutation needs no scatter.
     bwtHeads.alloc(H);
-    mk_head_ranks(saT.p, hChar.p, H, headRank.p, bwtHeads.p, st);
+    mk_head_chars(saT.p, hChar.p, H, bwtHeads.p, st);
 
     // ---- next-head ranks, sorted per item (FN:1480-1494): small items by an
     // in-place insertion sort, large ones by one global (item, nhr) sort
@@ -1614,11 +1614,11 @@ struct Engine {
       {
         DBuf<uint32_t> nbi;
         nbi.alloc(H);
-        mk_nhr_slot(Pm.p, headRank.p, hNext.p, H, nbi.p, nhr.p, st);
+        mk_nhr_slot(Pm.p, grp.p, 1u, hNext.p, H, nbi.p, nhr.p, st);
       }
       sort_nhr_items(S, K, itemOfSlot.p, nhr.p, H);
     }
-    headRank.release();
+    grp.release();
     Pm.release();
 
     // ---- counterSmallerThanHead (FN:1523-1603)

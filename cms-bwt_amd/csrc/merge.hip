@@ -668,11 +668,17 @@ __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ ite
 // next-head rank of each member, in slot order (FN:1480-1494): first per head
 // in document order (nexthead is small, so headRank[idx + nexthead] is read
 // almost sequentially), then one gather through the slot permutation
-__global__ void k_nhr_idx(const uint32_t* __restrict__ headRank, const uint16_t* __restrict__ nexthead, uint32_t H,
-                          uint32_t* __restrict__ nbi) {
+__global__ void k_nhr_idx(const uint32_t* __restrict__ headRank, uint32_t sub, const uint16_t* __restrict__ nexthead,
+                          uint32_t H, uint32_t* __restrict__ nbi) {
   uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= H) return;
-  nbi[idx] = headRank[idx + nexthead[idx]];
+  nbi[idx] = headRank[idx + nexthead[idx]] - sub;
+}
+// BWTheads (FN:1471): the character before each head, in head-rank order
+__global__ void k_head_chars(const uint32_t* __restrict__ sa, const uint8_t* __restrict__ lchar, uint32_t H,
+                             uint8_t* __restrict__ bwtHeads) {
+  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < H) bwtHeads[r] = lchar[sa[r + 1]];
 }
 __global__ void k_nhr_slot(const uint32_t* __restrict__ Pm, const uint32_t* __restrict__ nbi, uint32_t H,
                            uint32_t* __restrict__ nhr) {
@@ -1739,10 +1745,13 @@ void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_
     hipLaunchKernelGGL(k_ranks_slot, g1(H), dim3(256), 0, st, it, itemOfSlot, Pm, H, rankBase, gBase, n, T, sa, grp,
                        actv);
 }
-void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, const uint16_t* nexthead, uint32_t H, uint32_t* nbi,
-                 uint32_t* nhr, hipStream_t st) {
+void mk_head_chars(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint8_t* bwtHeads, hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_head_chars, g1(H), dim3(256), 0, st, sa, lchar, H, bwtHeads);
+}
+void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, uint32_t sub, const uint16_t* nexthead, uint32_t H,
+                 uint32_t* nbi, uint32_t* nhr, hipStream_t st) {
   if (!H) return;
-  hipLaunchKernelGGL(k_nhr_idx, g1(H), dim3(256), 0, st, headRank, nexthead, H, nbi);
+  hipLaunchKernelGGL(k_nhr_idx, g1(H), dim3(256), 0, st, headRank, sub, nexthead, H, nbi);
   hipLaunchKernelGGL(k_nhr_slot, g1(H), dim3(256), 0, st, Pm, nbi, H, nhr);
 }
 void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigList, hipStream_t st) {

@@ -61,8 +61,10 @@ void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_
                    const uint32_t* rankBase, const uint32_t* gBase, uint32_t n, int32_t* T, uint32_t* sa,
                    uint32_t* grp, uint32_t* actv, hipStream_t st);
 // nbi: H scratch words (next-head rank per head in document order)
-void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, const uint16_t* nexthead, uint32_t H, uint32_t* nbi,
-                 uint32_t* nhr, hipStream_t st);
+// headRank - sub = rank of each head (sub 1 with the final group labels)
+void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, uint32_t sub, const uint16_t* nexthead, uint32_t H,
+                 uint32_t* nbi, uint32_t* nhr, hipStream_t st);
+void mk_head_chars(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint8_t* bwtHeads, hipStream_t st);
 void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigList, hipStream_t st);
 void mk_nhr_big_fill(const uint32_t* items, const uint32_t* off, uint32_t nb, const ItemsSoA& it, const uint32_t* nhr,
                      unsigned long long* key, uint32_t* slots, hipStream_t st);
