@@ -1096,6 +1096,20 @@ constexpr uint32_t kTgtQ = 256;     // undecided queries listed per wave before 
 constexpr uint32_t kTgtS = 320;     // queries listed per wave for binary searches
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
+// v (wave-uniform) in the lanes of mask m, 0 elsewhere: one v_cndmask on the
+// SGPR-pair mask (keeps decision masks out of VGPRs)
+__device__ __forceinline__ uint32_t sel_u32(uint32_t v, uint64_t m) {
+  uint32_t r;
+  asm volatile("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(m));
+  return r;
+}
+// unsigned compare of each lane, as a wave mask (llvm.amdgcn.icmp predicates)
+constexpr int kNE = 33, kUGT = 34, kUGE = 35, kULT = 36, kULE = 37;
+template <int P>
+__device__ __forceinline__ uint64_t ucmp(uint32_t a, uint32_t b) {
+  return __builtin_amdgcn_uicmp(a, b, P);
+}
+
 __global__ void __launch_bounds__(256) k_counter_tgt(CounterArgs A) {
   __shared__ uint4 recG[4][kTgtRec];  // 16 KB: per wave, the records reaching its targets
   __shared__ uint32_t qL[4][kTgtQ];   // 8 KB
@@ -1130,6 +1144,7 @@ __global__ void __launch_bounds__(256) k_counter_tgt(CounterArgs A) {
     nF3 = nF == 3;
   }
   const bool hasF0 = fs0 != kNoSlot, hasF1 = fs1 != kNoSlot, hasF2 = fs2 != kNoSlot;
+  const uint64_t hasM = __ballot(has), hasF0M = __ballot(hasF0), hasF1M = __ballot(hasF1);  // per wave
   const uint32_t flags = (hasF0 ? 1u : 0u) | (hasF1 ? 2u : 0u) | (hasF2 ? 4u : 0u) | (nS3 ? 8u : 0u) | (nF3 ? 16u : 0u);
   for (uint32_t k = 0; k < 6; k++) accL[k][tid] = 0;
   // accumulators: first F item (f), S items top 0..2, F items 1..2
@@ -1176,30 +1191,34 @@ __global__ void __launch_bounds__(256) k_counter_tgt(CounterArgs A) {
           const uint32_t cq = __builtin_amdgcn_readlane(my.z, e) & 0x7fffffffu;
           const uint32_t L = __builtin_amdgcn_readlane(my.x, e) - t;
           const uint32_t aO = ab & 0xffffu, bO = ab >> 16;
-          const bool inr = (toff >= aO) & (toff <= bO);
           // lower_bound (FN:1534) settled by the two longest items of the
-          // query's class (k_counter_win's fast tests, exact lens; bitwise
-          // & and | keep the body free of branches); the rest is listed
-          bool sl;
-          const bool vh = inr & has;
+          // query's class (k_counter_win's fast tests, exact lens).  The
+          // decisions are wave masks (SGPR pairs; the per-target flags are
+          // loop-invariant masks) and an add is one v_cndmask on its mask.
+          const uint64_t mR = ucmp<kUGE>(toff, aO) & ucmp<kULE>(toff, bO);
+          const uint64_t mIn = mR & hasM;
+          const uint32_t cqv = __builtin_amdgcn_readfirstlane(cq);
+          uint64_t mF0, mX, msl;
           if (S) {  // smaller=true: S items ascending, then F items
-            const bool c1 = (L > sl0) & (L != fl0);  // past every S item: f (or end)
-            const bool c2 = (L < sl0) & (L > sl1);   // the longest S item
-            aF0 += (vh & c1 & hasF0) ? cq : 0u;
-            aS0 += (vh & c2) ? cq : 0u;
-            nGood += (vh & ((c1 & hasF0) | c2)) ? 1u : 0u;
-            sl = vh & !c1 & !c2;
+            const uint64_t m1 = ucmp<kUGT>(L, sl0) & ucmp<kNE>(L, fl0);  // past every S item: f (or end)
+            const uint64_t m2 = ucmp<kULT>(L, sl0) & ucmp<kUGT>(L, sl1);   // the longest S item
+            mF0 = mIn & m1 & hasF0M;
+            mX = mIn & m2;
+            aS0 += sel_u32(cqv, mX);
+            msl = mIn & ~(m1 | m2);
           } else {  // smaller=false: F items descending
-            const bool c1 = L > fl0;                 // f
-            const bool c2 = (L < fl0) & (L > fl1);   // the second F item (or end)
-            aF0 += (vh & c1 & hasF0) ? cq : 0u;
-            aF1 += (vh & c2 & hasF1) ? cq : 0u;
-            nGood += (vh & ((c1 & hasF0) | (c2 & hasF1))) ? 1u : 0u;
-            sl = vh & !c1 & !c2;
+            const uint64_t m1 = ucmp<kUGT>(L, fl0);                       // f
+            const uint64_t m2 = ucmp<kULT>(L, fl0) & ucmp<kUGT>(L, fl1);   // the second F item (or end)
+            mF0 = mIn & m1 & hasF0M;
+            mX = mIn & m2 & hasF1M;
+            aF1 += sel_u32(cqv, mX);
+            msl = mIn & ~(m1 | m2);
           }
-          nNothing += (inr & !has) ? 1u : 0u;
-          const uint64_t sm = __ballot(sl);
-          if (sl) {
+          aF0 += sel_u32(cqv, mF0);
+          nGood += (uint32_t)__popcll(mF0 | mX);
+          nNothing += (uint32_t)__popcll(mR & ~hasM);
+          const uint64_t sm = msl;
+          if ((sm >> lane) & 1) {
             const uint32_t rk =
                 __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
             myQ[qn + rk] = (r + e) | (toff << 16);
@@ -1297,8 +1316,10 @@ __global__ void __launch_bounds__(256) k_counter_tgt(CounterArgs A) {
   if (aS0) atomicAdd(&A.counter[ss0], (unsigned long long)aS0);
   if (aS1) atomicAdd(&A.counter[ss1], (unsigned long long)aS1);
   if (aS2) atomicAdd(&A.counter[ss2], (unsigned long long)aS2);
-  qs.good += nGood;
-  qs.nothing += nNothing;
+  if (lane == 0) {  // wave-uniform counts
+    qs.good += nGood;
+    qs.nothing += nNothing;
+  }
   if (qs.bad) atomicAdd(&A.stats[0], (unsigned long long)qs.bad);
   if (qs.good) atomicAdd(&A.stats[1], (unsigned long long)qs.good);
   if (qs.nothing) atomicAdd(&A.stats[2], (unsigned long long)qs.nothing);
