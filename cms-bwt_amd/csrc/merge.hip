@@ -1283,8 +1283,23 @@ __global__ void __launch_bounds__(256) k_counter_tgt(CounterArgs A) {
     if (tid < 8) nG[tid] = 0;
     __syncthreads();  // the previous chunk's lists are no longer read
     if (tid < nr) {
+      // every chunk mixes crossing items (they reach the first waves'
+      // targets) and starting items taken from all four quarters of the
+      // window, so the four waves get similar lists between two barriers
       const uint32_t j = ch + tid;
-      const uint32_t q = j < nCross ? A.crossList[c0 + j] : iBeg + (j - nCross);
+      const uint32_t nSt = nList - nCross;
+      const uint32_t cj = (uint32_t)((uint64_t)j * nCross / nList);
+      const bool isCross = (uint32_t)((uint64_t)(j + 1) * nCross / nList) > cj;
+      uint32_t q;
+      if (isCross) {
+        q = A.crossList[c0 + cj];
+      } else {
+        const uint32_t sj = j - cj, qs4 = (nSt + 3) >> 2;  // quarter-interleaved starting items
+        const uint32_t rq = sj & 3, kq = sj >> 2;
+        // the first (nSt mod 4 or 4) quarters hold qs4 items, the rest qs4 - 1
+        const uint32_t full = nSt - 4 * (qs4 - 1);  // quarters with qs4 items (1..4)
+        q = iBeg + (rq < full ? rq * qs4 : full * qs4 + (rq - full) * (qs4 - 1)) + kq;
+      }
       const uint32_t p = it.pos[q], u = it.until[q];
       if (u) {
         const uint32_t lo = max(p + 1, T0);
