@@ -62,7 +62,7 @@ def cpu_baseline(ref_len, copies, p, seed, rle=True):
             "seconds": round(t_coll, 3)}
 
 
-PMC_FILE = "r02_pmc.json"  # tools/gpu_prof_r.sh + tools/pmc_main.py
+PMC_FILE = "r02_pmc.json"  # tools/gpu_prof_r.sh + tools/pmc_main.py (this round's kernels)
 
 
 def pmc_traffic(args, kernel="k_ms_walk2"):
@@ -167,7 +167,7 @@ def main():
     t_ms = st.ms_walk_kernel_ms / 1e3
     achieved = b_ms / t_ms / 1e9 if t_ms > 0 else 0.0
     traffic, traffic_src = pmc_traffic(args) if world == 1 else (None, None)
-    ctraffic, _ = pmc_traffic(args, "k_counter_win") if world == 1 else (None, None)
+    ctraffic, _ = pmc_traffic(args, "k_counter_tgt") if world == 1 else (None, None)
     c_ms = st.counter_kernel_ms
     out = {
         "metric": ("collection MB/s to .bwt" if args.plain else
@@ -194,8 +194,8 @@ def main():
                      "traffic_GBps": round(traffic / t_ms / 1e9, 1) if traffic and t_ms > 0 else None,
                      "traffic_frac": round(traffic / t_ms / 1e9 / HBM_PEAK_GBS, 4) if traffic and t_ms > 0 else None},
         # the merge's largest kernel (counterSmallerThanHead, FN:1523-1603):
-        # LDS- and VALU-bound, measured HBM traffic for reference
-        "counter_kernel": {"kernel": "k_counter_win", "kernel_ms": round(c_ms, 3),
+        # register/LDS-bound, measured HBM traffic for reference
+        "counter_kernel": {"kernel": "k_counter_tgt", "kernel_ms": round(c_ms, 3),
                            "queries": int(st.counter_good + st.counter_bad + st.counter_nothing),
                            "traffic": ctraffic,
                            "traffic_GBps": round(ctraffic / (c_ms / 1e3) / 1e9, 1) if ctraffic and c_ms > 0 else None},

@@ -13,7 +13,7 @@ for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HI
            "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES" \
            "SQ_ACTIVE_INST_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES"; do
   i=$((i+1))
-  timeout -k 10 120 rocprofv3 --pmc $grp --kernel-include-regex "ms_walk2|counter_win" -d $OUT/p$i -o p$i --output-format csv -- $B1 > $OUT/p$i.log 2>&1 || echo "pass $i failed"
+  timeout -k 10 120 rocprofv3 --pmc $grp --kernel-include-regex "ms_walk2|counter_tgt" -d $OUT/p$i -o p$i --output-format csv -- $B1 > $OUT/p$i.log 2>&1 || echo "pass $i failed"
 done
 python3 tools/pmc_summary.py $OUT > $OUT/pmc_summary.json
 head -30 $OUT/kt_summary.txt

@@ -13,7 +13,8 @@ vals = collections.defaultdict(lambda: collections.defaultdict(dict))  # kernel 
 for f in sorted(glob.glob(os.path.join(root, "p*", "p*_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        key = "k_ms_walk2" if "ms_walk2" in name else "k_counter_win" if "counter_win" in name else name[:60]
+        key = ("k_ms_walk2" if "ms_walk2" in name else "k_counter_tgt" if "counter_tgt" in name
+               else "k_counter_win" if "counter_win" in name else name[:60])
         vals[key][r["Counter_Name"]][r["Dispatch_Id"]] = float(r["Counter_Value"])
 out = {}
 for k, cs in vals.items():

@@ -13,7 +13,8 @@ disp = collections.defaultdict(set)
 for f in sorted(glob.glob(os.path.join(root, "p*", "p*_counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        key = "k_ms_walk2" if "ms_walk2" in name else "k_counter_win" if "counter_win" in name else name[:60]
+        key = ("k_ms_walk2" if "ms_walk2" in name else "k_counter_tgt" if "counter_tgt" in name
+               else "k_counter_win" if "counter_win" in name else name[:60])
         per[key][r["Counter_Name"]] += float(r["Counter_Value"])
         disp[(key, r["Counter_Name"])].add(r["Dispatch_Id"])
 out = {}
