@@ -1019,6 +1019,7 @@ struct Engine {
       hasHead.alloc(R.n);
       hasHead.zero(st);
       sync();
+      runsValid = true;
       orderInvariant = true;
       walked = true;
       stats.order_invariant = 1;
@@ -1117,28 +1118,11 @@ struct Engine {
     errf.zero(st);
     launch_finalize(R, h, H, docEnd.p, (uint32_t)ndocs, dtext.p, ddoc.p, errf.p, hDoc.p, st);
     HIPCHK(hipGetLastError());
-    // run buckets (diff, hasHead) through position bins, no random atomics
-    diff.alloc((uint64_t)R.n + 1);
-    hasHead.alloc(R.n);
-    {
-      // CMSBWT_RUN_BIN_SHIFT / CMSBWT_RUN_BIN_GLOBAL: smaller bins and the
-      // global-counter path, for the tests
-      const uint32_t sh = std::max(1u, std::min(kRunBinShift, env_u32("CMSBWT_RUN_BIN_SHIFT", kRunBinShift)));
-      const bool global = env_u32("CMSBWT_RUN_BIN_GLOBAL", 0) != 0;
-      const uint32_t nb = (R.n >> sh) + 1;
-      DBuf<uint32_t> binCnt, binOff, binCur, vals;
-      binCnt.alloc((uint64_t)nb + 1);
-      binCnt.zero(st);
-      binOff.alloc((uint64_t)nb + 1);
-      binCur.alloc(nb);
-      vals.alloc(2ull * H + 1);
-      launch_run_bin_count(h, H, R.n, nb, sh, global, binCnt.p, st);
-      exscan(binCnt.p, binOff.p, 0u, (uint64_t)nb + 1);
-      HIPCHK(hipMemcpyAsync(binCur.p, binOff.p, (uint64_t)nb * 4, hipMemcpyDeviceToDevice, st));
-      launch_run_bin_scatter(h, H, R.n, nb, sh, global, binCur.p, vals.p, st);
-      launch_run_bin_emit(vals.p, binOff.p, R.n, nb, sh, diff.p, hasHead.p, st);
-      HIPCHK(hipGetLastError());
-    }
+    // run buckets (diff, hasHead): from the grouping's position sort in
+    // merge(), or through position bins on demand (ensure_runs)
+    runsValid = false;
+    if (env_u32("CMSBWT_RUN_BINS", 0) || env_u32("CMSBWT_RUN_BIN_SHIFT", 0) || env_u32("CMSBWT_RUN_BIN_GLOBAL", 0))
+      ensure_runs();
     uint32_t ef = read1(errf.p);
     orderInvariant = (ef & 8u) == 0;
     if (ef & 1) throw InputError{CMSBWT_EINPUT, "internal: match ends not monotone inside a document"};
@@ -1226,6 +1210,36 @@ struct Engine {
     plan.valid = true;
   }
 
+  // Run buckets (FN:1162-1171, 1203) through position bins, no random
+  // atomics: head i covers [pos_i, pos_i + start_{i+1} - start_i).
+  bool runsValid = false;
+  void ensure_runs() {
+    if (runsValid) return;
+    HeadsSoA h = heads();
+    diff.alloc((uint64_t)R.n + 1);
+    hasHead.alloc(R.n);
+    {
+      // CMSBWT_RUN_BIN_SHIFT / CMSBWT_RUN_BIN_GLOBAL: smaller bins and the
+      // global-counter path, for the tests
+      const uint32_t sh = std::max(1u, std::min(kRunBinShift, env_u32("CMSBWT_RUN_BIN_SHIFT", kRunBinShift)));
+      const bool global = env_u32("CMSBWT_RUN_BIN_GLOBAL", 0) != 0;
+      const uint32_t nb = (R.n >> sh) + 1;
+      DBuf<uint32_t> binCnt, binOff, binCur, vals;
+      binCnt.alloc((uint64_t)nb + 1);
+      binCnt.zero(st);
+      binOff.alloc((uint64_t)nb + 1);
+      binCur.alloc(nb);
+      vals.alloc(2ull * H + 1);
+      launch_run_bin_count(h, H, R.n, nb, sh, global, binCnt.p, st);
+      exscan(binCnt.p, binOff.p, 0u, (uint64_t)nb + 1);
+      HIPCHK(hipMemcpyAsync(binCur.p, binOff.p, (uint64_t)nb * 4, hipMemcpyDeviceToDevice, st));
+      launch_run_bin_scatter(h, H, R.n, nb, sh, global, binCur.p, vals.p, st);
+      launch_run_bin_emit(vals.p, binOff.p, R.n, nb, sh, diff.p, hasHead.p, st);
+      HIPCHK(hipGetLastError());
+    }
+    runsValid = true;
+  }
+
   HeadsSoA heads() {
     return HeadsSoA{hStart.p, hPos.p, hLen.p, hSmall.p, hChar.p, hIsa.p, hTonext.p, hNext.p};
   }
@@ -1272,12 +1286,21 @@ struct Engine {
         HIPCHK(rocprim::radix_sort_pairs(nullptr, b, h.pos, posS.p, kvIn, kv.p, (size_t)H, 0u, (unsigned)bN, st));
         HIPCHK(rocprim::radix_sort_pairs(scratch(b), b, h.pos, posS.p, kvIn, kv.p, (size_t)H, 0u, (unsigned)bN, st));
         mk_pos_begin(posS.p, H, n, hb.p, st);
+        // run buckets from the sorted heads: starts per position from hb,
+        // ends counted in k_grp_seg (LDS histogram near the block's positions)
+        const bool runsHere = !runsValid;
+        if (runsHere) {
+          diff.alloc((uint64_t)n + 1);
+          hasHead.alloc(n);
+          mk_run_starts(hb.p, n, diff.p, hasHead.p, st);
+        }
         DBuf<uint32_t> bigList;
         bigList.alloc((uint64_t)n + 1);
         HIPCHK(hipMemsetAsync(bigList.p, 0, 4, st));
         tsS.alloc(H); smS.alloc(H);
         mk_grp_seg(posS.p, hb.p, kv.p, H, bN, bL, gk2.p, perm2.p, tsS.p, smS.p, bigList.p,
-                   env_u32("CMSBWT_GROUP_SMALL", 64), st);
+                   env_u32("CMSBWT_GROUP_SMALL", 64), runsHere ? diff.p : nullptr, n, st);
+        if (runsHere) runsValid = true;
         kv.release();
         posS.release();
         const uint32_t nb = read1(bigList.p);
@@ -1481,6 +1504,7 @@ struct Engine {
     HeadsSoA h = heads();
     ItemSet IS;
     group_items(h, H, n, IS);
+    ensure_runs();  // (the position-first grouping already counted them)
     K = IS.K;
     DBuf<uint32_t>& P = IS.P;
     DBuf<uint32_t>& sPos = IS.pos;
@@ -1938,6 +1962,7 @@ struct Engine {
     in(hTonext.p, a[6], (uint64_t)H * 4); in(hNext.p, a[7], (uint64_t)H * 2);
     in(diff.p, a[8], ((uint64_t)R.n + 1) * 4); in(hasHead.p, a[9], R.n);
     sync();
+    runsValid = true;
     ndocs = nd;
     chars = nchars;
     collLoaded = walked = true;
@@ -1999,8 +2024,8 @@ struct Engine {
     if (name == "h_isa") return cp(hIsa.p, (uint64_t)H * 4);
     if (name == "h_tonext") return cp(hTonext.p, (uint64_t)H * 4);
     if (name == "h_nexthead") return cp(hNext.p, (uint64_t)H * 2);
-    if (name == "diff") return cp(diff.p, ((uint64_t)R.n + 1) * 4);
-    if (name == "hashead") return cp(hasHead.p, R.n);
+    if (name == "diff") { ensure_runs(); return cp(diff.p, ((uint64_t)R.n + 1) * 4); }
+    if (name == "hashead") { ensure_runs(); return cp(hasHead.p, R.n); }
     if (!merged) throw InputError{CMSBWT_EARG, "run merge first"};
     if (dm.on) throw InputError{CMSBWT_EARG, "merge stage arrays are not kept by the sharded merge"};
     if (name == "bucket") return cp(bucket.p, (uint64_t)R.n * 8);

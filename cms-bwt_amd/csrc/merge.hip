@@ -59,14 +59,17 @@ __global__ void k_group_key(const HeadsSoA h, uint64_t H, int bN, int bL, unsign
 // pos|len|isaNext of every sorted head (what the one-sort path produces) and
 // its idx.  Segments longer than maxSmall are listed for a radix sort.
 constexpr uint32_t kGrpBlock = 256, kGrpHalo = 64;  // segments of <= kGrpHalo heads are ranked in LDS
+constexpr uint32_t kGrpEnds = 2048;  // run ends counted in LDS: [first position of the block, + kGrpEnds)
 __global__ void __launch_bounds__(256) k_grp_seg(const uint32_t* __restrict__ posS, const uint32_t* __restrict__ hb,
                                                  const HeadKV* __restrict__ kv, uint32_t H, int bN, int bL,
                                                  unsigned long long* __restrict__ key, uint32_t* __restrict__ perm,
                                                  uint32_t* __restrict__ tsOut, uint8_t* __restrict__ smOut,
-                                                 uint32_t* __restrict__ bigList, uint32_t maxSmall) {
+                                                 uint32_t* __restrict__ bigList, uint32_t maxSmall,
+                                                 int32_t* __restrict__ diffEnds, uint32_t n) {
   // one thread per sorted head: its rank inside its position's segment by
   // counting over the segment, staged in LDS with a halo either side
   __shared__ unsigned long long lk[kGrpBlock + 2 * kGrpHalo];
+  __shared__ int32_t endL[kGrpEnds];
   const uint32_t k0 = blockIdx.x * kGrpBlock;
   const int64_t base = (int64_t)k0 - kGrpHalo;
   for (uint32_t i = threadIdx.x; i < kGrpBlock + 2 * kGrpHalo; i += blockDim.x) {
@@ -76,8 +79,26 @@ __global__ void __launch_bounds__(256) k_grp_seg(const uint32_t* __restrict__ po
       lk[i] = ((unsigned long long)(w.len & 0x7fffffffu) << bN) | w.isa;
     }
   }
+  if (diffEnds)
+    for (uint32_t i = threadIdx.x; i < kGrpEnds; i += blockDim.x) endL[i] = 0;
   __syncthreads();
   const uint32_t k = k0 + threadIdx.x;
+  if (diffEnds) {
+    // run ends (FN:1162-1171, 1203): head i covers [pos_i, pos_i + start_{i+1}
+    // - start_i) = [pos, pos + toNext + 1) (an end phrase: [n-1, n)); ends
+    // near the block's first position are counted in LDS, the rest atomically
+    const uint32_t pmin = posS[k0];
+    if (k < H) {
+      const uint64_t e = (uint64_t)posS[k] + kv[k].tonext + 1;
+      if (e <= n) {
+        if (e - pmin < kGrpEnds) atomicAdd(&endL[e - pmin], 1);
+        else atomicAdd(&diffEnds[e], -1);
+      }
+    }
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < kGrpEnds; i += blockDim.x)
+      if (endL[i]) atomicAdd(&diffEnds[pmin + i], -endL[i]);
+  }
   if (k >= H) return;
   const uint32_t p = posS[k];
   const uint32_t b = hb[p], e = hb[p + 1];
@@ -1987,9 +2008,22 @@ void mk_el_wr_emit(const ElemIn& w, uint32_t V, const unsigned long long* runOff
 }
 void mk_grp_seg(const uint32_t* posS, const uint32_t* hb, const HeadKV* kv, uint32_t H, int bN, int bL,
                 unsigned long long* key, uint32_t* perm, uint32_t* tsOut, uint8_t* smOut, uint32_t* bigList,
-                uint32_t maxSmall, hipStream_t st) {
+                uint32_t maxSmall, int32_t* diffEnds, uint32_t n, hipStream_t st) {
   if (H) hipLaunchKernelGGL(k_grp_seg, dim3((H + kGrpBlock - 1) / kGrpBlock), dim3(kGrpBlock), 0, st, posS, hb, kv, H, bN,
-                            bL, key, perm, tsOut, smOut, bigList, maxSmall);
+                            bL, key, perm, tsOut, smOut, bigList, maxSmall, diffEnds, n);
+}
+// run starts per position from the sorted heads' position offsets:
+// diff[p] = #heads at p (ends are subtracted by k_grp_seg), hasHead[p]
+__global__ void k_run_starts(const uint32_t* __restrict__ hb, uint32_t n, int32_t* __restrict__ diff,
+                             uint8_t* __restrict__ hasHead) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p > n) return;
+  const uint32_t c = p < n ? hb[p + 1] - hb[p] : 0u;
+  diff[p] = (int32_t)c;
+  if (p < n) hasHead[p] = c != 0;
+}
+void mk_run_starts(const uint32_t* hb, uint32_t n, int32_t* diff, uint8_t* hasHead, hipStream_t st) {
+  hipLaunchKernelGGL(k_run_starts, g1((uint64_t)n + 1), dim3(256), 0, st, hb, n, diff, hasHead);
 }
 void mk_grp_big_fields(const uint32_t* idx, uint32_t B, const uint32_t* perm, const HeadsSoA& h, uint32_t* tsOut,
                        uint8_t* smOut, hipStream_t st) {

@@ -32,7 +32,8 @@ void mk_group_key(const HeadsSoA& h, uint64_t H, int bN, int bL, unsigned long l
 // grouping, position first (radix by pos, then per-position segments)
 void mk_grp_seg(const uint32_t* posS, const uint32_t* hb, const HeadKV* kv, uint32_t H, int bN, int bL,
                 unsigned long long* key, uint32_t* perm, uint32_t* tsOut, uint8_t* smOut, uint32_t* bigList,
-                uint32_t maxSmall, hipStream_t st);
+                uint32_t maxSmall, int32_t* diffEnds, uint32_t n, hipStream_t st);
+void mk_run_starts(const uint32_t* hb, uint32_t n, int32_t* diff, uint8_t* hasHead, hipStream_t st);
 void mk_grp_big_fields(const uint32_t* idx, uint32_t B, const uint32_t* perm, const HeadsSoA& h, uint32_t* tsOut,
                        uint8_t* smOut, hipStream_t st);
 void mk_grp_big_sizes(const uint32_t* pos, uint32_t nb, const uint32_t* hb, uint32_t* sz, hipStream_t st);
