@@ -63,6 +63,20 @@ struct MakeHeadKV {  // head idx -> its grouping fields
     return HeadKV{i, len[i] | (smaller[i] ? 0x80000000u : 0u), isa[i], tonext[i]};
   }
 };
+struct AdjustedRuns {  // k_wr_adjust's rule, as a scan input
+  const uint32_t* runs;
+  const uint32_t* hl;
+  const uint32_t* prev;
+  __host__ __device__ unsigned long long operator()(uint32_t u) const {
+    const uint32_t a = hl[u], pv = prev[u];
+    return (unsigned long long)runs[u] - (((a >> 16) && (pv >> 16) && (a & 0xff) == ((pv >> 8) & 0xff)) ? 1u : 0u);
+  }
+  template <class Eng>
+  unsigned long long host(uint32_t u, Eng* e) const {  // the last element's value, read back to the host
+    const uint32_t a = e->read1(hl + u), pv = e->read1(prev + u), r = e->read1(runs + u);
+    return (unsigned long long)r - (((a >> 16) && (pv >> 16) && (a & 0xff) == ((pv >> 8) & 0xff)) ? 1u : 0u);
+  }
+};
 struct PlusOneU64 {
   __host__ __device__ unsigned long long operator()(unsigned long long v) const { return v + 1; }
 };
@@ -1712,18 +1726,24 @@ struct Engine {
       DBuf<unsigned long long> cum;
       cum.alloc(H);
       inscan(rocprim::make_transform_iterator(counter.p, PlusOneU64()), cum.p, H, rocprim::plus<unsigned long long>());
+      DBuf<uint4> info1;
+      DBuf<unsigned long long> info2;
+      info1.alloc(n); info2.alloc(n);
       ElemIn ei{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, itemOfSlot.p, headBase.p, eBase.p, rOf.p, bwtHeads.p,
-                counter.p, cum.p, n, E, H, rle};
+                counter.p, cum.p, info1.p, info2.p, n, E, H, rle};
+      mk_el_info(ei, st);
       DBuf<uint32_t> wruns, whl, wprev;
       DBuf<unsigned long long> wsym, wrunOff, wsymOff;
       wruns.alloc(V); whl.alloc(V); wprev.alloc(V); wsym.alloc(V); wrunOff.alloc(V); wsymOff.alloc(V);
       mk_el_wr_count(ei, V, wruns.p, wsym.p, whl.p, st);
       exscan(whl.p, wprev.p, 0u, V, LastNonEmpty());
-      mk_wr_adjust(whl.p, wprev.p, V, wruns.p, st);
-      auto runs64 = rocprim::make_transform_iterator(wruns.p, WidenU64());
+      // runs of each element, less one when its first segment continues the
+      // previous non-empty element's run (k_wr_adjust, fused into the scan)
+      auto runs64 = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint32_t>(0u),
+                                                     AdjustedRuns{wruns.p, whl.p, wprev.p});
       exscan(runs64, wrunOff.p, 0ull, V);
       exscan(wsym.p, wsymOff.p, 0ull, V);
-      Rn = read1(wrunOff.p + (V - 1)) + read1(wruns.p + (V - 1));
+      Rn = read1(wrunOff.p + (V - 1)) + AdjustedRuns{wruns.p, whl.p, wprev.p}.host(V - 1, this);
       symbols = read1(wsymOff.p + (V - 1)) + read1(wsym.p + (V - 1));
       runStart.alloc(std::max<uint64_t>(Rn, 1)); runChar.alloc(std::max<uint64_t>(Rn, 1));
       mk_el_wr_emit(ei, V, wrunOff.p, wsymOff.p, wprev.p, runStart.p, runChar.p, st);

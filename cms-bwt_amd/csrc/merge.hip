@@ -1609,6 +1609,8 @@ struct ElemArgs {
   const uint8_t* bwtHeads;
   const unsigned long long* counter;   // by slot
   const unsigned long long* cum;       // by slot: inclusive sum of counter + 1
+  const uint4* info1;                  // per SA rank: element base, heads, slot base, head base
+  const unsigned long long* info2;     // per SA rank: bucket (56-bit two's complement) | BWT char << 56
   uint32_t n, E, H;
   int rle;
 };
@@ -1616,28 +1618,51 @@ struct ElemArgs {
 template <class F>
 __device__ __forceinline__ void d_elem_segments(const ElemArgs& A, uint32_t e, F&& f) {
   const uint32_t r = A.rOf[e];
-  const uint32_t k = e - A.elemBase[r];
+  const uint4 I = A.info1[r];  // the rank's fields, read once per element (k_el_info)
+  const uint32_t k = e - I.x;
   if (r == 0) { f(A.bwtHeads[k], 1ull); return; }  // end phrases (units u < E)
-  const uint32_t p = (uint32_t)A.sa[r];
-  const uint8_t c = A.bwt[r];
-  const int64_t b = A.bucket[p];
+  const unsigned long long J = A.info2[r];
+  const uint8_t c = (uint8_t)(J >> 56);
+  const int64_t b = ((int64_t)(J << 8)) >> 8;
   if (b > 0) { if (k == 0) f(c, (unsigned long long)b); return; }
   if (b == 0) return;
-  const uint32_t hb = A.headBase[r];
-  const uint32_t nh = (r + 1 < A.n ? A.headBase[r + 1] : A.H) - hb;
+  const uint32_t nh = I.y;
   if (nh == 0) {  // no items: the item loop is empty (FN:1761-1770 / 1678-1686)
     if (!A.rle) f(c, (unsigned long long)(-b));
     return;
   }
-  const uint32_t s0 = A.slot[A.posBegin[p]], s = s0 + k;
+  const uint32_t s0 = I.z, s = s0 + k;
   const unsigned long long cs = A.counter[s];
   if (cs) f(c, cs);
-  f(A.bwtHeads[hb + k], 1ull);
+  f(A.bwtHeads[I.w + k], 1ull);
   const bool last = A.rle ? (s + 1 >= A.H || A.itemOfSlot[s + 1] != A.itemOfSlot[s]) : k + 1 == nh;
   if (last) {
     const int64_t acc = b + (int64_t)(A.cum[s] - (s0 ? A.cum[s0 - 1] : 0ull));
     if (A.rle ? acc != 0 : acc < 0) f(c, (unsigned long long)(-acc));
   }
+}
+
+// per-rank fields of the element writer: element base, head count, slot
+// base of the rank's position, head base; bucket and BWT character
+__global__ void k_el_info(const int32_t* __restrict__ sa, const uint8_t* __restrict__ bwt,
+                          const int64_t* __restrict__ bucket, const uint32_t* __restrict__ posBegin,
+                          const uint32_t* __restrict__ slot, const uint32_t* __restrict__ headBase,
+                          const uint32_t* __restrict__ elemBase, uint32_t n, uint32_t E, uint32_t H,
+                          uint4* __restrict__ info1, unsigned long long* __restrict__ info2) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  const uint32_t hb = headBase[r];
+  const uint32_t nh = (r + 1 < n ? headBase[r + 1] : H) - hb;
+  uint32_t s0 = 0;
+  unsigned long long j = 0;
+  if (r > 0) {
+    const uint32_t p = (uint32_t)sa[r];
+    const int64_t b = bucket[p];
+    if (b < 0 && nh) s0 = slot[posBegin[p]];
+    j = ((unsigned long long)b & 0x00ffffffffffffffull) | ((unsigned long long)bwt[r] << 56);
+  }
+  info1[r] = make_uint4(elemBase[r], r == 0 ? E : nh, s0, hb);
+  info2[r] = j;
 }
 
 // elements per SA rank: E at rank 0, otherwise max(heads, 1)
@@ -1989,7 +2014,11 @@ void mk_wr_emit(const WriterIn& w, uint32_t U, const unsigned long long* runOff,
 }
 static ElemArgs elem_args(const ElemIn& w) {
   return ElemArgs{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.itemOfSlot, w.headBase, w.elemBase, w.rOf,
-                  w.bwtHeads, w.counter, w.cum, w.n, w.E, w.H, w.rle};
+                  w.bwtHeads, w.counter, w.cum, w.info1, w.info2, w.n, w.E, w.H, w.rle};
+}
+void mk_el_info(const ElemIn& w, hipStream_t st) {
+  if (w.n) hipLaunchKernelGGL(k_el_info, g1(w.n), dim3(256), 0, st, w.sa, w.bwt, w.bucket, w.posBegin, w.slot,
+                              w.headBase, w.elemBase, w.n, w.E, w.H, w.info1, w.info2);
 }
 void mk_el_count(const uint32_t* headBase, uint32_t n, uint32_t E, uint32_t H, uint32_t* m, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_el_count, g1(n), dim3(256), 0, st, headBase, n, E, H, m);

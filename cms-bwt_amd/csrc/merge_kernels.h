@@ -155,9 +155,12 @@ struct ElemIn {
   const uint8_t* bwtHeads;
   const unsigned long long* counter;
   const unsigned long long* cum;  // inclusive scan of counter + 1 over slots
+  uint4* info1;                   // per SA rank (filled by mk_el_info)
+  unsigned long long* info2;
   uint32_t n, E, H;
   int rle;
 };
+void mk_el_info(const ElemIn& w, hipStream_t st);
 void mk_el_count(const uint32_t* headBase, uint32_t n, uint32_t E, uint32_t H, uint32_t* m, hipStream_t st);
 void mk_el_rof(const uint32_t* elemBase, const uint32_t* m, uint32_t n, uint32_t* rOf, hipStream_t st);
 void mk_el_wr_count(const ElemIn& w, uint32_t V, uint32_t* runs, unsigned long long* sym, uint32_t* hl,
