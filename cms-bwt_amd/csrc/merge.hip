@@ -1112,9 +1112,12 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
 // appended to the wave's LDS list and searched 64 at a time when it fills
 // (items from global memory / L2, adds by global atomics); at the end each
 // accumulator is added to its slot.
-constexpr uint32_t kTgtRec = 256;   // item records staged per chunk (= threads per block)
+#ifndef TGT_REC
+#define TGT_REC 128
+#endif
+constexpr uint32_t kTgtRec = TGT_REC;   // item records staged per chunk
 constexpr uint32_t kTgtQ = 256;     // undecided queries listed per wave before a search pass
-constexpr uint32_t kTgtS = 320;     // queries listed per wave for binary searches
+constexpr uint32_t kTgtS = 256;     // queries listed per wave for binary searches
 constexpr uint32_t kNoSlot = 0xffffffffu;
 
 // v (wave-uniform) in the lanes of mask m, 0 elsewhere: one v_cndmask on the
@@ -1131,12 +1134,13 @@ __device__ __forceinline__ uint64_t ucmp(uint32_t a, uint32_t b) {
   return __builtin_amdgcn_uicmp(a, b, P);
 }
 
-__global__ void __launch_bounds__(256) k_counter_tgt(CounterArgs A) {
-  __shared__ uint4 recG[4][kTgtRec];  // 16 KB: per wave, the records reaching its targets
+// 7 waves per SIMD: <= 72 VGPRs, 22 KB of LDS per block (chunks of 128 records)
+__global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
+  __shared__ uint4 recG[4][kTgtRec];  // 8 KB: per wave, the records reaching its targets
   __shared__ uint32_t qL[4][kTgtQ];   // 8 KB
   __shared__ uint32_t nG[8];  // per wave: smaller=true records (front), smaller=false (back)
-  __shared__ uint32_t accL[6][kTgtRec];  // 6 KB: adds settled in the search passes, per target
-  __shared__ uint32_t qS[4][kTgtS];       // 5 KB: queries left for binary searches
+  __shared__ uint32_t accL[6][256];      // 6 KB: adds settled in the search passes, per target
+  __shared__ uint32_t qS[4][kTgtS];       // 4 KB: queries left for binary searches
   const ItemsSoA& it = A.it;
   const uint32_t w = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1303,11 +1307,11 @@ __global__ void __launch_bounds__(256) k_counter_tgt(CounterArgs A) {
     const uint32_t nr = min(kTgtRec, nList - ch);
     if (tid < 8) nG[tid] = 0;
     __syncthreads();  // the previous chunk's lists are no longer read
-    if (tid < nr) {
+    for (uint32_t ti = tid; ti < nr; ti += blockDim.x) {
       // every chunk mixes crossing items (they reach the first waves'
       // targets) and starting items taken from all four quarters of the
       // window, so the four waves get similar lists between two barriers
-      const uint32_t j = ch + tid;
+      const uint32_t j = ch + ti;
       const uint32_t nSt = nList - nCross;
       const uint32_t cj = (uint32_t)((uint64_t)j * nCross / nList);
       const bool isCross = (uint32_t)((uint64_t)(j + 1) * nCross / nList) > cj;
