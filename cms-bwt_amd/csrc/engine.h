@@ -1400,13 +1400,15 @@ struct Engine {
 
   // FN:1480-1494 sort of each item's next-head ranks (slot order): small
   // items by an in-place insertion sort, large ones by one global (item, nhr) sort
-  void sort_nhr_items(const ItemsSoA& S, uint32_t K, const uint32_t* itemOfSlotP, uint32_t* nhrP, uint32_t H) {
+  void sort_nhr_items(const ItemsSoA& S, uint32_t K, const uint32_t* itemOfSlotP, uint32_t* nhrP, uint32_t H,
+                      bool smallDone = false) {
     (void)itemOfSlotP;
     (void)H;
     DBuf<uint32_t> bigList;
     bigList.alloc((uint64_t)K + 1);
     HIPCHK(hipMemsetAsync(bigList.p, 0, 4, st));
-    mk_nhr_sort_small(S, K, nhrP, bigList.p, st);
+    if (smallDone) mk_nhr_big_list(S, K, bigList.p, st);  // items <= kSmallSeg ranked by k_nhr_rank
+    else mk_nhr_sort_small(S, K, nhrP, bigList.p, st);
     const uint32_t nb = K ? read1(bigList.p) : 0;
     if (!nb) return;
     // the large items in item order, their members at exclusive offsets
@@ -1649,12 +1651,18 @@ struct Engine {
     DBuf<uint32_t> nhr;
     nhr.alloc(H);
     {
+      const bool fused = !env_u32("CMSBWT_NHR_SORT", 0);  // 1: gather, then per-item insertion sorts
       {
         DBuf<uint32_t> nbi;
         nbi.alloc(H);
-        mk_nhr_slot(Pm.p, grp.p, 1u, hNext.p, H, nbi.p, nhr.p, st);
+        if (fused) {  // gather + rank inside the item in one pass
+          mk_nhr_idx(grp.p, 1u, hNext.p, H, nbi.p, st);
+          mk_nhr_rank(Pm.p, nbi.p, itemOfSlot.p, H, nhr.p, st);
+        } else {
+          mk_nhr_slot(Pm.p, grp.p, 1u, hNext.p, H, nbi.p, nhr.p, st);
+        }
       }
-      sort_nhr_items(S, K, itemOfSlot.p, nhr.p, H);
+      sort_nhr_items(S, K, itemOfSlot.p, nhr.p, H, fused);
     }
     grp.release();
     Pm.release();

@@ -711,6 +711,37 @@ __global__ void k_nhr_slot(const uint32_t* __restrict__ Pm, const uint32_t* __re
 // members; larger items are appended to a list (bigList[0] = their number)
 // for one global sort of their members.
 constexpr uint32_t kSmallSeg = 32;
+// FN:1480-1494 fused: one thread per slot gathers its member's next-head
+// rank (nbi, in document order) and ranks it inside its item by counting
+// over an LDS copy of the block's slots with a halo (items of <= kSmallSeg
+// members, the rest keep their order here and are sorted by the big path).
+// Writes the item's members' ranks sorted (std::sort of idxs, FN:1492).
+constexpr uint32_t kNhrBlock = 256, kNhrHalo = kSmallSeg + 1;  // the scans go kSmallSeg + 1 slots either way
+__global__ void __launch_bounds__(256) k_nhr_rank(const uint32_t* __restrict__ Pm, const uint32_t* __restrict__ nbi,
+                                                  const uint32_t* __restrict__ itemOfSlot, uint32_t H,
+                                                  uint32_t* __restrict__ nhr) {
+  __shared__ uint32_t vL[kNhrBlock + 2 * kNhrHalo], qL2[kNhrBlock + 2 * kNhrHalo];
+  const uint32_t s0 = blockIdx.x * kNhrBlock;
+  const int64_t base = (int64_t)s0 - kNhrHalo;
+  for (uint32_t i = threadIdx.x; i < kNhrBlock + 2 * kNhrHalo; i += blockDim.x) {
+    const int64_t j = base + i;
+    if (j >= 0 && j < (int64_t)H) { vL[i] = nbi[Pm[j]]; qL2[i] = itemOfSlot[j]; }
+  }
+  __syncthreads();
+  const uint32_t s = s0 + threadIdx.x;
+  if (s >= H) return;
+  const uint32_t me = threadIdx.x + kNhrHalo, q = qL2[me], v = vL[me];
+  uint32_t lo = me, hi = me + 1;
+  while (lo > 0 && base + lo > 0 && qL2[lo - 1] == q && me - lo <= kSmallSeg) lo--;
+  while (hi < kNhrBlock + 2 * kNhrHalo && base + hi < (int64_t)H && qL2[hi] == q && hi - me <= kSmallSeg) hi++;
+  if (hi - lo > kSmallSeg) { nhr[s] = v; return; }  // a long item: the big path sorts it
+  uint32_t r = 0;
+  for (uint32_t j = lo; j < hi; j++) {
+    const uint32_t w = vL[j];
+    r += (w < v || (w == v && j < me)) ? 1u : 0u;
+  }
+  nhr[(uint32_t)(base + lo + r)] = v;
+}
 __global__ void k_nhr_sort_small(const ItemsSoA it, uint32_t K, uint32_t* __restrict__ nhr,
                                  uint32_t* __restrict__ bigList) {
   uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1834,11 +1865,28 @@ void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_
 void mk_head_chars(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint8_t* bwtHeads, hipStream_t st) {
   if (H) hipLaunchKernelGGL(k_head_chars, g1(H), dim3(256), 0, st, sa, lchar, H, bwtHeads);
 }
+void mk_nhr_idx(const uint32_t* headRank, uint32_t sub, const uint16_t* nexthead, uint32_t H, uint32_t* nbi,
+                hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_nhr_idx, g1(H), dim3(256), 0, st, headRank, sub, nexthead, H, nbi);
+}
 void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, uint32_t sub, const uint16_t* nexthead, uint32_t H,
                  uint32_t* nbi, uint32_t* nhr, hipStream_t st) {
   if (!H) return;
   hipLaunchKernelGGL(k_nhr_idx, g1(H), dim3(256), 0, st, headRank, sub, nexthead, H, nbi);
   hipLaunchKernelGGL(k_nhr_slot, g1(H), dim3(256), 0, st, Pm, nbi, H, nhr);
+}
+void mk_nhr_rank(const uint32_t* Pm, const uint32_t* nbi, const uint32_t* itemOfSlot, uint32_t H, uint32_t* nhr,
+                 hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_nhr_rank, dim3((H + kNhrBlock - 1) / kNhrBlock), dim3(kNhrBlock), 0, st, Pm, nbi,
+                            itemOfSlot, H, nhr);
+}
+// items of more than kSmallSeg members, for the big path
+__global__ void k_nhr_big_list(const ItemsSoA it, uint32_t K, uint32_t* __restrict__ bigList) {
+  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < K && it.count[q] > kSmallSeg) bigList[1 + atomicAdd(bigList, 1u)] = q;
+}
+void mk_nhr_big_list(const ItemsSoA& it, uint32_t K, uint32_t* bigList, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_nhr_big_list, g1(K), dim3(256), 0, st, it, K, bigList);
 }
 void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigList, hipStream_t st) {
   if (K) hipLaunchKernelGGL(k_nhr_sort_small, g1(K), dim3(256), 0, st, it, K, nhr, bigList);

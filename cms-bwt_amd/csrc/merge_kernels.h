@@ -66,7 +66,13 @@ void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_
 void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, uint32_t sub, const uint16_t* nexthead, uint32_t H,
                  uint32_t* nbi, uint32_t* nhr, hipStream_t st);
 void mk_head_chars(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint8_t* bwtHeads, hipStream_t st);
+void mk_nhr_idx(const uint32_t* headRank, uint32_t sub, const uint16_t* nexthead, uint32_t H, uint32_t* nbi,
+                hipStream_t st);
 void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigList, hipStream_t st);
+// next-head rank of each slot's member ranked inside its item (items <= kSmallSeg)
+void mk_nhr_rank(const uint32_t* Pm, const uint32_t* nbi, const uint32_t* itemOfSlot, uint32_t H, uint32_t* nhr,
+                 hipStream_t st);
+void mk_nhr_big_list(const ItemsSoA& it, uint32_t K, uint32_t* bigList, hipStream_t st);
 void mk_nhr_big_fill(const uint32_t* items, const uint32_t* off, uint32_t nb, const ItemsSoA& it, const uint32_t* nhr,
                      unsigned long long* key, uint32_t* slots, hipStream_t st);
 void mk_item_counts_of(const uint32_t* items, uint32_t nb, const uint32_t* count, uint32_t* out, hipStream_t st);
