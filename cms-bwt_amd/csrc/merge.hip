@@ -1158,6 +1158,13 @@ __device__ __forceinline__ uint32_t sel_u32(uint32_t v, uint64_t m) {
   asm volatile("v_cndmask_b32_e64 %0, 0, %1, %2" : "=v"(r) : "v"(v), "s"(m));
   return r;
 }
+// acc + (lane's bit of m): one v_addc on the VALU (per-lane statistics without
+// scalar popcounts: the scalar unit, one per CU, bounds this kernel)
+__device__ __forceinline__ uint32_t addc_mask(uint32_t acc, uint64_t m) {
+  uint32_t r;
+  asm volatile("v_addc_co_u32_e64 %0, vcc, 0, %1, %2" : "=v"(r) : "v"(acc), "s"(m) : "vcc");
+  return r;
+}
 // unsigned compare of each lane, as a wave mask (llvm.amdgcn.icmp predicates)
 constexpr int kNE = 33, kUGT = 34, kUGE = 35, kULT = 36, kULE = 37;
 template <int P>
@@ -1172,6 +1179,7 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
   __shared__ uint32_t nG[8];  // per wave: smaller=true records (front), smaller=false (back)
   __shared__ uint32_t accL[6][256];      // 6 KB: adds settled in the search passes, per target
   __shared__ uint32_t qS[4][kTgtS];       // 4 KB: queries left for binary searches
+  __shared__ uint64_t noItL[4];           // per wave: targets without items
   const ItemsSoA& it = A.it;
   const uint32_t w = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1200,9 +1208,16 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
     nF3 = nF == 3;
   }
   const bool hasF0 = fs0 != kNoSlot, hasF1 = fs1 != kNoSlot, hasF2 = fs2 != kNoSlot;
-  const uint64_t hasM = __ballot(has), hasF0M = __ballot(hasF0), hasF1M = __ballot(hasF1);  // per wave
+  const uint64_t hasF0M = __ballot(hasF0), hasF1M = __ballot(hasF1);  // per wave
   const uint32_t flags = (hasF0 ? 1u : 0u) | (hasF1 ? 2u : 0u) | (hasF2 ? 4u : 0u) | (nS3 ? 8u : 0u) | (nF3 ? 16u : 0u);
   for (uint32_t k = 0; k < 6; k++) accL[k][tid] = 0;
+  // lanes without items never fall in a record's range (their pairs are
+  // counted once per staged record: counterDoNothing, FN:1530)
+  const uint32_t tofH = has ? toff : 0x40000000u;
+  {
+    const uint64_t hm = __ballot(has);
+    if (lane == 0) noItL[wv] = ~hm;
+  }
   // accumulators: first F item (f), S items top 0..2, F items 1..2
   uint32_t aF0 = 0, aS0 = 0, aS1 = 0, aS2 = 0, aF1 = 0, aF2 = 0, nGood = 0, nNothing = 0;
   QueryStats qs;
@@ -1242,18 +1257,21 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
         const uint32_t nb = min(64u, re - r);
         const uint4 my = lane < nb ? myR[r + lane] : make_uint4(0u, 0u, 0u, 0u);
         uint32_t e = 0;
-        for (; e < nb && qn <= kTgtQ - 64; e++) {
+        while (e < nb && qn <= kTgtQ - 64) {
+          // records that cannot overflow the query list (<= 64 queries each)
+          const uint32_t lim = min(nb, e + ((kTgtQ - qn) >> 6));
+          for (; e < lim; e++) {
+          // record: x = match end E, y = aO | span << 16 (targets T0 + aO ..
+          // T0 + aO + span), z = count
           const uint32_t ab = __builtin_amdgcn_readlane(my.y, e);
-          const uint32_t cq = __builtin_amdgcn_readlane(my.z, e) & 0x7fffffffu;
+          const uint32_t cqv = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(my.z, e));
           const uint32_t L = __builtin_amdgcn_readlane(my.x, e) - t;
-          const uint32_t aO = ab & 0xffffu, bO = ab >> 16;
           // lower_bound (FN:1534) settled by the two longest items of the
           // query's class (k_counter_win's fast tests, exact lens).  The
           // decisions are wave masks (SGPR pairs; the per-target flags are
-          // loop-invariant masks) and an add is one v_cndmask on its mask.
-          const uint64_t mR = ucmp<kUGE>(toff, aO) & ucmp<kULE>(toff, bO);
-          const uint64_t mIn = mR & hasM;
-          const uint32_t cqv = __builtin_amdgcn_readfirstlane(cq);
+          // loop-invariant masks) and an add is one v_cndmask on its mask;
+          // range test and statistics stay on the VALU.
+          const uint64_t mIn = ucmp<kULE>(tofH - (ab & 0xffffu), ab >> 16);
           uint64_t mF0, mX, msl;
           if (S) {  // smaller=true: S items ascending, then F items
             const uint64_t m1 = ucmp<kUGT>(L, sl0) & ucmp<kNE>(L, fl0);  // past every S item: f (or end)
@@ -1271,15 +1289,16 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
             msl = mIn & ~(m1 | m2);
           }
           aF0 += sel_u32(cqv, mF0);
-          nGood += (uint32_t)__popcll(mF0 | mX);
-          nNothing += (uint32_t)__popcll(mR & ~hasM);
-          const uint64_t sm = msl;
-          if ((sm >> lane) & 1) {
-            const uint32_t rk =
-                __builtin_amdgcn_mbcnt_hi((uint32_t)(sm >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)sm, 0u));
-            myQ[qn + rk] = (r + e) | (toff << 16);
+          nGood = addc_mask(addc_mask(nGood, mF0), mX);
+          if (msl) {
+            if ((msl >> lane) & 1) {
+              const uint32_t rk =
+                  __builtin_amdgcn_mbcnt_hi((uint32_t)(msl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msl, 0u));
+              myQ[qn + rk] = (r + e) | (toff << 16);
+            }
+            qn += (uint32_t)__popcll(msl);
           }
-          qn += (uint32_t)__popcll(sm);
+          }
         }
         r += e;
       }
@@ -1363,8 +1382,11 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
         if (lo <= hi) {
           const uint32_t aO = lo - T0, bO = hi - T0;
           const bool sm = it.smaller[q] != 0;
-          const uint4 rec = make_uint4(it.len[q] + p, aO | (bO << 16), it.count[q] | (sm ? 0x80000000u : 0u), q);
+          const uint4 rec = make_uint4(it.len[q] + p, aO | ((bO - aO) << 16), it.count[q], q);
           for (uint32_t k = aO >> 6; k <= (bO >> 6); k++) {
+            // pairs of this record whose target has no heads (FN:1530)
+            const uint32_t a = k == (aO >> 6) ? (aO & 63u) : 0u, b = k == (bO >> 6) ? (bO & 63u) : 63u;
+            nNothing += (uint32_t)__popcll(noItL[k] & (~0ull >> (63u - b)) & (~0ull << a));
             const uint32_t o = atomicAdd(&nG[2 * k + (sm ? 0 : 1)], 1u);
             recG[k][sm ? o : kTgtRec - 1 - o] = rec;
           }
@@ -1387,10 +1409,8 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
   if (aS0) atomicAdd(&A.counter[ss0], (unsigned long long)aS0);
   if (aS1) atomicAdd(&A.counter[ss1], (unsigned long long)aS1);
   if (aS2) atomicAdd(&A.counter[ss2], (unsigned long long)aS2);
-  if (lane == 0) {  // wave-uniform counts
-    qs.good += nGood;
-    qs.nothing += nNothing;
-  }
+  qs.good += nGood;
+  qs.nothing += nNothing;
   if (qs.bad) atomicAdd(&A.stats[0], (unsigned long long)qs.bad);
   if (qs.good) atomicAdd(&A.stats[1], (unsigned long long)qs.good);
   if (qs.nothing) atomicAdd(&A.stats[2], (unsigned long long)qs.nothing);
