@@ -1208,12 +1208,13 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
     nF3 = nF == 3;
   }
   const bool hasF0 = fs0 != kNoSlot, hasF1 = fs1 != kNoSlot, hasF2 = fs2 != kNoSlot;
-  const uint64_t hasF0M = __ballot(hasF0), hasF1M = __ballot(hasF1);  // per wave
+  const uint64_t hasF1M = __ballot(hasF1);  // per wave
   const uint32_t flags = (hasF0 ? 1u : 0u) | (hasF1 ? 2u : 0u) | (hasF2 ? 4u : 0u) | (nS3 ? 8u : 0u) | (nF3 ? 16u : 0u);
   for (uint32_t k = 0; k < 6; k++) accL[k][tid] = 0;
   // lanes without items never fall in a record's range (their pairs are
   // counted once per staged record: counterDoNothing, FN:1530)
   const uint32_t tofH = has ? toff : 0x40000000u;
+  const uint32_t tofF = hasF0 ? toff : 0x40000000u;  // (an F item implies items)
   {
     const uint64_t hm = __ballot(has);
     if (lane == 0) noItL[wv] = ~hm;
@@ -1246,6 +1247,48 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
     __builtin_amdgcn_wave_barrier();
     nSearch = 0;
   };
+  // one staged record against the wave's 64 targets.  Record: x = match end
+  // E, y = aO | span << 16 (targets T0 + aO .. T0 + aO + span), z = count.
+  // lower_bound (FN:1534) is settled by the two longest items of the query's
+  // class (k_counter_win's fast tests, exact lens).  The decisions are wave
+  // masks (SGPR pairs; the per-target flags are loop-invariant masks) and an
+  // add is one v_cndmask on its mask; range tests and statistics stay on the
+  // VALU (the scalar unit, one per CU, bounds this loop).
+  auto rec = [&](auto cls, const uint4& my, uint32_t r, uint32_t e, uint32_t& qn) {
+    constexpr bool S = decltype(cls)::value;
+    const uint32_t ab = __builtin_amdgcn_readlane(my.y, e);
+    const uint32_t cqv = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(my.z, e));
+    const uint32_t L = __builtin_amdgcn_readlane(my.x, e) - t;
+    const uint32_t aO = ab & 0xffffu, span = ab >> 16;
+    const uint64_t mIn = ucmp<kULE>(tofH - aO, span);    // targets with items
+    const uint64_t mInF = ucmp<kULE>(tofF - aO, span);   // ... and a smaller=false item
+    uint64_t mF0, mX, msl;
+    if (S) {  // smaller=true: S items ascending, then F items
+      const uint64_t m1 = ucmp<kUGT>(L, sl0) & ucmp<kNE>(L, fl0);  // past every S item: f (or end)
+      const uint64_t m2 = ucmp<kULT>(L, sl0) & ucmp<kUGT>(L, sl1);   // the longest S item
+      mF0 = mInF & m1;
+      mX = mIn & m2;
+      aS0 += sel_u32(cqv, mX);
+      msl = mIn & ~(m1 | m2);
+    } else {  // smaller=false: F items descending
+      const uint64_t m1 = ucmp<kUGT>(L, fl0);                       // f
+      const uint64_t m2 = ucmp<kULT>(L, fl0) & ucmp<kUGT>(L, fl1);   // the second F item (or end)
+      mF0 = mInF & m1;
+      mX = mIn & m2 & hasF1M;
+      aF1 += sel_u32(cqv, mX);
+      msl = mIn & ~(m1 | m2);
+    }
+    aF0 += sel_u32(cqv, mF0);
+    nGood = addc_mask(addc_mask(nGood, mF0), mX);
+    if (msl) {
+      if ((msl >> lane) & 1) {
+        const uint32_t rk =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(msl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msl, 0u));
+        myQ[qn + rk] = (r + e) | (toff << 16);
+      }
+      qn += (uint32_t)__popcll(msl);
+    }
+  };
   // one walk over a wave's records of one class (smaller=true records from
   // the front of its list, smaller=false ones from the back)
   auto walk = [&](auto cls, uint32_t rb, uint32_t re) {
@@ -1260,45 +1303,12 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
         while (e < nb && qn <= kTgtQ - 64) {
           // records that cannot overflow the query list (<= 64 queries each)
           const uint32_t lim = min(nb, e + ((kTgtQ - qn) >> 6));
-          for (; e < lim; e++) {
-          // record: x = match end E, y = aO | span << 16 (targets T0 + aO ..
-          // T0 + aO + span), z = count
-          const uint32_t ab = __builtin_amdgcn_readlane(my.y, e);
-          const uint32_t cqv = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(my.z, e));
-          const uint32_t L = __builtin_amdgcn_readlane(my.x, e) - t;
-          // lower_bound (FN:1534) settled by the two longest items of the
-          // query's class (k_counter_win's fast tests, exact lens).  The
-          // decisions are wave masks (SGPR pairs; the per-target flags are
-          // loop-invariant masks) and an add is one v_cndmask on its mask;
-          // range test and statistics stay on the VALU.
-          const uint64_t mIn = ucmp<kULE>(tofH - (ab & 0xffffu), ab >> 16);
-          uint64_t mF0, mX, msl;
-          if (S) {  // smaller=true: S items ascending, then F items
-            const uint64_t m1 = ucmp<kUGT>(L, sl0) & ucmp<kNE>(L, fl0);  // past every S item: f (or end)
-            const uint64_t m2 = ucmp<kULT>(L, sl0) & ucmp<kUGT>(L, sl1);   // the longest S item
-            mF0 = mIn & m1 & hasF0M;
-            mX = mIn & m2;
-            aS0 += sel_u32(cqv, mX);
-            msl = mIn & ~(m1 | m2);
-          } else {  // smaller=false: F items descending
-            const uint64_t m1 = ucmp<kUGT>(L, fl0);                       // f
-            const uint64_t m2 = ucmp<kULT>(L, fl0) & ucmp<kUGT>(L, fl1);   // the second F item (or end)
-            mF0 = mIn & m1 & hasF0M;
-            mX = mIn & m2 & hasF1M;
-            aF1 += sel_u32(cqv, mX);
-            msl = mIn & ~(m1 | m2);
+          // (unrolled by two: the loop control is scalar work too)
+          for (; e + 1 < lim; e += 2) {
+            rec(cls, my, r, e, qn);
+            rec(cls, my, r, e + 1, qn);
           }
-          aF0 += sel_u32(cqv, mF0);
-          nGood = addc_mask(addc_mask(nGood, mF0), mX);
-          if (msl) {
-            if ((msl >> lane) & 1) {
-              const uint32_t rk =
-                  __builtin_amdgcn_mbcnt_hi((uint32_t)(msl >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)msl, 0u));
-              myQ[qn + rk] = (r + e) | (toff << 16);
-            }
-            qn += (uint32_t)__popcll(msl);
-          }
-          }
+          if (e < lim) rec(cls, my, r, e++, qn);
         }
         r += e;
       }

@@ -299,10 +299,9 @@ __global__ void k_scatter_heads(Pool pool, uint32_t blocksUsed, const uint32_t* 
   h.pos[idx] = r.pos;
   h.len[idx] = r.len;
   h.smaller[idx] = (uint8_t)(r.flags & 1u);
-  // BWT character of the phrase: the text byte before it, 0x02 at a document start
-  const uint32_t d = chunks[cid].doc;
-  h.lchar[idx] = r.start == 0 ? (uint8_t)kSep : text[docOff[d] + r.start - 1];
-  hdoc[idx] = d;
+  // (the BWT character before the phrase is read by k_finalize, whose
+  // document-ordered threads read the text lines coalesced)
+  hdoc[idx] = chunks[cid].doc;
 }
 
 // End-of-document phrase (FN:1198-1212): (docLen, n-1, 0, false), char =
@@ -365,17 +364,23 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
   const uint32_t j = k;
   const uint32_t s1 = h.start[i + 1];
   h.tonext[i] = s1 - si - 1;
-  uint32_t q = h.pos[j] + (ei - h.start[j]);
+  const uint32_t sj = h.start[j];
+  uint32_t q = h.pos[j] + (ei - sj);
   if (q >= R.n) { atomicOr(errFlags, 2u); q = R.n - 1; }
   h.isa[i] = R.isa[q];
   // Order invariant: the isaNext suffix starts with the mismatching text byte
   // (or the head ends at the document separator and isaNext is the smallest
   // suffix).  When it holds for every head, MatchInSet::operator< is a strict
   // weak order on every position's keys and queries.
+  const uint8_t* dt = text + docOff[lo];
   {
-    const uint8_t c = text[docOff[lo] + ei];
+    const uint8_t c = dt[ei];
     if (!(c == R.x[q] || (c == kSep && q == R.n - 1))) atomicOr(errFlags, 8u);
   }
+  // BWT character of the phrase (FN:1158-1161): the text byte before it, 0x02
+  // at a document start.  Read here rather than in k_scatter_heads: heads are
+  // in document order, so a wave reads the same text lines as for the check.
+  h.lchar[i] = si == 0 ? (uint8_t)kSep : dt[si - 1];
   h.nexthead[i] = (uint16_t)(j - i);
   if ((uint64_t)h.pos[i] + (s1 - si) > R.n) atomicOr(errFlags, 4u);
 }
