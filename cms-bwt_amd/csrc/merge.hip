@@ -919,6 +919,17 @@ struct GlobalView {
   __device__ unsigned long long sk(uint32_t q) const { return it->sk[q]; }
   __device__ uint32_t slot(uint32_t q) const { return it->slot[q]; }
 };
+// GlobalView with the query target's item range already known (passed from
+// the lane that owns the target): no posBegin / posF loads in the search
+struct KnownView {
+  const ItemsSoA* it;
+  const uint32_t* nhr;
+  uint32_t t0, b0, b1, f;
+  __device__ uint32_t begin(uint32_t t) const { return t == t0 ? b0 : b1; }
+  __device__ uint32_t fbeg(uint32_t) const { return f; }
+  __device__ unsigned long long sk(uint32_t q) const { return it->sk[q]; }
+  __device__ uint32_t slot(uint32_t q) const { return it->slot[q]; }
+};
 struct LdsView {  // items and positions rebased to the window
   const unsigned long long* skL;
   const uint32_t* slotL;
@@ -1194,6 +1205,7 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
   uint32_t sl0 = 0, sl1 = 0, sl2 = 0, fl0 = 0, fl1 = 0, fl2 = 0;
   uint32_t ss0 = kNoSlot, ss1 = kNoSlot, ss2 = kNoSlot, fs0 = kNoSlot, fs1 = kNoSlot, fs2 = kNoSlot;
   bool has = false, nS3 = false, nF3 = false;
+  uint32_t fidx = 0, nS8 = 255, nF8 = 255;  // first F item; class sizes (255: 255 or more)
   if (t < T1) {
     const uint32_t b0 = A.posBegin[t], b1 = A.posBegin[t + 1], f = A.posF[t];
     has = b0 != b1;
@@ -1206,10 +1218,14 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
     if (nF >= 3) { fl2 = it.len[f + 2]; fs2 = it.slot[f + 2]; }
     nS3 = nS == 3;
     nF3 = nF == 3;
+    fidx = f;
+    nS8 = min(nS, 255u);
+    nF8 = min(nF, 255u);
   }
   const bool hasF0 = fs0 != kNoSlot, hasF1 = fs1 != kNoSlot, hasF2 = fs2 != kNoSlot;
   const uint64_t hasF1M = __ballot(hasF1);  // per wave
-  const uint32_t flags = (hasF0 ? 1u : 0u) | (hasF1 ? 2u : 0u) | (hasF2 ? 4u : 0u) | (nS3 ? 8u : 0u) | (nF3 ? 16u : 0u);
+  const uint32_t flags = (hasF0 ? 1u : 0u) | (hasF1 ? 2u : 0u) | (hasF2 ? 4u : 0u) | (nS3 ? 8u : 0u) |
+                         (nF3 ? 16u : 0u) | (nS8 << 8) | (nF8 << 16);
   for (uint32_t k = 0; k < 6; k++) accL[k][tid] = 0;
   // lanes without items never fall in a record's range (their pairs are
   // counted once per staged record: counterDoNothing, FN:1530)
@@ -1233,15 +1249,25 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
   auto search = [&]() {
     __builtin_amdgcn_wave_barrier();
     for (uint32_t d = 0; d < nSearch; d += 64) {
-      if (d + lane < nSearch) {
-        const uint32_t en = myS[d + lane];
+      const bool act = d + lane < nSearch;
+      const uint32_t en = act ? myS[d + lane] : 0u;
+      // the target's item range from its owning lane
+      const int own = (int)((en >> 16) & 63u);
+      const uint32_t fo = __shfl(fidx, own), fl = __shfl(flags, own);
+      if (act) {
         const uint4 rc = myR[en & 0xffffu];
         const uint32_t tq = T0 + ((en >> 16) & 0xffu);
         const uint32_t q = rc.w, L = rc.x - tq;
         const bool S = (en >> 31) != 0;
         qs.slow++;
         auto addG = [&](uint32_t s, uint32_t v) { atomicAdd(&A.counter[s], (unsigned long long)v); };
-        d_counter_query_L<false>(GV, L, it.isa[q], S, rc.z & 0x7fffffffu, it.slot[q], tq, qs, addG);
+        const uint32_t nS = (fl >> 8) & 0xffu, nF = (fl >> 16) & 0xffu;
+        if (nS < 255u && nF < 255u) {
+          const KnownView KV{&A.it, A.nhr, tq, fo - nS, fo + nF, fo};
+          d_counter_query_L<false>(KV, L, it.isa[q], S, rc.z & 0x7fffffffu, it.slot[q], tq, qs, addG);
+        } else {
+          d_counter_query_L<false>(GV, L, it.isa[q], S, rc.z & 0x7fffffffu, it.slot[q], tq, qs, addG);
+        }
       }
     }
     __builtin_amdgcn_wave_barrier();
