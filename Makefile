@@ -23,7 +23,7 @@ $(OUT)/%.o: $(SRC)/%.hip $(HDRS) | $(OUT)
 
 # the uniform-step walk keeps its addresses in registers only without
 # SimplifyCFG store sinking (which otherwise moves them to scratch)
-W2WAVES ?= 5
+W2WAVES ?= 4
 $(OUT)/ms_walk2.o: $(SRC)/ms_walk2.hip $(HDRS) | $(OUT)
 	$(HIPCC) $(HIPFLAGS) -mllvm -simplifycfg-sink-common=false -DCMSBWT_W2_WAVES=$(W2WAVES) -c -o $@ $<
 
