@@ -1006,9 +1006,19 @@ struct Engine {
 
   uint32_t chunk_size() const {
     if (const char* e = getenv("CMSBWT_CHUNK")) return (uint32_t)std::max(64L, atol(e));
-    if (!walk_v1()) {  // queue-fed: ~1 chunk per lane (restarts cost; measured best at 16 K)
-      uint64_t c = chars / (uint64_t)walk_lanes();
-      return (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(16384, c));
+    if (!walk_v1()) {
+      // queue-fed: about 1.5 chunks per resident lane (CUs x 4 SIMDs x 4 waves
+      // x 64; restarts cost, a long last round of chunks costs too).  Config 3
+      // (10 GB, 256 CUs): 16 K 16.6 ms, 20 K 16.3, 22-26 K 15.6-15.8, 28 K
+      // 16.2, 32 K 16.5, 48 K 18.5 (walk kernel).
+      int dev = 0, cus = 256;
+      if (hipGetDevice(&dev) == hipSuccess) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
+      }
+      const uint64_t resident = (uint64_t)cus * 4 * 4 * 64;
+      uint64_t c = chars * 2 / (3 * resident);
+      return (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(32768, c));
     }
     uint64_t c = chars / (256ull * 64 * 64);
     c = std::max<uint64_t>(2048, std::min<uint64_t>(32768, c));
