@@ -341,6 +341,16 @@ struct Engine {
   }
   uint32_t select_flagged(const uint32_t* in, const uint32_t* flags, uint32_t* out, uint32_t n) {
     if (!n) return 0;
+    if (!env_u32("CMSBWT_ROCPRIM_SELECT", 0)) {  // two-pass tile compaction (merge.hip)
+      const uint32_t nt = sel_tiles(n);
+      DBuf<uint32_t> tc, to;
+      tc.alloc(nt);
+      to.alloc(nt);
+      mk_sel_count(flags, n, tc.p, st);
+      exscan(tc.p, to.p, 0u, nt);
+      mk_sel_write(in, flags, n, to.p, out, st);
+      return read1(to.p + (nt - 1)) + read1(tc.p + (nt - 1));
+    }
     DBuf<uint32_t> cnt;
     cnt.alloc(1);
     size_t b = 0;

@@ -1869,7 +1869,64 @@ __global__ void k_count_distinct(const uint32_t* __restrict__ v, uint32_t K, uns
 }
 
 // ------------------------------------------------------------ launchers
+
+// ---- stream compaction (order-preserving select of flagged u32 values).
+// Tiles of kSelRows x 256 elements: pass 1 counts each tile's flagged
+// elements, an exclusive scan gives the tile offsets, pass 2 ranks each row
+// by wave ballots and writes the kept values (replaces rocprim::select, which
+// ran at ~1/8 of the bandwidth this needs).
+constexpr uint32_t kSelRows = 8, kSelTile = kSelRows * 256;
+__global__ void __launch_bounds__(256) k_sel_count(const uint32_t* __restrict__ flags, uint32_t n,
+                                                   uint32_t* __restrict__ tileCnt) {
+  __shared__ uint32_t wc[4];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kSelTile;
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kSelRows; j++) {
+    const uint64_t e = t0 + j * 256 + threadIdx.x;
+    c += (e < n && flags[e] != 0) ? 1u : 0u;
+  }
+  for (uint32_t d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, (int)d);
+  if ((threadIdx.x & 63) == 0) wc[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) tileCnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
+}
+__global__ void __launch_bounds__(256) k_sel_write(const uint32_t* __restrict__ in, const uint32_t* __restrict__ flags,
+                                                   uint32_t n, const uint32_t* __restrict__ tileOff,
+                                                   uint32_t* __restrict__ out) {
+  __shared__ uint32_t wc[kSelRows][4];
+  const uint64_t t0 = (uint64_t)blockIdx.x * kSelTile;
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  bool keep[kSelRows];
+  uint32_t rk[kSelRows];
+#pragma unroll
+  for (uint32_t j = 0; j < kSelRows; j++) {
+    const uint64_t e = t0 + j * 256 + threadIdx.x;
+    keep[j] = e < n && flags[e] != 0;
+    const uint64_t m = __ballot(keep[j]);
+    rk[j] = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+    if (lane == 0) wc[j][wv] = (uint32_t)__popcll(m);
+  }
+  __syncthreads();
+  uint32_t base = tileOff[blockIdx.x];
+#pragma unroll
+  for (uint32_t j = 0; j < kSelRows; j++) {
+    uint32_t before = 0;
+    for (uint32_t w = 0; w < wv; w++) before += wc[j][w];
+    if (keep[j]) out[base + before + rk[j]] = in[t0 + j * 256 + threadIdx.x];
+    base += wc[j][0] + wc[j][1] + wc[j][2] + wc[j][3];
+  }
+}
 static inline dim3 g1(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+uint32_t sel_tiles(uint32_t n) { return (uint32_t)(((uint64_t)n + kSelTile - 1) / kSelTile); }
+void mk_sel_count(const uint32_t* flags, uint32_t n, uint32_t* tileCnt, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_sel_count, dim3(sel_tiles(n)), dim3(256), 0, st, flags, n, tileCnt);
+}
+void mk_sel_write(const uint32_t* in, const uint32_t* flags, uint32_t n, const uint32_t* tileOff, uint32_t* out,
+                  hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_sel_write, dim3(sel_tiles(n)), dim3(256), 0, st, in, flags, n, tileOff, out);
+}
+
 
 void mk_iota(uint32_t* p, uint64_t n, hipStream_t st) { if (n) hipLaunchKernelGGL(k_iota, g1(n), dim3(256), 0, st, p, n); }
 void mk_gather(const uint32_t* src, const uint32_t* perm, uint32_t* dst, uint64_t n, hipStream_t st) {
