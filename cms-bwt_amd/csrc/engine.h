@@ -292,9 +292,32 @@ struct Engine {
     HIPCHK(rocprim::exclusive_scan(nullptr, b, in, out, init, (size_t)n, op, st));
     HIPCHK(rocprim::exclusive_scan(scratch(b), b, in, out, init, (size_t)n, op, st));
   }
+  // u32 plus scans of plain arrays: the tile scan of merge.hip (tile sums,
+  // their rocPRIM scan, the tiles); anything else: rocPRIM
+  template <class In, class Out>
+  static constexpr bool kTileScan =
+      (std::is_same_v<In, uint32_t*> || std::is_same_v<In, const uint32_t*>) && std::is_same_v<Out, uint32_t*>;
+  void tile_scan(const uint32_t* in, uint32_t* out, uint32_t init, uint64_t n, bool inclusive) {
+    const uint64_t nt = scan_tiles(n);
+    DBuf<uint32_t> sums, off;
+    sums.alloc(nt);
+    off.alloc(nt);
+    mk_scan_sums(in, n, sums.p, st);
+    size_t b = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, b, sums.p, off.p, 0u, (size_t)nt, rocprim::plus<uint32_t>(), st));
+    HIPCHK(rocprim::exclusive_scan(scratch(b), b, sums.p, off.p, 0u, (size_t)nt, rocprim::plus<uint32_t>(), st));
+    mk_scan_tiles(in, out, n, off.p, init, inclusive, st);
+  }
+  static bool rocprim_scan() {
+    static const bool v = env_u32("CMSBWT_ROCPRIM_SCAN", 0) != 0;
+    return v;
+  }
   template <class In, class Out, class Init>
   void exscan(In in, Out out, Init init, uint64_t n) {
     if (!n) return;
+    if constexpr (kTileScan<In, Out> && std::is_same_v<Init, uint32_t>) {
+      if (!rocprim_scan()) { tile_scan(in, out, init, n, false); return; }
+    }
     size_t b = 0;
     HIPCHK(rocprim::exclusive_scan(nullptr, b, in, out, init, (size_t)n, rocprim::plus<Init>(), st));
     HIPCHK(rocprim::exclusive_scan(scratch(b), b, in, out, init, (size_t)n, rocprim::plus<Init>(), st));
@@ -302,6 +325,9 @@ struct Engine {
   template <class In, class Out, class Op>
   void inscan(In in, Out out, uint64_t n, Op op) {
     if (!n) return;
+    if constexpr (kTileScan<In, Out> && std::is_same_v<Op, rocprim::plus<uint32_t>>) {
+      if (!rocprim_scan()) { tile_scan(in, out, 0u, n, true); return; }
+    }
     size_t b = 0;
     HIPCHK(rocprim::inclusive_scan(nullptr, b, in, out, (size_t)n, op, st));
     HIPCHK(rocprim::inclusive_scan(scratch(b), b, in, out, (size_t)n, op, st));

@@ -1917,7 +1917,85 @@ __global__ void __launch_bounds__(256) k_sel_write(const uint32_t* __restrict__ 
     base += wc[j][0] + wc[j][1] + wc[j][2] + wc[j][3];
   }
 }
+
+// ---- u32 plus scans (exclusive / inclusive), two passes over tiles of 2048:
+// tile sums, a scan of the sums, then each thread scans its 8 contiguous
+// values (two 16-byte loads) under a block scan of the thread totals.
+// (rocprim's lookback scan ran at ~1.3 TB/s on these arrays.)
+constexpr uint32_t kScanIpt = 8, kScanTile = 256 * kScanIpt;
+__device__ __forceinline__ void scan_load8(const uint32_t* __restrict__ in, uint64_t e, uint64_t n, bool vec,
+                                           uint32_t v[kScanIpt]) {
+  if (vec && e + kScanIpt <= n) {
+    const uint4 a = *reinterpret_cast<const uint4*>(in + e), b = *reinterpret_cast<const uint4*>(in + e + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kScanIpt; k++) v[k] = e + k < n ? in[e + k] : 0u;
+  }
+}
+__global__ void __launch_bounds__(256) k_scan_sums(const uint32_t* __restrict__ in, uint64_t n, int vec,
+                                                   uint32_t* __restrict__ sums) {
+  __shared__ uint32_t wsum[4];
+  const uint64_t e = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanIpt;
+  uint32_t v[kScanIpt];
+  scan_load8(in, e, n, vec != 0, v);
+  uint32_t c = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanIpt; k++) c += v[k];
+  for (uint32_t d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, (int)d);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) sums[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+__global__ void __launch_bounds__(256) k_scan_tiles(const uint32_t* in, uint32_t* out, uint64_t n, int vec,
+                                                    const uint32_t* __restrict__ tileOff, uint32_t init,
+                                                    int inclusive) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t e = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanIpt;
+  uint32_t v[kScanIpt];
+  scan_load8(in, e, n, vec != 0, v);
+  uint32_t tot = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanIpt; k++) tot += v[k];
+  uint32_t inc = tot;  // inclusive scan of the thread totals in the wave
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t o = __shfl_up(inc, d);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  uint32_t base = init + tileOff[blockIdx.x] + (inc - tot);
+  for (uint32_t w = 0; w < wv; w++) base += wsum[w];
+  uint32_t r[kScanIpt];
+#pragma unroll
+  for (uint32_t k = 0; k < kScanIpt; k++) {
+    if (inclusive) { base += v[k]; r[k] = base; }
+    else { r[k] = base; base += v[k]; }
+  }
+  if (vec != 0 && e + kScanIpt <= n) {
+    *reinterpret_cast<uint4*>(out + e) = make_uint4(r[0], r[1], r[2], r[3]);
+    *reinterpret_cast<uint4*>(out + e + 4) = make_uint4(r[4], r[5], r[6], r[7]);
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kScanIpt; k++)
+      if (e + k < n) out[e + k] = r[k];
+  }
+}
 static inline dim3 g1(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
+uint64_t scan_tiles(uint64_t n) { return (n + kScanTile - 1) / kScanTile; }
+void mk_scan_sums(const uint32_t* in, uint64_t n, uint32_t* sums, hipStream_t st) {
+  const int vec = (((uintptr_t)in) & 15) == 0;
+  if (n) hipLaunchKernelGGL(k_scan_sums, dim3((unsigned)scan_tiles(n)), dim3(256), 0, st, in, n, vec, sums);
+}
+void mk_scan_tiles(const uint32_t* in, uint32_t* out, uint64_t n, const uint32_t* tileOff, uint32_t init,
+                   bool inclusive, hipStream_t st) {
+  const int vec = ((((uintptr_t)in) | ((uintptr_t)out)) & 15) == 0;
+  if (n)
+    hipLaunchKernelGGL(k_scan_tiles, dim3((unsigned)scan_tiles(n)), dim3(256), 0, st, in, out, n, vec, tileOff, init,
+                       inclusive ? 1 : 0);
+}
+
 uint32_t sel_tiles(uint32_t n) { return (uint32_t)(((uint64_t)n + kSelTile - 1) / kSelTile); }
 void mk_sel_count(const uint32_t* flags, uint32_t n, uint32_t* tileCnt, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_sel_count, dim3(sel_tiles(n)), dim3(256), 0, st, flags, n, tileCnt);

@@ -102,6 +102,11 @@ void mk_dbl_groups(const uint32_t* act, const uint64_t* key, const uint32_t* val
 void mk_head_ranks(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint32_t* headRank, uint8_t* bwtHeads,
                    hipStream_t st);
 // map order of each position's items (one thread per position)
+// u32 plus scans over tiles of 2048 (tile sums, their scan, the tiles)
+uint64_t scan_tiles(uint64_t n);
+void mk_scan_sums(const uint32_t* in, uint64_t n, uint32_t* sums, hipStream_t st);
+void mk_scan_tiles(const uint32_t* in, uint32_t* out, uint64_t n, const uint32_t* tileOff, uint32_t init,
+                   bool inclusive, hipStream_t st);
 // order-preserving compaction of flagged u32 values (tiles of 2048)
 uint32_t sel_tiles(uint32_t n);
 void mk_sel_count(const uint32_t* flags, uint32_t n, uint32_t* tileCnt, hipStream_t st);
