@@ -10,10 +10,11 @@ HOSTFLAGS := -O3 -std=c++17 -fPIC -Wall
 OBJS := $(OUT)/engine.o $(OUT)/dist_merge.o $(OUT)/dist_kernels.o $(OUT)/ms_walk.o $(OUT)/ms_walk2.o $(OUT)/merge.o $(OUT)/synth.o $(OUT)/coll_read.o $(OUT)/ref_index.o $(OUT)/host_index.o $(OUT)/host_reader.o
 HDRS := $(wildcard $(SRC)/*.h) include/cmsbwt.h
 
-all: lib cli oracle
+all: lib cli gen oracle
 
 lib: $(OUT)/libcmsbwt.so
 cli: $(OUT)/cmsbwt
+gen: $(OUT)/gen_synth
 
 $(OUT):
 	mkdir -p $(OUT)
@@ -36,6 +37,11 @@ $(OUT)/libcmsbwt.so: $(OBJS)
 $(OUT)/cmsbwt: $(SRC)/cli_main.cpp $(OUT)/libcmsbwt.so include/cmsbwt.h
 	g++ $(HOSTFLAGS) -o $@ $< -L$(OUT) -lcmsbwt -Wl,-rpath,'$$ORIGIN'
 
+# synthetic FASTA workload writer, used by bench.py's
+# end-to-end leg: product-side, independent of the oracle's copy
+$(OUT)/gen_synth: tools/gen_synth.cpp $(SRC)/synth.h | $(OUT)
+	g++ $(HOSTFLAGS) -pthread -o $@ tools/gen_synth.cpp
+
 oracle:
 	$(MAKE) -C oracle
 
@@ -43,4 +49,4 @@ clean:
 	rm -rf $(OUT)
 	$(MAKE) -C oracle clean
 
-.PHONY: all lib cli oracle clean
+.PHONY: all lib cli gen oracle clean

@@ -6,9 +6,16 @@ reference + 1000 copies mutated at 0.1 % SNP rate (10 GB of collection text),
 counter-based generator as tools/gen_synth (synth.h), so the timed region
 starts with inputs resident.  One step = MS walk + j-scan + the whole merge to
 packed .rl_bwt run records in HBM (cmsbwt_step); the reference index is built
-once before timing (north_star keeps libsais-equivalent SA on the host).
+once before timing.
 
 value = collection sequence bytes / 1e6 / seconds per step, whole job.
+
+Two more legs ride on the same line (rank 0, N = 1):
+* "e2e" — SURVEY.md §8(d) Metric 1: the `cmsbwt -r` process on FASTA files
+  of the same workload written by the product's gen_synth (page cache), wall
+  time from process start to output closed; the .rl_bwt's sha256 is compared
+  with the oracle's golden for this workload (tests/golden/golden.json).
+* "cpu_baseline" — the single-threaded CPU oracle on a bounded sample.
 """
 import argparse
 import json
@@ -62,16 +69,33 @@ def cpu_baseline(ref_len, copies, p, seed, rle=True):
             "seconds": round(t_coll, 3)}
 
 
-PMC_FILE = "r02_pmc.json"  # tools/gpu_prof_r.sh + tools/pmc_main.py (this round's kernels)
+PMC_FILE = "r02_pmc.json"  # tools/gpu_prof_r.sh + tools/pmc_summary.py (this round's kernels)
+
+# Algorithmic bytes of the MS walk (k_ms_walk2) -- what THIS algorithm must
+# move, each byte counted once (DESIGN.md §3.1 "Roofline"):
+#   per collection character: the text byte and the reference byte it is
+#     compared with at the extension frontier (FN:52-62); positions the PLCP
+#     skip covers (FN:1176-1185) are compared once, by the extension that
+#     reached them;
+#   per head: its 16-B record (pool write), the 8-B prefix-table entry that
+#     resolves it (one probe per head), and the 4-B PLCP entry at the skip exit.
+WALK_B_PER_CHAR = 2
+WALK_B_PER_HEAD = 16 + 8 + 4
+# SURVEY.md §8(d)'s model prices the reference's per-character streams
+# (1 B text + 1 B ref + 4 B PLCP + 16 B int64 bucket RMW per character, 24 B
+# per head), which this walk replaces by run difference arrays and one skip
+# per head; reported beside, as frac_survey_model.
+SURVEY_B_PER_CHAR, SURVEY_B_PER_HEAD = 22, 24
 
 
 def pmc_traffic(args, kernel="k_ms_walk2"):
-    """Beyond-L2 bytes per launch of the walk kernel from the committed PMC
-    summary (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes, KiB
-    units; tools/gpu_prof.sh), for the default workload only.  Per
+    """Beyond-L2 bytes per launch of a kernel from the committed PMC summary
+    (rocprofv3 --pmc FETCH_SIZE and WRITE_SIZE in separate passes, KiB units;
+    tools/gpu_prof_r.sh), for the default workload only.  Per
     MI355X_MICROARCH.md (HBM): FETCH_SIZE = TCC_EA0_RDREQ x 64 B counts half
     the bytes of 128-B requests on gfx950, so it is doubled; both counters
-    include Infinity-Cache hits."""
+    include Infinity-Cache hits, so this is fabric traffic, an upper bound on
+    HBM bytes."""
     default = (args.ref_len, args.copies, args.p, args.seed) == (10_000_000, 1000, 0.001, 4)
     path = os.path.join(ROOT, "profiles", PMC_FILE)
     if not default or not os.path.exists(path):
@@ -84,17 +108,83 @@ def pmc_traffic(args, kernel="k_ms_walk2"):
         return None, None
 
 
+def golden_for(args, rle):
+    """The oracle's sha256 for this exact workload, when committed."""
+    try:
+        g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
+    except (OSError, ValueError):
+        return None
+    for k, v in g.items():
+        if isinstance(v, dict) and v.get("generator") == "synth.h" and \
+                v.get("args") == [args.ref_len, args.copies, args.p, args.seed]:
+            return v.get("rl_bwt_sha256" if rle else "bwt_sha256")
+    return None
+
+
+def _sha256_file(path):
+    import hashlib
+    h = hashlib.sha256()
+    with open(path, "rb") as f:
+        for blk in iter(lambda: f.read(1 << 24), b""):
+            h.update(blk)
+    return h.hexdigest()
+
+
+def e2e_leg(args, rle):
+    """SURVEY.md §8(d) Metric 1: collection MB/s of the drop-in CLI, wall time
+    from process start to output closed, on FASTA files in the page cache."""
+    import shutil
+    build = os.path.join(ROOT, "cms-bwt_amd", "build")
+    gen, cli = os.path.join(build, "gen_synth"), os.path.join(build, "cmsbwt")
+    base = os.environ.get("CMSBWT_E2E_DIR") or os.environ.get("TMPDIR") or "/tmp"
+    chars = args.ref_len * args.copies
+    need = int(chars * 1.05) + (chars // 8 if rle else chars) + (1 << 30)
+    free = shutil.disk_usage(base).free
+    if free < need:
+        return {"skipped": f"{base} has {free >> 20} MiB free, needs {need >> 20} MiB"}
+    td = tempfile.mkdtemp(prefix="cmsbwt_e2e_", dir=base)
+    try:
+        pre = os.path.join(td, "w")
+        t0 = time.perf_counter()
+        subprocess.run([gen, str(args.ref_len), str(args.copies), str(args.p), str(args.seed), pre], check=True)
+        t_gen = time.perf_counter() - t0
+        walls, stages = [], ""
+        for _ in range(args.e2e_reps):
+            cmd = [cli] + (["-r"] if rle else []) + ["-v", "-o", pre + "_out", pre + ".list"]
+            t0 = time.perf_counter()
+            r = subprocess.run(cmd, stdout=subprocess.DEVNULL, stderr=subprocess.PIPE, text=True)
+            walls.append(time.perf_counter() - t0)
+            if r.returncode:
+                return {"error": f"cmsbwt exit {r.returncode}: {r.stderr[-400:]}"}
+            stages = (r.stderr.strip().splitlines() or [""])[-1]
+        out = pre + "_out" + (".rl_bwt" if rle else ".bwt")
+        sha = _sha256_file(out)
+        want = golden_for(args, rle)
+        med = sorted(walls)[len(walls) // 2]
+        return {"metric": "collection MB/s, cmsbwt process start to output closed (SURVEY.md §8d Metric 1)",
+                "value": round(chars / 1e6 / med, 1), "unit": "MB/s", "wall_s": [round(w, 3) for w in walls],
+                "wall_median_s": round(med, 3), "output_bytes": os.path.getsize(out),
+                "stages": stages, "input": "FASTA files in the page cache (product gen_synth, %.1f s)" % t_gen,
+                "sha256": sha[:16],
+                "parity": ("bit-exact vs oracle golden" if want and sha == want else
+                           "MISMATCH vs oracle golden" if want else "no golden for this workload")}
+    finally:
+        shutil.rmtree(td, ignore_errors=True)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--ref-len", type=int, default=10_000_000)
     ap.add_argument("--copies", type=int, default=1000)
     ap.add_argument("--p", type=float, default=0.001)
     ap.add_argument("--seed", type=int, default=4)
-    ap.add_argument("--cpu-copies", type=int, default=10)
+    ap.add_argument("--cpu-copies", type=int, default=30)
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end CLI leg (Metric 1)")
+    ap.add_argument("--e2e-reps", type=int, default=3)
     ap.add_argument("--plain", action="store_true",
                     help="plain .bwt instead of .rl_bwt (BASELINE config 5 runs without -r)")
     args = ap.parse_args()
@@ -158,14 +248,15 @@ def main():
     ms_step = dt / args.steps * 1e3
     value = chars_total / 1e6 / (dt / args.steps)
 
-    # Roofline of the dominant kernel: the MS walk, priced with SURVEY.md §8(d)'s
-    # per-character streams of the reference algorithm (B_MS = 22 N + 24 H) over
-    # its measured HIP-event duration (last step, on the engine's stream).
+    # Roofline of the dominant kernel, the MS walk: algorithmic bytes of this
+    # algorithm (WALK_B_PER_*) over its HIP-event duration (last step, on the
+    # engine's stream, where the kernel is launched)
     n_local = st_walk_chars
     heads_local = st.heads if world == 1 else int(st.heads * (c1 - c0) / max(1, args.copies))
-    b_ms = 22 * n_local + 24 * heads_local
+    b_alg = WALK_B_PER_CHAR * n_local + WALK_B_PER_HEAD * heads_local
+    b_survey = SURVEY_B_PER_CHAR * n_local + SURVEY_B_PER_HEAD * heads_local
     t_ms = st.ms_walk_kernel_ms / 1e3
-    achieved = b_ms / t_ms / 1e9 if t_ms > 0 else 0.0
+    achieved = b_alg / t_ms / 1e9 if t_ms > 0 else 0.0
     traffic, traffic_src = pmc_traffic(args) if world == 1 else (None, None)
     ctraffic, _ = pmc_traffic(args, "k_counter_tgt") if world == 1 else (None, None)
     c_ms = st.counter_kernel_ms
@@ -188,11 +279,15 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_ms_walk2", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "algorithmic_bytes": b_ms, "kernel_ms": round(st.ms_walk_kernel_ms, 3),
-                     "bytes_model": "22 B/char + 24 B/head (SURVEY.md §8d); the walk skips the "
-                                    "reference's per-character streams, so achieved can exceed the peak",
+                     "algorithmic_bytes": b_alg, "kernel_ms": round(st.ms_walk_kernel_ms, 3),
+                     "bytes_model": f"{WALK_B_PER_CHAR} B/char (text + reference byte at the extension frontier) "
+                                    f"+ {WALK_B_PER_HEAD} B/head (16-B record, 8-B prefix probe, 4-B PLCP exit); "
+                                    "DESIGN.md §3.1",
+                     "traffic_over_algorithmic": round(traffic / b_alg, 2) if traffic else None,
                      "traffic_GBps": round(traffic / t_ms / 1e9, 1) if traffic and t_ms > 0 else None,
-                     "traffic_frac": round(traffic / t_ms / 1e9 / HBM_PEAK_GBS, 4) if traffic and t_ms > 0 else None},
+                     "frac_survey_model": round(b_survey / t_ms / 1e9 / HBM_PEAK_GBS, 4) if t_ms > 0 else None,
+                     "survey_model": "22 B/char + 24 B/head (SURVEY.md §8d: the reference's per-character "
+                                     "streams; exceeds 1 because this walk does not perform them)"},
         # the merge's largest kernel (counterSmallerThanHead, FN:1523-1603):
         # register/LDS-bound, measured HBM traffic for reference
         "counter_kernel": {"kernel": "k_counter_tgt", "kernel_ms": round(c_ms, 3),
@@ -203,6 +298,12 @@ def main():
                       "ms_walk_kernel": round(st.ms_walk_kernel_ms, 2),
                       "counter_kernel": round(st.counter_kernel_ms, 2)},
     }
+    eng.close()
+    if rank == 0 and world == 1 and not args.no_e2e:
+        try:
+            out["e2e"] = e2e_leg(args, rle)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["e2e"] = {"error": str(e)[-400:]}
     if rank == 0 and not args.no_cpu:
         try:
             out["cpu_baseline"] = cpu_baseline(args.ref_len, args.cpu_copies, args.p, args.seed, rle=rle)
@@ -210,7 +311,6 @@ def main():
             out["cpu_baseline"] = {"error": str(e)}
     if rank == 0:
         print(json.dumps(out), flush=True)
-    eng.close()
     if dist:
         dist.destroy_process_group()
 

@@ -65,7 +65,11 @@ class Stats(ctypes.Structure):
         "counter_bad", "counter_good", "counter_nothing", "runs", "symbols", "order_violations")] + \
         [(k, ctypes.c_double) for k in (
             "t_index_s", "t_upload_s", "t_ms_walk_s", "t_merge_s", "t_write_s", "ms_walk_kernel_ms",
-            "counter_kernel_ms")] + [("counter_work", ctypes.c_uint64), ("order_invariant", ctypes.c_uint64)]
+            "counter_kernel_ms")] + [("counter_work", ctypes.c_uint64), ("order_invariant", ctypes.c_uint64)] + \
+        [(k, ctypes.c_uint64) for k in ("ref_file_bytes", "ref_read_size", "coll_file_bytes", "sn_initial")] + \
+        [(k, ctypes.c_int64) for k in ("first_rank_to_head", "last_rank_to_head")] + \
+        [(k, ctypes.c_double) for k in ("t_augment_ms", "t_sa_ms", "t_isa_ms", "t_lcp_ms", "t_rmq_ms", "t_bwt_ms",
+                                        "t_ranks_ms", "t_libsais_int_ms", "t_counter_ms")]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

@@ -438,6 +438,7 @@ void Engine::dm_finish(const unsigned long long* const* starts, const uint8_t* c
   lastRle = dm.rle;
   merged = true;
   dm.on = true;
+  stats.first_rank_to_head = stats.last_rank_to_head = -1;  // head ranks stay on the document ranks
   // gstats: heads, keys, ndocs, chars, bad, good, nothing, violations
   stats.heads = gstats[0];
   stats.keys = gstats[1];

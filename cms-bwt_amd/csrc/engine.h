@@ -254,6 +254,10 @@ struct Engine {
   DBuf<uint8_t> tmp;  // rocPRIM scratch
 
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  // merge phase marks for the reference's log timers: ranks start, doubling
+  // start / end, ranks end, counter start / end
+  hipEvent_t evm[6] = {};
+  DBuf<uint32_t> rthFL;  // grp[0], grp[H-1] of the last merge (First/Last rankToHead + 1)
 
   explicit Engine(int dev) : device(dev) {
     g_alloc = &alloc;
@@ -261,12 +265,14 @@ struct Engine {
     HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
     HIPCHK(hipEventCreate(&ev0));
     HIPCHK(hipEventCreate(&ev1));
+    for (auto& e : evm) HIPCHK(hipEventCreate(&e));
   }
   ~Engine() {
     g_alloc = &alloc;
     for (void* b : pinned) (void)hipHostFree(b);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
+    for (auto e : evm) if (e) (void)hipEventDestroy(e);
     if (st) (void)hipStreamDestroy(st);
   }
 
@@ -452,11 +458,19 @@ struct Engine {
     err.alloc(1);
     err.zero(st);
     if (env_u32("CMSBWT_TIMING", 0)) fprintf(stderr, "[index] sa         %.3f s\n", std::chrono::duration<double>(t1 - t0).count());
+    // stage times of the reference's log (FN:258-299): ISA, LCP + PLCP, RMQ
+    // (the LCP block minima the PSV/NSV scans climb), BWT, by HIP events
+    hipEvent_t ix[5];
+    for (auto& e : ix) HIPCHK(hipEventCreate(&e));
+    HIPCHK(hipEventRecord(ix[0], st));
     {
       DBuf<int32_t> phi, plcpRaw;
       phi.alloc(n);
       plcpRaw.alloc(n);
-      launch_ix_lcp(dx.p, dsa.p, n, disa.p, phi.p, plcpRaw.p, dlcp.p, dbwt.p, dplcp.p, st);
+      launch_ix_isa(dsa.p, n, disa.p, phi.p, st);
+      HIPCHK(hipEventRecord(ix[1], st));
+      launch_ix_lcp(dx.p, dsa.p, n, disa.p, phi.p, plcpRaw.p, dlcp.p, dplcp.p, st);
+      HIPCHK(hipEventRecord(ix[2], st));
     }
     launch_ix_plcp_check(dplcp.p, n, err.p, st);
     uint64_t off = pad((uint64_t)n + 1);
@@ -474,6 +488,19 @@ struct Engine {
       L++;
     }
     R.nlvl = L;
+    HIPCHK(hipEventRecord(ix[3], st));
+    launch_ix_bwt(dx.p, dsa.p, n, dbwt.p, st);
+    HIPCHK(hipEventRecord(ix[4], st));
+    HIPCHK(hipEventSynchronize(ix[4]));
+    {
+      float v = 0;
+      double* dst[4] = {&hix.t_isa, &hix.t_lcp_only, &hix.t_rmq, &hix.t_bwt};
+      for (int k = 0; k < 4; k++) {
+        HIPCHK(hipEventElapsedTime(&v, ix[k], ix[k + 1]));
+        *dst[k] = v / 1e3;
+      }
+    }
+    for (auto e : ix) (void)hipEventDestroy(e);
     R.x = dx.p;
     R.sa = dsa.p;
     R.isa = disa.p;
@@ -524,15 +551,27 @@ struct Engine {
       throw InputError{CMSBWT_EINPUT, "reference contains byte 0x02 (the document separator)"};
     if (trimmed.size() + 130 >= (1ull << 31)) throw InputError{CMSBWT_ELIMIT, "reference longer than 2^31 (int32 SA)"};
     const char* hi = getenv("CMSBWT_HOST_INDEX");
+    hix.t_isa = hix.t_lcp_only = hix.t_rmq = hix.t_bwt = 0;
     if (hi && *hi && *hi != '0') {
       build_index(trimmed, hix);
+      hix.t_augment = 0;
       stage_host();
     } else {
+      auto ta = std::chrono::steady_clock::now();
       augment_reference(trimmed, hix);
+      hix.t_augment = std::chrono::duration<double>(std::chrono::steady_clock::now() - ta).count();
       stage_device();
     }
     refLoaded = true;
     stats.n = hix.n;
+    stats.t_augment_ms = hix.t_augment * 1e3;
+    stats.t_sa_ms = hix.t_sa * 1e3;
+    stats.t_isa_ms = hix.t_isa * 1e3;
+    stats.t_lcp_ms = hix.t_lcp_only * 1e3;
+    stats.t_rmq_ms = hix.t_rmq * 1e3;
+    stats.t_bwt_ms = hix.t_bwt * 1e3;
+    stats.ref_file_bytes = hix.file_bytes;
+    stats.ref_read_size = hix.read_size;
     stats.t_index_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
 
@@ -1582,6 +1621,7 @@ struct Engine {
     if (!orderInvariant || env_u32("CMSBWT_FORCE_CHECK", 0)) mk_check_items(S, posBegin.p, posF.p, K, cstats.p + 3, st);
 
     // ---- ranks (FN:1432-1453)
+    HIPCHK(hipEventRecord(evm[0], st));
     DBuf<uint32_t> itemsSA, headsSA, itemRankBase, headBase;
     // rank2head (T) is only kept for parity copies (CMSBWT_KEEP_STAGES=1):
     // the suffix sort below needs the group labels, not the ranks themselves
@@ -1628,6 +1668,7 @@ struct Engine {
     stats.rank = (uint64_t)E + 2 + (uint64_t)(K - 1);
 
     // ---- suffix sort of the head string (libsais_int, FN:1455-1459)
+    HIPCHK(hipEventRecord(evm[1], st));
     {
       const int bH = bits_for(H);
       const bool dstats = env_u32("CMSBWT_DBL_STATS", 0) != 0;
@@ -1689,6 +1730,10 @@ struct Engine {
     // Every group is a single head now, and a group's label is its first sa
     // position: grp[idx] = 1 + rank of head idx (FN:1468-1471's rankToHead),
     // so the inverse permutation needs no scatter.
+    HIPCHK(hipEventRecord(evm[2], st));
+    rthFL.alloc(2);
+    HIPCHK(hipMemcpyAsync(rthFL.p, grp.p, 4, hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipMemcpyAsync(rthFL.p + 1, grp.p + (H - 1), 4, hipMemcpyDeviceToDevice, st));
     bwtHeads.alloc(H);
     mk_head_chars(saT.p, hChar.p, H, bwtHeads.p, st);
 
@@ -1712,6 +1757,7 @@ struct Engine {
     }
     grp.release();
     Pm.release();
+    HIPCHK(hipEventRecord(evm[3], st));
 
     // ---- counterSmallerThanHead (FN:1523-1603)
     counter.alloc((uint64_t)H + 1);
@@ -1727,7 +1773,9 @@ struct Engine {
       HIPCHK(rocprim::reduce(scratch(b), b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
       W = read1(wsum.p);
       const bool check = !orderInvariant || env_u32("CMSBWT_FORCE_CHECK", 0) != 0;
+      HIPCHK(hipEventRecord(evm[4], st));
       counter_phase(S, K, posBegin.p, posF.p, nhr.p, counter.p, cstats.p, n, 0, n, check);
+      HIPCHK(hipEventRecord(evm[5], st));
     }
     unsigned long long cs[8];
     HIPCHK(hipMemcpyAsync(cs, cstats.p, sizeof(cs), hipMemcpyDeviceToHost, st));
@@ -1815,6 +1863,19 @@ struct Engine {
     stats.runs = Rn;
     stats.symbols = symbols;
     stats.positions = count_positions(sPos);
+    {
+      uint32_t fl[2] = {0, 0};
+      HIPCHK(hipMemcpy(fl, rthFL.p, 8, hipMemcpyDeviceToHost));
+      stats.first_rank_to_head = (int64_t)fl[0] - 1;
+      stats.last_rank_to_head = (int64_t)fl[1] - 1;
+      float a = 0, b = 0, c = 0;
+      HIPCHK(hipEventElapsedTime(&a, evm[0], evm[3]));
+      HIPCHK(hipEventElapsedTime(&b, evm[1], evm[2]));
+      HIPCHK(hipEventElapsedTime(&c, evm[4], evm[5]));
+      stats.t_ranks_ms = a;
+      stats.t_libsais_int_ms = b;
+      stats.t_counter_ms = c;
+    }
     stats.t_merge_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
   double poolDensity = 1.0 / 32;  // head-pool records per collection char (learned per engine)

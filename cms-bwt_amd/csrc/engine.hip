@@ -63,14 +63,20 @@ int cmsbwt_load_reference_file(cmsbwt_ctx* ctx, const char* path) {
   if (!ctx || !path) return CMSBWT_EARG;
   return guard(ctx, [&] {
     std::string x, err;
-    if (!cmsbwt::read_reference(path, x, err)) throw cmsbwt::InputError{CMSBWT_EIO, err};
+    uint64_t fb = 0, rs = 0;
+    if (!cmsbwt::read_reference(path, x, err, &fb, &rs)) throw cmsbwt::InputError{CMSBWT_EIO, err};
+    ctx->e->hix.file_bytes = fb;
+    ctx->e->hix.read_size = rs;
     ctx->e->load_reference_bytes(x);
   });
 }
 
 int cmsbwt_load_reference(cmsbwt_ctx* ctx, const uint8_t* ref, uint64_t len) {
   if (!ctx || (!ref && len)) return CMSBWT_EARG;
-  return guard(ctx, [&] { ctx->e->load_reference_bytes(std::string((const char*)ref, len)); });
+  return guard(ctx, [&] {
+    ctx->e->hix.file_bytes = ctx->e->hix.read_size = len;
+    ctx->e->load_reference_bytes(std::string((const char*)ref, len));
+  });
 }
 
 int cmsbwt_load_collection_file(cmsbwt_ctx* ctx, const char* path, uint64_t prefix) {
@@ -82,12 +88,16 @@ int cmsbwt_load_collection_file(cmsbwt_ctx* ctx, const char* path, uint64_t pref
     const char* hr = getenv("CMSBWT_HOST_READER");
     if (prefix == UINT64_MAX && !(hr && *hr && *hr != '0')) {
       ctx->e->load_collection_file_gpu(path);
-      return;
+    } else {
+      cmsbwt::Collection c;
+      std::string err;
+      if (!cmsbwt::read_collection(path, prefix, c, err)) throw cmsbwt::InputError{CMSBWT_EIO, err};
+      ctx->e->upload_collection(c);
     }
-    cmsbwt::Collection c;
-    std::string err;
-    if (!cmsbwt::read_collection(path, prefix, c, err)) throw cmsbwt::InputError{CMSBWT_EIO, err};
-    ctx->e->upload_collection(c);
+    struct stat sb;  // FN:221-224: ftello of the collection and the initial _sn
+    const uint64_t fsz = stat(path, &sb) == 0 ? (uint64_t)sb.st_size : 0;
+    ctx->e->stats.coll_file_bytes = fsz;
+    ctx->e->stats.sn_initial = std::min<uint64_t>(fsz, prefix);
   });
 }
 
@@ -197,7 +207,9 @@ int cmsbwt_host_suffix_array(const uint8_t* s, uint64_t n, int32_t* sa_out) {
   return CMSBWT_OK;
 }
 
-// Whole run with the reference's log (FN keys).
+// Whole run with the reference's log (FN keys in the reference's order,
+// SURVEY.md App. C): initialize_reference FN:151-310, then the large- or
+// small-reference collection pass (FN:1093-1628 / FN:312-936) and a writer.
 int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path, cmsbwt_stats* stats_out) {
   if (!a || !ref_path || !coll_path || !a->outname) return CMSBWT_EARG;
   std::string out = a->outname;
@@ -214,44 +226,96 @@ int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path
   auto ms = [](std::chrono::steady_clock::time_point x, std::chrono::steady_clock::time_point y) {
     return (long long)std::chrono::duration_cast<std::chrono::milliseconds>(y - x).count();
   };
+  auto fail = [&](int code) {
+    log << ctx->err << "\n";
+    cmsbwt_ctx_destroy(ctx);
+    return code;
+  };
   auto t0 = now();
   log << "About to read ref\n";
+  {
+    // FN:155-160: the reference is opened first (errno reported)
+    FILE* f = fopen(ref_path, "r");
+    if (!f) {
+      log << "Error opening file of base sequence " << ref_path << ", errno=" << errno << '\n';
+      cmsbwt_ctx_destroy(ctx);
+      return CMSBWT_EIO;
+    }
+    fclose(f);
+  }
   rc = cmsbwt_load_reference_file(ctx, ref_path);
-  if (rc) { log << ctx->err << "\n"; cmsbwt_ctx_destroy(ctx); return rc; }
   Engine& e = *ctx->e;
-  log << "Reference (size = " << e.hix.x.size() << "):\n\t";
-  log << "Computing SA done in " << (long long)(e.hix.t_sa * 1000) << " ms\n";
-  log << "Computing LCP and PLCP done in " << (long long)(e.hix.t_lcp * 1000) << " ms\n";
+  if (rc) {
+    if (e.hix.file_bytes) log << "n = " << e.hix.file_bytes << '\n';
+    return fail(rc);
+  }
+  const cmsbwt_stats& s = e.stats;
+  const uint64_t sn0 = [&] {  // FN:215-224: the collection is opened here, before augmenting
+    struct stat sb;
+    return stat(coll_path, &sb) == 0 ? (uint64_t)sb.st_size : ~0ull;
+  }();
+  log << "n = " << s.ref_file_bytes << '\n';
+  log << "Reference (size = " << s.ref_read_size << "):\n\t";
+  if (sn0 == ~0ull) {
+    log << "Error opening file of sequence (" << coll_path << ")\n";
+    cmsbwt_ctx_destroy(ctx);
+    return CMSBWT_EIO;
+  }
+  log << "ftello(infile): " << sn0 << '\n';
+  log << "sn: " << std::min<uint64_t>(sn0, a->prefix) << '\n';
+  log << "Augmenting reference done in " << (long long)s.t_augment_ms << " ms\n";
+  log << "Computing SA done in " << (long long)s.t_sa_ms << " ms\n";
+  log << "\tComputing ISA..." << '\n';
+  log << "Computing ISA done in " << (long long)s.t_isa_ms << " ms\n";
+  log << "Computing LCP and PLCP done in " << (long long)s.t_lcp_ms << " ms\n";
+  log << "Computing RMQ...\n";
+  log << "Computing RMQ done in " << (long long)s.t_rmq_ms << " ms\n";
+  log << "Computing BWT...\n";
+  log << "Computing BWT done in " << (long long)s.t_bwt_ms << " ms\n";
+  log << "Finished pre-processing\n";
   log << "Preprocessing done in " << ms(t0, now()) << " ms\n";
   auto t1 = now();
   rc = cmsbwt_load_collection_file(ctx, coll_path, a->prefix);
-  if (rc) { log << ctx->err << "\n"; cmsbwt_ctx_destroy(ctx); return rc; }
+  if (rc) return fail(rc);
+  const bool small = e.R.n < 1000000;  // FN:1792: small-reference path below 1e6
   log << "File is in memory\n";
   log << "_x.len: " << e.R.n << '\n';
-  log << "_sx.len: " << e.sn << '\n';
+  log << "_sx.len: " << s.sn_initial << '\n';
+  log << "About to start main parsing loop...\n";
   rc = cmsbwt_ms_walk(ctx);
-  if (rc) { log << ctx->err << "\n"; cmsbwt_ctx_destroy(ctx); return rc; }
+  if (rc) return fail(rc);
   log << "Finished parsing file of length: " << e.sn << "\n";
   rc = cmsbwt_merge(ctx, a->rle ? 1 : 0);
-  if (rc) { log << ctx->err << "\n"; cmsbwt_ctx_destroy(ctx); return rc; }
-  const cmsbwt_stats& s = e.stats;
-  log << "phrasesSet.size(): " << s.positions << "\n";
+  if (rc) return fail(rc);
+  if (!small) log << "phrasesSet.size(): " << s.positions << "\n";
   log << "headNumber: " << s.heads << "\n";
-  if (e.R.n < 1000000) log << "uniqueHeadNumber: " << s.keys << "\n";
+  if (small) log << "uniqueHeadNumber: " << s.keys << "\n";
   log << "ndoc: " << s.ndocs + 1 << "\n";
   log << "docBoundaries.size(): " << s.ndocs + 1 << "\n";
   log << "Time to compute matching statistics: " << (long long)(s.t_ms_walk_s * 1000) << " milliseconds\n";
-  log << "Rank: " << s.rank << "\n";
+  log << "Going to compute ranks for positions\n";
+  if (!small) log << "Rank: " << s.rank << "\n";
+  log << "libsais_int ran in " << (long long)s.t_libsais_int_ms << " milliseconds\n";
+  log << "First rankToHead: " << s.first_rank_to_head << "\n";
+  log << "Last rankToHead: " << s.last_rank_to_head << "\n";
+  log << "Done computing ranks for positions in " << (long long)s.t_ranks_ms << " milliseconds\n";
   log << "currentSum: " << s.current_sum << "\n";
+  log << "Going to compute counterSmallerThanHead for positions\n";
+  if (small) {  // FN:713-727: the -b buffer of the small path (unsigned int GB * 2^30, wrapping)
+    const uint32_t cap32 = a->buffer_gb * 1073741824u;
+    const double ram = e.sn < (uint64_t)cap32 ? (double)e.sn : (double)cap32;
+    log << "capOfBufferSuffixes = " << (uint64_t)(ram / 20.0 + 1) << "\n";
+  }
   log << "counterBad: " << s.counter_bad << "\n";
   log << "counterGood: " << s.counter_good << "\n";
   log << "counterDoNothing: " << s.counter_nothing << "\n";
-  log << "Done computing counterSmallerThanHead for positions in " << (long long)(s.t_merge_s * 1000)
+  log << "Done computing counterSmallerThanHead for positions in " << (long long)s.t_counter_ms
       << " milliseconds\n";
   log << "Inverted data in bucketsForExpandedBWT\n";
   rc = cmsbwt_write_output(ctx, out.c_str(), a->rle ? 1 : 0);
-  if (rc) { log << ctx->err << "\n"; cmsbwt_ctx_destroy(ctx); return rc; }
+  if (rc) return fail(rc);
   log << "MS-walk kernel: " << s.ms_walk_kernel_ms << " ms; collection pass: " << ms(t1, now()) << " ms\n";
+  log.flush();
   if (stats_out) *stats_out = e.stats;
   auto td0 = now();
   if (a->verbose) fprintf(stderr, "context %.3fs ", tCtx);

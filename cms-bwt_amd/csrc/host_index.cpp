@@ -90,12 +90,14 @@ void suffix_array_sais(const int32_t* s, int32_t* sa, int64_t n, int64_t k) {
   for (int64_t i = 0; i < n; i++) sa[i] = w[i + 1];
 }
 
-bool read_reference(const std::string& path, std::string& x, std::string& err) {
+bool read_reference(const std::string& path, std::string& x, std::string& err, uint64_t* file_bytes,
+                    uint64_t* read_size) {
   FILE* f = fopen(path.c_str(), "rb");
   if (!f) { err = "Error opening file of base sequence " + path; return false; }
   fseek(f, 0, SEEK_END);
   long sz = ftell(f);
   fseek(f, 0, SEEK_SET);
+  if (file_bytes) *file_bytes = sz > 0 ? (uint64_t)sz : 0;
   if (sz <= 0) { fclose(f); err = "Reference file is empty!"; return false; }
   std::string raw((size_t)sz, '\0');
   size_t got = fread(&raw[0], 1, (size_t)sz, f);
@@ -119,6 +121,7 @@ bool read_reference(const std::string& path, std::string& x, std::string& err) {
   } else {
     x.swap(raw);  // FN:190-199
   }
+  if (read_size) *read_size = x.size();
   // FN:208-213
   if (!x.empty() && (x.back() == '\n' || x.back() == '\r' || x.back() == 0)) x.pop_back();
   if (!x.empty() && x.back() == '$') x.pop_back();

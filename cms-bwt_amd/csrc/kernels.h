@@ -101,8 +101,10 @@ void launch_ix_place(const uint32_t* val, const uint32_t* slot, const uint32_t* 
                      uint32_t* rank, hipStream_t st);
 void launch_ix_keys(const uint32_t* act, uint32_t U, const int32_t* sa, const uint32_t* rank, uint32_t n, uint32_t h,
                     unsigned long long* key, uint32_t* val, hipStream_t st);
-void launch_ix_lcp(const uint8_t* x, const int32_t* sa, uint32_t n, uint32_t* isa, int32_t* phi, int32_t* plcpRaw,
-                   int32_t* lcp, uint8_t* bwt, int32_t* plcp, hipStream_t st);
+void launch_ix_isa(const int32_t* sa, uint32_t n, uint32_t* isa, int32_t* phi, hipStream_t st);
+void launch_ix_lcp(const uint8_t* x, const int32_t* sa, uint32_t n, const uint32_t* isa, const int32_t* phi,
+                   int32_t* plcpRaw, int32_t* lcp, int32_t* plcp, hipStream_t st);
+void launch_ix_bwt(const uint8_t* x, const int32_t* sa, uint32_t n, uint8_t* bwt, hipStream_t st);
 void launch_ix_plcp_check(const int32_t* plcp, uint32_t n, uint32_t* err, hipStream_t st);
 void launch_ix_level(const int32_t* prev, uint32_t prevLen, int32_t* cur, uint32_t curLen, hipStream_t st);
 void launch_ix_child(const uint8_t* x, const int32_t* sa, const int32_t* lcp, uint32_t n, uint32_t* ld,

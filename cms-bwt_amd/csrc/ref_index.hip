@@ -96,14 +96,21 @@ __global__ void k_ix_plcp(const uint8_t* __restrict__ x, uint32_t n, const int32
   }
 }
 
-// LCP[r] = PLCP[SA[r]] (LCP[n] = -1), BWT[r] = x[SA[r]-1] (0 at SA = 0)
-__global__ void k_ix_lcp_bwt(const uint8_t* __restrict__ x, const int32_t* __restrict__ sa, uint32_t n,
-                             const int32_t* __restrict__ plcp, int32_t* __restrict__ lcp, uint8_t* __restrict__ bwt) {
+// LCP[r] = PLCP[SA[r]] (LCP[n] = -1)
+__global__ void k_ix_lcp(const int32_t* __restrict__ sa, uint32_t n, const int32_t* __restrict__ plcp,
+                         int32_t* __restrict__ lcp) {
   const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
   if (r > n) return;
   if (r == n) { lcp[n] = -1; return; }
+  lcp[r] = plcp[sa[r]];
+}
+
+// FN:294-297: BWT[r] = x[SA[r]-1] (0 at SA = 0)
+__global__ void k_ix_bwt(const uint8_t* __restrict__ x, const int32_t* __restrict__ sa, uint32_t n,
+                         uint8_t* __restrict__ bwt) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
   const int32_t s = sa[r];
-  lcp[r] = plcp[s];
   bwt[r] = s > 0 ? x[s - 1] : 0;
 }
 
@@ -132,14 +139,21 @@ void launch_ix_keys(const uint32_t* act, uint32_t U, const int32_t* sa, const ui
                     unsigned long long* key, uint32_t* val, hipStream_t st) {
   if (U) hipLaunchKernelGGL(k_ix_keys, gidx(U), dim3(256), 0, st, act, U, sa, rank, n, h, key, val);
 }
-void launch_ix_lcp(const uint8_t* x, const int32_t* sa, uint32_t n, uint32_t* isa, int32_t* phi, int32_t* plcpRaw,
-                   int32_t* lcp, uint8_t* bwt, int32_t* plcp, hipStream_t st) {
+// FN:258-263 (ISA) with the Phi array of the PLCP pass
+void launch_ix_isa(const int32_t* sa, uint32_t n, uint32_t* isa, int32_t* phi, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_ix_isa_phi, gidx(n), dim3(256), 0, st, sa, n, isa, phi);
+}
+// FN:270-274: PLCP by Phi, LCP, then the max-neighbour PLCP
+void launch_ix_lcp(const uint8_t* x, const int32_t* sa, uint32_t n, const uint32_t* isa, const int32_t* phi,
+                   int32_t* plcpRaw, int32_t* lcp, int32_t* plcp, hipStream_t st) {
   if (!n) return;
-  hipLaunchKernelGGL(k_ix_isa_phi, gidx(n), dim3(256), 0, st, sa, n, isa, phi);
   const uint64_t chunks = ((uint64_t)n + kIdxChunk - 1) / kIdxChunk;
   hipLaunchKernelGGL(k_ix_plcp, gidx(chunks), dim3(256), 0, st, x, n, phi, plcpRaw);
-  hipLaunchKernelGGL(k_ix_lcp_bwt, gidx((uint64_t)n + 1), dim3(256), 0, st, x, sa, n, plcpRaw, lcp, bwt);
+  hipLaunchKernelGGL(k_ix_lcp, gidx((uint64_t)n + 1), dim3(256), 0, st, sa, n, plcpRaw, lcp);
   hipLaunchKernelGGL(k_ix_plcp_max, gidx(n), dim3(256), 0, st, isa, lcp, n, plcp);
+}
+void launch_ix_bwt(const uint8_t* x, const int32_t* sa, uint32_t n, uint8_t* bwt, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_ix_bwt, gidx(n), dim3(256), 0, st, x, sa, n, bwt);
 }
 }  // namespace cmsbwt
 

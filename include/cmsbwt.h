@@ -61,6 +61,16 @@ typedef struct cmsbwt_stats {
   uint64_t counter_work;     /* (item, offset) pairs visited by that kernel     */
   uint64_t order_invariant;  /* 1: every isaNext suffix starts with its head's   */
                              /* mismatch byte, comparator provably consistent   */
+  /* the rest of the reference's .log keys */
+  uint64_t ref_file_bytes;   /* `n = `              reference file size, FN:166 */
+  uint64_t ref_read_size;    /* `Reference (size = ` read, before trimming, FN:205 */
+  uint64_t coll_file_bytes;  /* `ftello(infile): `  collection file size, FN:222 */
+  uint64_t sn_initial;       /* `sn: ` / `_sx.len: ` min(file size, -p), FN:223 */
+  int64_t first_rank_to_head, last_rank_to_head;  /* FN:1476-1477 (-1: n/a)   */
+  double t_augment_ms, t_sa_ms, t_isa_ms, t_lcp_ms, t_rmq_ms, t_bwt_ms;  /* FN:240-299 */
+  double t_ranks_ms;         /* ranks .. next-head ranks, FN:1429-1498          */
+  double t_libsais_int_ms;   /* head-string suffix sort, FN:1455-1461           */
+  double t_counter_ms;       /* counterSmallerThanHead, FN:1517-1611            */
 } cmsbwt_stats;
 
 typedef struct cmsbwt_ctx cmsbwt_ctx;
@@ -77,7 +87,8 @@ void cmsbwt_ctx_destroy(cmsbwt_ctx* ctx);
 const char* cmsbwt_last_error(const cmsbwt_ctx* ctx);
 
 /* initialize_reference (FN:151-310): read FASTA/raw, trim (FN:208-213),
- * augment (FN:231-237), SA/ISA/LCP/PLCP/BWT on the host, stage into HBM. */
+ * augment (FN:231-237), then SA/ISA/LCP/PLCP/BWT and the walk tables built in
+ * HBM (ref_index.hip; CMSBWT_HOST_INDEX=1 builds them on the host instead). */
 int cmsbwt_load_reference_file(cmsbwt_ctx* ctx, const char* ref_path);
 /* Same from bytes already read and trimmed (no augmentation applied yet). */
 int cmsbwt_load_reference(cmsbwt_ctx* ctx, const uint8_t* ref, uint64_t len);

@@ -37,6 +37,36 @@ def test_cli_exists_and_prints_help(built):
     assert r.returncode == 255 and "Usage:" in r.stdout and "-r" in r.stdout
 
 
+def test_cli_argument_and_list_file_exit_codes(built, tmp_path):
+    """main.cpp:27-115, before any device work: -h, an unknown option and a
+    wrong argument count exit(-1) (255); a missing list file, an empty first
+    line and an empty (or blank) second line exit(1)."""
+    import subprocess
+    cli = os.path.join(ROOT, "cms-bwt_amd", "build", "cmsbwt")
+
+    def run(*a):
+        return subprocess.run([cli, *a], capture_output=True, text=True, timeout=60)
+    assert run("-h").returncode == 255
+    r = run("-z", "x.list")
+    assert r.returncode == 255 and "Unknown option" in r.stdout
+    r = run()
+    assert r.returncode == 255 and "Invalid number of arguments" in r.stdout
+    assert run("a.list", "b.list").returncode == 255
+    r = run(str(tmp_path / "missing.list"))
+    assert r.returncode == 1 and "Error opening file" in r.stderr
+    for body, msg in ((b"\nb.fa\n", "first line"), (b"a.fa\n\n", "second line"), (b"a.fa\n  \t\n", "second line"),
+                      (b"a.fa\n", "second line")):
+        p = tmp_path / "l.list"
+        p.write_bytes(body)
+        r = run("-r", str(p))
+        assert r.returncode == 1 and msg in r.stderr, (body, r.stderr)
+    # echo of the command line and parameters (main.cpp:31-34, 74-80)
+    p.write_bytes(b"\nb\n")
+    r = run("-p", "123", "-b", "4", "-o", "base", str(p))
+    assert "==== Command line:" in r.stdout and "Prefix length: 123" in r.stdout
+    assert "Buffer size: 4 GB" in r.stdout and "Output basename: base" in r.stdout and "FULL" in r.stdout
+
+
 # Reader quirks, each restated from the reference line that causes it.  The
 # committed small goldens are oracle outputs (parity with the reference itself
 # is unpinned for them); these are the line-by-line cross-checks.
