@@ -121,8 +121,9 @@ def load_library() -> ctypes.CDLL:
                                               ctypes.POINTER(U64), ctypes.POINTER(U64)]),
         "cmsbwt_host_suffix_array": (I32, [VP, U64, VP]),
         "cmsbwt_walk_import": (I32, [P, U64, U64, U64, ctypes.c_uint32, ctypes.POINTER(ctypes.c_void_p)]),
+        "cmsbwt_selftest": (I32, [P, ctypes.c_char_p, U64, U64, I32, ctypes.POINTER(U64)]),
         # position-sharded merge (device pointers; cmsbwt.dist drives the transport)
-        "cmsbwt_dm_begin": (I32, [P, ctypes.c_uint32, ctypes.c_uint32, U64, U64, ctypes.c_uint32, VP, VP, I32]),
+        "cmsbwt_dm_begin": (I32, [P, ctypes.c_uint32, ctypes.c_uint32, U64, U64, ctypes.c_uint32, I32]),
         "cmsbwt_dm_route_heads": (I32, [P, VP]),
         "cmsbwt_dm_pack_heads": (I32, [P, VP]),
         "cmsbwt_dm_group": (I32, [P, VP, U64, VP]),
@@ -156,6 +157,7 @@ EXPORTED = [
     "cmsbwt_load_collection", "cmsbwt_load_collection_synth", "cmsbwt_ms_walk", "cmsbwt_merge",
     "cmsbwt_step", "cmsbwt_get_stats", "cmsbwt_num_runs", "cmsbwt_copy_runs", "cmsbwt_write_output",
     "cmsbwt_copy_array", "cmsbwt_host_read_collection", "cmsbwt_host_suffix_array", "cmsbwt_walk_import",
+    "cmsbwt_selftest",
     "cmsbwt_dm_begin", "cmsbwt_dm_route_heads", "cmsbwt_dm_pack_heads", "cmsbwt_dm_group", "cmsbwt_dm_labels",
     "cmsbwt_dm_dbl_init", "cmsbwt_dm_dbl_route", "cmsbwt_dm_dbl_pack", "cmsbwt_dm_dbl_sort", "cmsbwt_dm_dbl_apply",
     "cmsbwt_dm_pack_ranks", "cmsbwt_dm_load_ranks", "cmsbwt_dm_route_halo", "cmsbwt_dm_pack_halo",
@@ -294,10 +296,9 @@ class Engine:
     def _u64s(self, k):
         return (ctypes.c_uint64 * k)()
 
-    def dm_begin(self, world, rank, heads_total, docs_total, order_invariant, diff_ptr, hashead_ptr, rle=True):
+    def dm_begin(self, world, rank, heads_total, docs_total, order_invariant, rle=True):
         self._chk(self._lib.cmsbwt_dm_begin(self._ctx, world, rank, heads_total, docs_total,
-                                            1 if order_invariant else 0, ctypes.c_void_p(diff_ptr),
-                                            ctypes.c_void_p(hashead_ptr), 1 if rle else 0))
+                                            1 if order_invariant else 0, 1 if rle else 0))
 
     def dm_route_heads(self, world):
         c = self._u64s(world)
@@ -374,6 +375,13 @@ class Engine:
         cn = (ctypes.c_uint64 * k)(*counts)
         gs = (ctypes.c_uint64 * len(gstats))(*gstats)
         self._chk(self._lib.cmsbwt_dm_finish(self._ctx, sp, cp, cn, gs))
+
+    def selftest(self, what: str, n: int, offset: int = 0, inplace: bool = False) -> int:
+        """Mismatches of a device primitive against its host result (0 = equal)."""
+        bad = ctypes.c_uint64()
+        self._chk(self._lib.cmsbwt_selftest(self._ctx, what.encode(), n, offset, 1 if inplace else 0,
+                                            ctypes.byref(bad)))
+        return bad.value
 
     def write_output(self, outname: str, rle: bool = True):
         self._chk(self._lib.cmsbwt_write_output(self._ctx, outname.encode(), 1 if rle else 0))

@@ -202,15 +202,7 @@ def sharded_merge(eng, x: Transport, rle: bool = True):
     chars = sum(m[2] for m in meta)
     inv = all(m[3] for m in meta)
     i32, i64 = torch.int32, torch.int64
-    diff = x.empty(n + 1, i32)
-    hh = x.empty(n, torch.uint8)
-    x.sync()
-    eng.array_into("diff", diff.data_ptr())
-    eng.array_into("hashead", hh.data_ptr())
-    x.allreduce(diff, "sum")
-    x.allreduce(hh, "max")
-    eng.dm_begin(world, rank, Htot, E, inv, diff.data_ptr(), hh.data_ptr(), rle)
-    del diff, hh
+    eng.dm_begin(world, rank, Htot, E, inv, rle)
     # 1-2. heads to position owners; items; initial group labels
     hc = eng.dm_route_heads(world)
     send = x.empty((H, 5), i32)
@@ -219,7 +211,8 @@ def sharded_merge(eng, x: Transport, rle: bool = True):
     recv = x.a2a(send, hc, rc)
     del send
     Hp = sum(rc)
-    sa = x.empty(2 * n, i32)
+    # per-SA-rank item / head counts and the run difference array, one all-reduce
+    sa = x.empty(3 * n + 1, i32)
     eng.dm_group(recv.data_ptr(), Hp, sa.data_ptr())
     del recv
     x.allreduce(sa, "sum")

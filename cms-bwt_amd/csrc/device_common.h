@@ -7,12 +7,9 @@ namespace cmsbwt {
 
 constexpr int kMaxLevels = 6;   // block-minima levels over LCP (64^6 > 2^32)
 constexpr uint32_t kPoolB = 16; // head records per pool block
-#ifndef CMSBWT_POOL_BATCH
-#define CMSBWT_POOL_BATCH 16
-#endif
 // pool blocks a lane of the uniform-step walk reserves per atomic (it keeps
 // unused ones for its next chunk; blocks never started keep blkChunk = ~0)
-constexpr uint32_t kPoolBatch = CMSBWT_POOL_BATCH;
+constexpr uint32_t kPoolBatch = 16;
 constexpr uint8_t kSep = 2;     // CMS-BWT.h:28
 // Readable tail after x and after the collection text: the cooperative LCE
 // of the walk reads up to 4 KiB past its current position.
@@ -91,7 +88,7 @@ struct HeadRec {
   uint32_t start;   // doc-local position
   uint32_t pos;     // reference position of the match
   uint32_t len;     // match length
-  uint32_t flags;   // bit 0 smaller, bits 8..15 char before the head (listOfChars)
+  uint32_t flags;   // bit 0 smaller (the head's BWT character is read by k_finalize)
 };
 
 struct Pool {

@@ -194,15 +194,21 @@ __global__ void k_dm_pack_ranks(const uint32_t* __restrict__ perm, const uint32_
 __global__ void k_dm_load_ranks(const int32_t* __restrict__ in, const uint32_t* __restrict__ Pm,
                                 const uint32_t* __restrict__ itemOfSlot, const ItemsSoA it,
                                 const uint32_t* __restrict__ gItem, const uint8_t* __restrict__ lchar, uint32_t H,
-                                uint32_t* __restrict__ nhr, uint8_t* __restrict__ bwtSlot, uint32_t* __restrict__ err) {
+                                uint8_t* __restrict__ bwtSlot, uint32_t* __restrict__ err) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= H) return;
   const uint32_t r = Pm[s], q = itemOfSlot[s];
   const uint32_t hr = (uint32_t)in[2 * r];
-  nhr[s] = (uint32_t)in[2 * r + 1];
   const uint32_t k = hr - (gItem[q] - 1);
   if (k < it.count[q]) bwtSlot[it.slot[q] + k] = lchar[r];
   else atomicOr(err, 4u);
+}
+
+// next-head rank of every received head, in received order (k_nhr_rank
+// ranks them inside their items through Pm)
+__global__ void k_dm_nbi(const int32_t* __restrict__ in, uint32_t H, uint32_t* __restrict__ nbi) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r < H) nbi[r] = (uint32_t)in[2 * r + 1];
 }
 
 // ---- halo: items reaching past this rank's last position into later ranks
@@ -372,11 +378,11 @@ void mk_dm_pack_ranks(const uint32_t* perm, const uint32_t* grp, const uint16_t*
   if (n) hipLaunchKernelGGL(k_dm_pack_ranks, g1d(n), dim3(256), 0, st, perm, grp, nexthead, n, H, out, err);
 }
 void mk_dm_load_ranks(const int32_t* in, const uint32_t* Pm, const uint32_t* itemOfSlot, const ItemsSoA& it,
-                      const uint32_t* gItem, const uint8_t* lchar, uint32_t H, uint32_t* nhr, uint8_t* bwtSlot,
+                      const uint32_t* gItem, const uint8_t* lchar, uint32_t H, uint32_t* nbi, uint8_t* bwtSlot,
                       uint32_t* err, hipStream_t st) {
-  if (H)
-    hipLaunchKernelGGL(k_dm_load_ranks, g1d(H), dim3(256), 0, st, in, Pm, itemOfSlot, it, gItem, lchar, H, nhr,
-                       bwtSlot, err);
+  if (!H) return;
+  hipLaunchKernelGGL(k_dm_load_ranks, g1d(H), dim3(256), 0, st, in, Pm, itemOfSlot, it, gItem, lchar, H, bwtSlot, err);
+  hipLaunchKernelGGL(k_dm_nbi, g1d(H), dim3(256), 0, st, in, H, nbi);
 }
 void mk_dm_halo_count(const ItemsSoA& it, uint32_t K, const uint32_t* split, uint32_t world, uint32_t rank,
                       uint32_t n, uint32_t* c, hipStream_t st) {

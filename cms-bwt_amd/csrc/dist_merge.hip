@@ -38,6 +38,11 @@ void Engine::partition(const uint32_t* dest, uint64_t cnt, DBuf<uint32_t>& perm,
   perm.alloc(cnt);
   if (!cnt) return;
   if (cnt >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "partition larger than 2^32"};
+  if (world == 1) {  // one destination: send order = input order
+    mk_iota(perm.p, cnt, st);
+    counts[0] = cnt;
+    return;
+  }
   DBuf<uint32_t> io, k2, bnd;
   io.alloc(cnt); k2.alloc(cnt); bnd.alloc((uint64_t)world + 1);
   mk_iota(io.p, cnt, st);
@@ -56,13 +61,12 @@ void Engine::dm_check_err(const char* where) {
 }
 
 void Engine::dm_begin(uint32_t world, uint32_t rank, uint64_t heads_total, uint64_t docs_total, uint32_t flags,
-                      const int32_t* diffAll, const uint8_t* hashead, int rle) {
+                      int rle) {
   if (!walked) throw InputError{CMSBWT_EARG, "run ms_walk first"};
   if (world < 1 || world > 64 || rank >= world) throw InputError{CMSBWT_EARG, "bad world/rank"};
   if (heads_total >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^31-1 heads (int32 ranks, FN:1436)"};
   if (heads_total == 0)  // as Engine::merge: FN:1359-1385 is undefined without heads
     throw InputError{CMSBWT_EINPUT, "collection has no documents (reference behaviour undefined, FN:1359-1385)"};
-  if (!diffAll || !hashead) throw InputError{CMSBWT_EARG, "reduced diff/hashead arrays required"};
   const uint32_t n = R.n;
   merged = false;
   dm.on = false;
@@ -87,11 +91,6 @@ void Engine::dm_begin(uint32_t world, uint32_t rank, uint64_t heads_total, uint6
   HIPCHK(hipMemcpyAsync(dm.dGsplit.p, dm.Gsplit.data(), (world + 1) * 4, hipMemcpyHostToDevice, st));
   dm.err.alloc(1);
   dm.err.zero(st);
-  // the summed difference array and OR-ed head flags of all ranks
-  diff.alloc((uint64_t)n + 1);
-  hasHead.alloc(n);
-  HIPCHK(hipMemcpyAsync(diff.p, diffAll, ((uint64_t)n + 1) * 4, hipMemcpyDefault, st));
-  HIPCHK(hipMemcpyAsync(hasHead.p, hashead, n, hipMemcpyDefault, st));
   sync();
 }
 
@@ -120,7 +119,13 @@ void Engine::dm_group(const int32_t* recv, uint64_t nrecv, uint32_t* saCounts) {
   dm.rSm.alloc(Hp); dm.rCh.alloc(Hp);
   HeadsSoA r{nullptr, dm.rPos.p, dm.rLen.p, dm.rSm.p, dm.rCh.p, dm.rIsa.p, dm.rTon.p, nullptr};
   mk_dm_unpack_heads(recv, Hp, r, st);
+  // run buckets (FN:1162-1171) of the heads at the owned positions, from the
+  // grouping's position sort: head flags of the owned positions are final,
+  // the difference array is summed over ranks (a run may end in a later
+  // range) with the per-SA-rank counts, in saCounts[2n .. 3n]
+  runsValid = false;
   group_items(r, Hp, n, dm.IS);
+  if (!runsValid) throw InputError{CMSBWT_EINTERNAL, "internal: run buckets not built by the grouping"};
   const uint32_t K = dm.IS.K;
   ItemsSoA S = dm.IS.soa();
   dm.viol = 0;
@@ -144,12 +149,15 @@ void Engine::dm_group(const int32_t* recv, uint64_t nrecv, uint32_t* saCounts) {
   }
   const bool ownsEnd = dm.P0 <= n - 1 && n - 1 < dm.P1;
   mk_dm_sa_counts(dsa.p, dm.IS.posBegin.p, S.slot, n, ownsEnd ? dm.E : 0, saCounts, st);
+  HIPCHK(hipMemcpyAsync(saCounts + 2ull * n, diff.p, ((uint64_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipGetLastError());
   sync();
 }
 
 void Engine::dm_labels(const uint32_t* saCounts, uint32_t* back) {
   const uint32_t n = R.n;
+  // the difference array summed over ranks (head flags stay this rank's)
+  HIPCHK(hipMemcpyAsync(diff.p, saCounts + 2ull * n, ((uint64_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
   dm.headBase.alloc(n);
   exscan(saCounts + n, dm.headBase.p, 0u, n);
   dm.gItem.alloc(std::max<uint32_t>(dm.IS.K, 1));
@@ -236,8 +244,17 @@ void Engine::dm_load_ranks(const int32_t* recv) {
   dm.nhr.alloc(std::max<uint32_t>(Hp, 1));
   dm.bwtSlot.alloc(std::max<uint32_t>(Hp, 1));  // never null: selects the sharded writer
   ItemsSoA S = dm.IS.soa();
-  mk_dm_load_ranks(recv, dm.Pm.p, dm.itemOfSlot.p, S, dm.gItem.p, dm.rCh.p, Hp, dm.nhr.p, dm.bwtSlot.p, dm.err.p, st);
-  if (Hp) sort_nhr_items(S, dm.IS.K, dm.itemOfSlot.p, dm.nhr.p, Hp);
+  {
+    // FN:1480-1494: next-head ranks sorted per item, as on one GPU (ranked
+    // inside small items through Pm, large items by one sort)
+    DBuf<uint32_t> nbi;
+    nbi.alloc(std::max<uint32_t>(Hp, 1));
+    mk_dm_load_ranks(recv, dm.Pm.p, dm.itemOfSlot.p, S, dm.gItem.p, dm.rCh.p, Hp, nbi.p, dm.bwtSlot.p, dm.err.p, st);
+    if (Hp) {
+      mk_nhr_rank(dm.Pm.p, nbi.p, dm.itemOfSlot.p, Hp, dm.nhr.p, st);
+      sort_nhr_items(S, dm.IS.K, dm.itemOfSlot.p, dm.nhr.p, Hp, true);
+    }
+  }
   HIPCHK(hipGetLastError());
   sync();
   dm_check_err("head characters");
@@ -335,16 +352,9 @@ void Engine::dm_counter(const int32_t* hdr, uint64_t nh, const int32_t* words, u
   stats.counter_kernel_ms = counter_kernel_ms;
 }
 
-// ---- 6. writer
-WriterIn Engine::dm_writer_in() {
-  WriterIn wi{dsa.p, dbwt.p, dm.bucket.p, dm.IS.posBegin.p, dm.IS.slot.p, dm.IS.count.p, nullptr, nullptr,
-              dm.counter.p, R.n, dm.E, dm.rle};
-  wi.bwtSlot = dm.bwtSlot.p;
-  wi.P0 = dm.P0;
-  wi.P1 = dm.P1;
-  return wi;
-}
-
+// ---- 6. writer: the element writer of one GPU over the SA ranks of the
+// owned positions (one thread per end phrase / head / head-less rank);
+// elements summarised per writer unit for the all-reduce
 void Engine::dm_units(int64_t* out) {
   const uint32_t n = R.n;
   if ((uint64_t)dm.E + n - 1 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer units"};
@@ -356,26 +366,59 @@ void Engine::dm_units(int64_t* out) {
     inscan(diff.p, cnt.p, n, rocprim::plus<int32_t>());
     mk_bucket(cnt.p, hasHead.p, n, dm.bucket.p, st);
   }
-  const WriterIn wi = dm_writer_in();
-  DBuf<uint32_t> r, hl;
+  ItemSet& IS = dm.IS;
+  DBuf<uint32_t> m;
+  m.alloc(n);
+  dm.eBase.alloc(n);
+  mk_dm_el_count(dsa.p, IS.posBegin.p, IS.slot.p, n, dm.E, dm.P0, dm.P1, m.p, st);
+  exscan(m.p, dm.eBase.p, 0u, n);
+  const uint64_t V64 = (uint64_t)read1(dm.eBase.p + (n - 1)) + read1(m.p + (n - 1));
+  if (V64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer elements"};
+  const uint32_t V = dm.V = (uint32_t)V64;
+  dm.rOf.alloc(std::max<uint32_t>(V, 1));
+  mk_el_rof(dm.eBase.p, m.p, n, dm.rOf.p, st);
+  const uint32_t Hp = dm.Hp;
+  dm.cum.alloc(std::max<uint32_t>(Hp, 1));
+  if (Hp)
+    inscan(rocprim::make_transform_iterator(dm.counter.p, PlusOneU64()), dm.cum.p, Hp,
+           rocprim::plus<unsigned long long>());
+  dm.info1.alloc(n);
+  dm.info2.alloc(n);
+  const ElemIn ei = dm_elem_in();
+  mk_dm_el_info(ei, dm.P0, dm.P1, st);
+  DBuf<uint32_t> runs, adj;
   DBuf<unsigned long long> sym;
-  r.alloc(Uw); hl.alloc(Uw); sym.alloc(Uw);
-  mk_wr_count(wi, Uw, r.p, sym.p, hl.p, st);
-  mk_dm_units_pack(r.p, hl.p, sym.p, Uw, out, st);
+  runs.alloc(std::max<uint32_t>(V, 1)); adj.alloc(std::max<uint32_t>(V, 1)); sym.alloc(std::max<uint32_t>(V, 1));
+  dm.ehl.alloc(std::max<uint32_t>(V, 1));
+  dm.runIn.alloc(std::max<uint32_t>(V, 1));
+  dm.symIn.alloc(std::max<uint32_t>(V, 1));
+  if (V) {
+    mk_el_wr_count(ei, V, runs.p, sym.p, dm.ehl.p, st);
+    mk_dm_el_adj(dm.rOf.p, dm.ehl.p, runs.p, V, adj.p, st);
+    inscan(rocprim::make_transform_iterator(adj.p, WidenU64()), dm.runIn.p, V, rocprim::plus<unsigned long long>());
+    inscan(sym.p, dm.symIn.p, V, rocprim::plus<unsigned long long>());
+  }
+  mk_dm_el_units(dm.eBase.p, m.p, dm.runIn.p, dm.symIn.p, dm.ehl.p, n, dm.E, Uw, out, st);
   HIPCHK(hipGetLastError());
   sync();
 }
 
+ElemIn Engine::dm_elem_in() {
+  ElemIn ei{dsa.p, dbwt.p, dm.bucket.p, dm.IS.posBegin.p, dm.IS.slot.p, dm.itemOfSlot.p, nullptr, dm.eBase.p,
+            dm.rOf.p, nullptr, dm.counter.p, dm.cum.p, dm.info1.p, dm.info2.p, R.n, dm.E, dm.Hp, dm.rle};
+  ei.bwtSlot = dm.bwtSlot.p;
+  return ei;
+}
+
 uint64_t Engine::dm_emit(const int64_t* unitsAll) {
   const uint32_t n = R.n, Uw = dm.Uw;
-  DBuf<uint32_t> hl, prev;
   DBuf<unsigned long long> sym, own, srcOff;
-  dm.uruns.alloc(Uw); hl.alloc(Uw); sym.alloc(Uw); prev.alloc(Uw);
-  mk_dm_units_unpack(unitsAll, Uw, dm.uruns.p, hl.p, sym.p, st);
+  dm.uruns.alloc(Uw); dm.uhl.alloc(Uw); sym.alloc(Uw); dm.uprev.alloc(Uw);
+  mk_dm_units_unpack(unitsAll, Uw, dm.uruns.p, dm.uhl.p, sym.p, st);
   // a unit's first segment continues the previous non-empty unit's run when
   // the characters match (global over all ranks' units)
-  exscan(hl.p, prev.p, 0u, Uw, LastNonEmpty());
-  mk_wr_adjust(hl.p, prev.p, Uw, dm.uruns.p, st);
+  exscan(dm.uhl.p, dm.uprev.p, 0u, Uw, LastNonEmpty());
+  mk_wr_adjust(dm.uhl.p, dm.uprev.p, Uw, dm.uruns.p, st);
   dm.runOff.alloc(Uw);
   dm.symOff.alloc(Uw);
   auto runs64 = rocprim::make_transform_iterator(dm.uruns.p, WidenU64());
@@ -383,15 +426,26 @@ uint64_t Engine::dm_emit(const int64_t* unitsAll) {
   exscan(sym.p, dm.symOff.p, 0ull, Uw);
   dm.Rn = read1(dm.runOff.p + (Uw - 1)) + read1(dm.uruns.p + (Uw - 1));
   dm.symbols = read1(dm.symOff.p + (Uw - 1)) + read1(sym.p + (Uw - 1));
-  // this rank's runs, its units in unit order
-  own.alloc(Uw);
-  srcOff.alloc(Uw);
-  mk_dm_own_runs(dm.uruns.p, Uw, dsa.p, dm.E, n, dm.P0, dm.P1, own.p, st);
-  exscan(own.p, srcOff.p, 0ull, Uw);
-  dm.Rloc = read1(srcOff.p + (Uw - 1)) + read1(own.p + (Uw - 1));
-  dm.locStart.alloc(std::max<uint64_t>(dm.Rloc, 1));
-  dm.locChar.alloc(std::max<uint64_t>(dm.Rloc, 1));
-  mk_wr_emit(dm_writer_in(), Uw, srcOff.p, dm.symOff.p, prev.p, dm.locStart.p, dm.locChar.p, st);
+  const ElemIn ei = dm_elem_in();
+  if (dm.rank == 0) {
+    // rank 0 holds the output: its own runs go straight to their global indices
+    dm.gStart.alloc(std::max<uint64_t>(dm.Rn, 1));
+    dm.gChar.alloc(std::max<uint64_t>(dm.Rn, 1));
+    mk_dm_el_emit(ei, dm.V, dm.runIn.p, dm.symIn.p, dm.runOff.p, dm.symOff.p, dm.uprev.p, dm.uhl.p, dm.ehl.p,
+                  dm.gStart.p, dm.gChar.p, st);
+    dm.Rloc = 0;
+  } else {
+    // this rank's runs, its units in unit order (rank 0 places them)
+    own.alloc(Uw);
+    srcOff.alloc(Uw);
+    mk_dm_own_runs(dm.uruns.p, Uw, dsa.p, dm.E, n, dm.P0, dm.P1, own.p, st);
+    exscan(own.p, srcOff.p, 0ull, Uw);
+    dm.Rloc = read1(srcOff.p + (Uw - 1)) + read1(own.p + (Uw - 1));
+    dm.locStart.alloc(std::max<uint64_t>(dm.Rloc, 1));
+    dm.locChar.alloc(std::max<uint64_t>(dm.Rloc, 1));
+    mk_dm_el_emit(ei, dm.V, dm.runIn.p, dm.symIn.p, srcOff.p, dm.symOff.p, dm.uprev.p, dm.uhl.p, dm.ehl.p,
+                  dm.locStart.p, dm.locChar.p, st);
+  }
   HIPCHK(hipGetLastError());
   sync();
   return dm.Rloc;
@@ -405,31 +459,30 @@ void Engine::dm_copy_stream(unsigned long long* start, uint8_t* chars) {
   sync();
 }
 
-// rank 0: every rank's runs at their global run indices, then the records
+// rank 0: the other ranks' runs at their global run indices (its own are
+// there already), then the records
 void Engine::dm_finish(const unsigned long long* const* starts, const uint8_t* const* chars, const uint64_t* counts,
                        const uint64_t* gstats) {
+  if (dm.rank != 0) throw InputError{CMSBWT_EARG, "dm_finish runs on rank 0"};
   const uint32_t n = R.n, Uw = dm.Uw, world = dm.world;
   const uint64_t Rn = dm.Rn;
-  DBuf<unsigned long long> runStart, own, srcOff;
-  DBuf<uint8_t> runChar;
-  runStart.alloc(std::max<uint64_t>(Rn, 1));
-  runChar.alloc(std::max<uint64_t>(Rn, 1));
+  DBuf<unsigned long long> own, srcOff;
   own.alloc(Uw);
   srcOff.alloc(Uw);
-  uint64_t placed = 0;
   for (uint32_t k = 0; k < world; k++) {
-    if (!counts[k]) continue;
+    if (k == dm.rank) continue;
     mk_dm_own_runs(dm.uruns.p, Uw, dsa.p, dm.E, n, dm.Psplit[k], dm.Psplit[k + 1], own.p, st);
     exscan(own.p, srcOff.p, 0ull, Uw);
     const uint64_t rk = read1(srcOff.p + (Uw - 1)) + read1(own.p + (Uw - 1));
     if (rk != counts[k]) throw InputError{CMSBWT_EINPUT, "internal: rank " + std::to_string(k) + " sent " +
                                                              std::to_string(counts[k]) + " runs, expected " +
                                                              std::to_string(rk)};
-    mk_dm_place(dm.uruns.p, dm.runOff.p, srcOff.p, Uw, dsa.p, dm.E, n, dm.Psplit[k], dm.Psplit[k + 1], starts[k],
-                chars[k], runStart.p, runChar.p, st);
-    placed += rk;
+    if (rk)
+      mk_dm_place(dm.uruns.p, dm.runOff.p, srcOff.p, Uw, dsa.p, dm.E, n, dm.Psplit[k], dm.Psplit[k + 1], starts[k],
+                  chars[k], dm.gStart.p, dm.gChar.p, st);
   }
-  if (placed != Rn) throw InputError{CMSBWT_EINPUT, "internal: runs placed do not cover the output"};
+  DBuf<unsigned long long>& runStart = dm.gStart;
+  DBuf<uint8_t>& runChar = dm.gChar;
   runs.alloc(Rn * 9);
   mk_wr_records(runStart.p, runChar.p, Rn, dm.symbols, runs.p, st);
   HIPCHK(hipGetLastError());

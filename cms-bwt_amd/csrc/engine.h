@@ -314,10 +314,7 @@ struct Engine {
     HIPCHK(rocprim::exclusive_scan(scratch(b), b, sums.p, off.p, 0u, (size_t)nt, rocprim::plus<uint32_t>(), st));
     mk_scan_tiles(in, out, n, off.p, init, inclusive, st);
   }
-  static bool rocprim_scan() {
-    static const bool v = env_u32("CMSBWT_ROCPRIM_SCAN", 0) != 0;
-    return v;
-  }
+  static bool rocprim_scan() { return env_u32("CMSBWT_ROCPRIM_SCAN", 0) != 0; }
   template <class In, class Out, class Init>
   void exscan(In in, Out out, Init init, uint64_t n) {
     if (!n) return;
@@ -371,8 +368,10 @@ struct Engine {
     HIPCHK(rocprim::reduce(scratch(b), b, in, out.p, 0u, (size_t)n, rocprim::maximum<uint32_t>(), st));
     return read1(out.p);
   }
+  // order-preserving compaction; `out` must not alias `in` (both paths)
   uint32_t select_flagged(const uint32_t* in, const uint32_t* flags, uint32_t* out, uint32_t n) {
     if (!n) return 0;
+    if ((const void*)in == (const void*)out) throw InputError{CMSBWT_EINTERNAL, "internal: select_flagged in place"};
     if (!env_u32("CMSBWT_ROCPRIM_SELECT", 0)) {  // two-pass tile compaction (merge.hip)
       const uint32_t nt = sel_tiles(n);
       DBuf<uint32_t> tc, to;
@@ -521,13 +520,10 @@ struct Engine {
     mark("lcp+levels");
     build_prefix_tables(true);
     mark("pfx");
-    R.ld = nullptr;
-    if (env_u32("CMSBWT_EXT8", 1)) {
-      dld.alloc((uint64_t)n + 16);
-      dld.zero(st);
-      launch_ix_child(dx.p, dsa.p, dlcp.p, n, dld.p, st);
-      R.ld = dld.p;
-    }
+    dld.alloc((uint64_t)n + 16);
+    dld.zero(st);
+    launch_ix_child(dx.p, dsa.p, dlcp.p, n, dld.p, st);
+    R.ld = dld.p;
     mark("child");
     dpr.alloc((uint64_t)n + 16);
     dir.alloc((uint64_t)n + 16);
@@ -806,8 +802,6 @@ struct Engine {
   // character of computeMSFactorAt over a small interval needs one window of
   // ld instead of two binary searches (FN:94-149).
   void build_child_table() {
-    R.ld = nullptr;
-    if (!env_u32("CMSBWT_EXT8", 1)) return;
     const uint32_t n = hix.n;
     std::vector<uint32_t> ld((size_t)n + 16, 0);
     auto chr = [&](uint32_t k, int32_t l) -> uint32_t {
@@ -1073,31 +1067,29 @@ struct Engine {
   }
 
   // =====================================================================
-  // MS walk + head finalisation
-  // CMSBWT_WALK=1 selects the per-lane walk (k_ms_walk); default is the
-  // uniform-step walk (k_ms_walk2) over a chunk queue.
-  static bool walk_v1() { return env_u32("CMSBWT_WALK", 2) == 1; }
-  static uint32_t walk_lanes() { return std::max<uint32_t>(256, env_u32("CMSBWT_WALK_LANES", 256u * 32 * 64)); }
+  // MS walk (k_ms_walk2, a uniform-step walk over a chunk queue) + head
+  // finalisation
+  // lanes of the walk launch: at most 2048 blocks of 256 (chunks are pulled
+  // from queues, so lanes beyond the chunk count would idle)
+  static constexpr uint32_t kWalkLanes = 256u * 32 * 64;
+  // lanes resident at CMSBWT_W2_WAVES waves per SIMD (Makefile: 4)
+  static uint64_t resident_lanes() {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess) {
+      int v = 0;
+      if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
+    }
+    return (uint64_t)cus * 4 * 4 * 64;
+  }
 
   uint32_t chunk_size() const {
     if (const char* e = getenv("CMSBWT_CHUNK")) return (uint32_t)std::max(64L, atol(e));
-    if (!walk_v1()) {
-      // queue-fed: about 1.5 chunks per resident lane (CUs x 4 SIMDs x 4 waves
-      // x 64; restarts cost, a long last round of chunks costs too).  Config 3
-      // (10 GB, 256 CUs): 16 K 16.6 ms, 20 K 16.3, 22-26 K 15.6-15.8, 28 K
-      // 16.2, 32 K 16.5, 48 K 18.5 (walk kernel).
-      int dev = 0, cus = 256;
-      if (hipGetDevice(&dev) == hipSuccess) {
-        int v = 0;
-        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0) cus = v;
-      }
-      const uint64_t resident = (uint64_t)cus * 4 * 4 * 64;
-      uint64_t c = chars * 2 / (3 * resident);
-      return (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(32768, c));
-    }
-    uint64_t c = chars / (256ull * 64 * 64);
-    c = std::max<uint64_t>(2048, std::min<uint64_t>(32768, c));
-    return (uint32_t)c;
+    // queue-fed: about 1.5 chunks per resident lane (CUs x 4 SIMDs x 4 waves
+    // x 64; restarts cost, a long last round of chunks costs too).  Config 3
+    // (10 GB, 256 CUs): 16 K 16.6 ms, 20 K 16.3, 22-26 K 15.6-15.8, 28 K
+    // 16.2, 32 K 16.5, 48 K 18.5 (walk kernel).
+    uint64_t c = chars * 2 / (3 * resident_lanes());
+    return (uint32_t)std::max<uint64_t>(1024, std::min<uint64_t>(32768, c));
   }
 
   void ms_walk() {
@@ -1137,9 +1129,8 @@ struct Engine {
     chunkCount.alloc(nch);
     used.alloc(1);
     nextChunk.alloc(16 * 8);
-    const bool v1 = walk_v1();
     DBuf<unsigned long long> w2stats;  // CMSBWT_W2_STATS=1: step counts of the uniform-step walk
-    if (!v1 && env_u32("CMSBWT_W2_STATS", 0)) {
+    if (env_u32("CMSBWT_W2_STATS", 0)) {
       w2stats.alloc(32);
       w2stats.zero(st);
     }
@@ -1147,8 +1138,10 @@ struct Engine {
     // (3 % at first) + one partial block per chunk; an overflow re-runs the
     // walk with the measured size, so only the first walk of a denser
     // workload pays twice (1 % SNP collections have ~10 % heads)
-    if (!densityLearned && !v1 && nch >= 4096) sample_density(nch);
-    const uint64_t slack = v1 ? 0 : (uint64_t)std::min<uint32_t>(walk_lanes(), nch) * (kPoolBatch - 1);
+    if (!densityLearned && nch >= 4096) sample_density(nch);
+    // every launched lane may end holding kPoolBatch - 1 reserved blocks it
+    // never started (config 3: 393 K lanes x 15 x 256 B = 1.5 GB)
+    const uint64_t slack = (uint64_t)std::min<uint32_t>(kWalkLanes, nch) * (kPoolBatch - 1);
     uint64_t cap = (uint64_t)nch + slack + (uint64_t)((double)chars * poolDensity * 1.1) / kPoolB + 1024;
     DBuf<HeadRec> rec;
     DBuf<uint32_t> blkChunk, blkSeq;
@@ -1163,9 +1156,8 @@ struct Engine {
       HIPCHK(hipMemsetAsync(blkChunk.p, 0xff, cap * 4, st));
       Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
       HIPCHK(hipEventRecord(ev0, st));
-      if (v1) launch_ms_walk(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.laneChunk.p, pool, chunkCount.p, st);
-      else launch_ms_walk2(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.bandOrder.p, plan.bandStart.p, plan.nbands,
-                           nextChunk.p, pool, chunkCount.p, walk_lanes(), w2stats.p, st);
+      launch_ms_walk2(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.bandOrder.p, plan.bandStart.p, plan.nbands,
+                      nextChunk.p, pool, chunkCount.p, kWalkLanes, w2stats.p, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(ev1, st));
       usedBlocks = read1(used.p);
@@ -1220,8 +1212,7 @@ struct Engine {
     // run buckets (diff, hasHead): from the grouping's position sort in
     // merge(), or through position bins on demand (ensure_runs)
     runsValid = false;
-    if (env_u32("CMSBWT_RUN_BINS", 0) || env_u32("CMSBWT_RUN_BIN_SHIFT", 0) || env_u32("CMSBWT_RUN_BIN_GLOBAL", 0))
-      ensure_runs();
+    if (env_u32("CMSBWT_RUN_BIN_SHIFT", 0) || env_u32("CMSBWT_RUN_BIN_GLOBAL", 0)) ensure_runs();
     uint32_t ef = read1(errf.p);
     orderInvariant = (ef & 8u) == 0;
     if (ef & 1) throw InputError{CMSBWT_EINPUT, "internal: match ends not monotone inside a document"};
@@ -1241,19 +1232,17 @@ struct Engine {
     bool valid = false;
     uint32_t C = 0, nch = 0;
     DBuf<Chunk> dch;
-    DBuf<uint32_t> dLast, laneChunk;
+    DBuf<uint32_t> dLast;
     DBuf<uint32_t> bandOrder, bandStart;  // uniform-step walk: chunks grouped by offset band
     uint32_t nbands = 1;
   } plan;
 
   void build_plan(uint32_t C) {
     std::vector<Chunk> chunks;
-    std::vector<uint32_t> lastChunk(ndocs), firstChunk(ndocs);
-    uint32_t maxc = 0;
+    std::vector<uint32_t> lastChunk(ndocs);
     for (uint64_t d = 0; d < ndocs; d++) {
       uint64_t L = hdoc[d + 1] - hdoc[d] - 1;
       uint64_t nc = std::max<uint64_t>(1, (L + C - 1) / C);
-      firstChunk[d] = (uint32_t)chunks.size();
       for (uint64_t k = 0; k < nc; k++) {
         Chunk ch;
         ch.doc = (uint32_t)d;
@@ -1263,32 +1252,16 @@ struct Engine {
         chunks.push_back(ch);
       }
       lastChunk[d] = (uint32_t)chunks.size() - 1;
-      maxc = std::max<uint32_t>(maxc, (uint32_t)nc);
     }
     const uint32_t nch = (uint32_t)chunks.size();
-    // Lane order: document-major by default.  CMSBWT_OFFSET_MAJOR=1 puts the
-    // same offset of consecutive documents in one wave (shared reference
-    // lines, but same-offset text of equal-length copies collides in memory
-    // channels; measured slower on the benchmark).
-    std::vector<uint32_t> order(nch);
-    if (!env_u32("CMSBWT_OFFSET_MAJOR", 0)) {
-      for (uint32_t c = 0; c < nch; c++) order[c] = c;
-    } else {
-      uint32_t o = 0;
-      for (uint32_t k = 0; k < maxc; k++)
-        for (uint64_t d = 0; d < ndocs; d++)
-          if (firstChunk[d] + k <= lastChunk[d]) order[o++] = firstChunk[d] + k;
-    }
     plan.dch.alloc(nch);
     HIPCHK(hipMemcpyAsync(plan.dch.p, chunks.data(), nch * sizeof(Chunk), hipMemcpyHostToDevice, st));
     plan.dLast.alloc(ndocs);
     HIPCHK(hipMemcpyAsync(plan.dLast.p, lastChunk.data(), ndocs * 4, hipMemcpyHostToDevice, st));
-    plan.laneChunk.alloc(nch);
-    HIPCHK(hipMemcpyAsync(plan.laneChunk.p, order.data(), nch * 4, hipMemcpyHostToDevice, st));
     // Offset bands for the uniform-step walk: band = 8 * a / docLen, chunks of
     // a band in document order.  Copies of the reference then keep an XCD's
     // x / ISA / PLCP accesses inside one eighth of the reference.
-    const uint32_t nb = std::max<uint32_t>(1, std::min<uint32_t>(8, env_u32("CMSBWT_BANDS", 8)));
+    const uint32_t nb = 8;
     std::vector<uint32_t> bandCnt(nb + 1, 0), bandOf(nch);
     for (uint32_t c = 0; c < nch; c++) {
       const uint64_t L = hdoc[chunks[c].doc + 1] - hdoc[chunks[c].doc] - 1;
@@ -1567,32 +1540,6 @@ struct Engine {
     crossings = ncross;
   }
 
-  // per-SA-rank writer (one thread per unit), kept for A/B (CMSBWT_UNIT_WRITER=1)
-  void unit_writer(int rle, uint32_t E, DBuf<uint32_t>& posBegin, DBuf<uint32_t>& sSlot, DBuf<uint32_t>& sCount,
-                   DBuf<uint32_t>& headBase, uint64_t& Rn, uint64_t& symbols, DBuf<unsigned long long>& runStart,
-                   DBuf<uint8_t>& runChar) {
-    const uint32_t n = R.n;
-    WriterIn wi{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, sCount.p, headBase.p, bwtHeads.p, counter.p,
-                n, E, rle};
-    // units: the E end phrases, then SA ranks 1..n-1; runs counted per unit,
-    // joined across unit boundaries, emitted as (start, char) and packed
-    const uint64_t U64 = (uint64_t)E + n - 1;
-    if (U64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer units"};
-    const uint32_t Uw = (uint32_t)U64;
-    DBuf<uint32_t> wruns, whl, wprev;
-    DBuf<unsigned long long> wsym, wrunOff, wsymOff;
-    wruns.alloc(Uw); whl.alloc(Uw); wprev.alloc(Uw); wsym.alloc(Uw); wrunOff.alloc(Uw); wsymOff.alloc(Uw);
-    mk_wr_count(wi, Uw, wruns.p, wsym.p, whl.p, st);
-    exscan(whl.p, wprev.p, 0u, Uw, LastNonEmpty());
-    mk_wr_adjust(whl.p, wprev.p, Uw, wruns.p, st);
-    auto runs64 = rocprim::make_transform_iterator(wruns.p, WidenU64());
-    exscan(runs64, wrunOff.p, 0ull, Uw);
-    exscan(wsym.p, wsymOff.p, 0ull, Uw);
-    Rn = read1(wrunOff.p + (Uw - 1)) + read1(wruns.p + (Uw - 1));
-    symbols = read1(wsymOff.p + (Uw - 1)) + read1(wsym.p + (Uw - 1));
-    runStart.alloc(std::max<uint64_t>(Rn, 1)); runChar.alloc(std::max<uint64_t>(Rn, 1));
-    mk_wr_emit(wi, Uw, wrunOff.p, wsymOff.p, wprev.p, runStart.p, runChar.p, st);
-  }
   void merge(int rle) {
     if (!walked) throw InputError{CMSBWT_EARG, "run ms_walk first"};
     // Zero heads: the j-scan's `phrasesVector.size() - 1` (FN:1359) wraps and
@@ -1809,10 +1756,7 @@ struct Engine {
     uint64_t Rn = 0, symbols = 0;
     DBuf<unsigned long long> runStart;
     DBuf<uint8_t> runChar;
-    if (env_u32("CMSBWT_UNIT_WRITER", 0)) {
-      itemOfSlot.release();
-      unit_writer(rle, E, posBegin, sSlot, sCount, headBase, Rn, symbols, runStart, runChar);
-    } else {
+    {
       // elements: end phrases, then per SA rank its heads (or one element)
       DBuf<uint32_t> m, eBase;
       m.alloc(n); eBase.alloc(n);
@@ -1899,7 +1843,7 @@ struct Engine {
     used.zero(st);
     next.zero(st);
     const uint64_t sampleChars = (uint64_t)ns * plan.C;
-    const uint32_t sampleLanes = std::min<uint32_t>(walk_lanes(), ns);
+    const uint32_t sampleLanes = std::min<uint32_t>(kWalkLanes, ns);
     const uint64_t cap = ns + (uint64_t)sampleLanes * (kPoolBatch - 1) + sampleChars / 2 / kPoolB + 1024;  // up to 50 % heads
     DBuf<HeadRec> rec;
     DBuf<uint32_t> blkChunk, blkSeq;
@@ -2202,19 +2146,23 @@ struct Engine {
     DBuf<uint32_t> pairItem, pairWordOff;
     uint32_t npairs = 0;
     uint64_t viol = 0;
-    // writer units (E end phrases + SA ranks 1..n-1)
-    uint32_t Uw = 0;
+    // writer: elements of the owned SA ranks (eBase, rOf, per-rank info,
+    // element first/last chars ehl, inclusive run / symbol scans) and units
+    // (E end phrases + SA ranks 1..n-1, all ranks' after the all-reduce)
+    uint32_t Uw = 0, V = 0;
     DBuf<int64_t> bucket;
-    DBuf<uint32_t> uruns;
-    DBuf<unsigned long long> runOff, symOff, locStart;
-    DBuf<uint8_t> locChar;
+    DBuf<uint32_t> eBase, rOf, ehl;
+    DBuf<uint4> info1;
+    DBuf<unsigned long long> info2, cum, runIn, symIn;
+    DBuf<uint32_t> uruns, uhl, uprev;
+    DBuf<unsigned long long> runOff, symOff, locStart, gStart;
+    DBuf<uint8_t> locChar, gChar;
     uint64_t Rloc = 0, Rn = 0, symbols = 0;
   } dm;
   void partition(const uint32_t* dest, uint64_t cnt, DBuf<uint32_t>& perm, std::vector<uint64_t>& counts);
   void dm_check_err(const char* where);
-  WriterIn dm_writer_in();
-  void dm_begin(uint32_t world, uint32_t rank, uint64_t heads_total, uint64_t docs_total, uint32_t flags,
-                const int32_t* diffAll, const uint8_t* hashead, int rle);
+  ElemIn dm_elem_in();
+  void dm_begin(uint32_t world, uint32_t rank, uint64_t heads_total, uint64_t docs_total, uint32_t flags, int rle);
   void dm_route_heads(uint64_t* counts);
   void dm_pack_heads(int32_t* out);
   void dm_group(const int32_t* recv, uint64_t nrecv, uint32_t* saCounts);

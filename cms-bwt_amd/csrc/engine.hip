@@ -4,6 +4,7 @@
 // =========================================================================
 // C ABI
 using cmsbwt::Engine;
+using cmsbwt::HipError;
 
 struct cmsbwt_ctx {
   Engine* e = nullptr;
@@ -174,6 +175,56 @@ int cmsbwt_copy_array(cmsbwt_ctx* ctx, const char* name, void* out, uint64_t* by
   });
 }
 
+// Device primitives checked against host results (tests/test_gpu_primitives.py):
+// "exscan" / "inscan" (u32 plus, tile scan or rocPRIM per CMSBWT_ROCPRIM_SCAN,
+// init 7 for the exclusive scan), "select" (flagged compaction).  Values are
+// pseudo-random; `offset` shifts both buffers by that many elements (unaligned
+// pointers), `inplace` runs a scan with out == in.
+int cmsbwt_selftest(cmsbwt_ctx* ctx, const char* what, uint64_t n, uint64_t offset, int inplace, uint64_t* mismatches) {
+  if (!ctx || !what || !mismatches || n >= (1ull << 31)) return CMSBWT_EARG;
+  return guard(ctx, [&] {
+    cmsbwt::Engine& e = *ctx->e;
+    const std::string w = what;
+    std::vector<uint32_t> in(n), fl(n), want;
+    uint64_t z = 0x9E3779B97F4A7C15ull * (n + 1) + offset;
+    for (uint64_t i = 0; i < n; i++) {
+      z ^= z << 13; z ^= z >> 7; z ^= z << 17;
+      in[i] = (uint32_t)(z >> 40) & 0xffff;  // sums stay below 2^32
+      fl[i] = (uint32_t)(z >> 20) & 1;
+    }
+    cmsbwt::DBuf<uint32_t> a, b, f;
+    a.alloc(n + offset + 1);
+    b.alloc(n + offset + 1);
+    f.alloc(n + 1);
+    HIPCHK(hipMemcpyAsync(a.p + offset, in.data(), n * 4, hipMemcpyHostToDevice, e.st));
+    HIPCHK(hipMemcpyAsync(f.p, fl.data(), n * 4, hipMemcpyHostToDevice, e.st));
+    uint32_t* src = a.p + offset;
+    uint32_t* dst = inplace ? src : b.p + offset;
+    uint64_t cnt = n;
+    if (w == "exscan") {
+      e.exscan((const uint32_t*)src, dst, 7u, n);
+      uint32_t acc = 7;
+      for (uint64_t i = 0; i < n; i++) { want.push_back(acc); acc += in[i]; }
+    } else if (w == "inscan") {
+      e.inscan((const uint32_t*)src, dst, n, rocprim::plus<uint32_t>());
+      uint32_t acc = 0;
+      for (uint64_t i = 0; i < n; i++) { acc += in[i]; want.push_back(acc); }
+    } else if (w == "select") {
+      if (inplace) throw cmsbwt::InputError{CMSBWT_EARG, "select cannot run in place"};
+      cnt = e.select_flagged(src, f.p, dst, (uint32_t)n);
+      for (uint64_t i = 0; i < n; i++) if (fl[i]) want.push_back(in[i]);
+    } else {
+      throw cmsbwt::InputError{CMSBWT_EARG, "unknown selftest " + w};
+    }
+    std::vector<uint32_t> got(cnt);
+    if (cnt) HIPCHK(hipMemcpyAsync(got.data(), dst, cnt * 4, hipMemcpyDeviceToHost, e.st));
+    e.sync();
+    uint64_t bad = cnt == want.size() ? 0 : 1 + (uint64_t)std::max(cnt, (uint64_t)want.size());
+    for (uint64_t i = 0; i < std::min<uint64_t>(cnt, want.size()); i++) bad += got[i] != want[i];
+    *mismatches = bad;
+  });
+}
+
 int cmsbwt_host_read_collection(const char* path, uint64_t prefix, uint8_t* text, uint64_t text_cap,
                                 uint64_t* text_len, uint64_t* doc_off, uint64_t doc_cap, uint64_t* ndocs,
                                 uint64_t* sn) {
@@ -330,9 +381,9 @@ int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path
 
 // ---- position-sharded merge (include/cmsbwt.h "Multi-GPU merge")
 int cmsbwt_dm_begin(cmsbwt_ctx* ctx, uint32_t world, uint32_t rank, uint64_t heads_total, uint64_t docs_total,
-                    uint32_t flags, const int32_t* diff, const uint8_t* hashead, int rle) {
+                    uint32_t flags, int rle) {
   if (!ctx) return CMSBWT_EARG;
-  return guard(ctx, [&] { ctx->e->dm_begin(world, rank, heads_total, docs_total, flags, diff, hashead, rle); });
+  return guard(ctx, [&] { ctx->e->dm_begin(world, rank, heads_total, docs_total, flags, rle); });
 }
 int cmsbwt_dm_route_heads(cmsbwt_ctx* ctx, uint64_t* counts) {
   if (!ctx || !counts) return CMSBWT_EARG;

@@ -39,9 +39,6 @@ struct ItemsSoA {
 };
 
 // ms_walk.hip
-void launch_ms_walk(const DevRef& R, const uint8_t* text, const uint64_t* docOff, const Chunk* chunks,
-                    uint32_t nchunks, const uint32_t* laneChunk, const Pool& pool, uint32_t* chunkCount,
-                    hipStream_t st);
 void launch_chunk_with_end(const Chunk* chunks, const uint32_t* chunkCount, uint32_t nch, unsigned long long* out,
                            hipStream_t st);
 void launch_scatter_heads(const Pool& pool, uint32_t blocksUsed, const uint32_t* chunkCount,

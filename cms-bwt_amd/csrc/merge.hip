@@ -23,16 +23,6 @@ __global__ void k_gather_u32(const uint32_t* __restrict__ src, const uint32_t* _
   if (i < n) dst[i] = src[perm[i]];
 }
 
-// key for the MatchInSet order (match.h:27-33) on consistent data:
-// smaller=true first by len ascending, then smaller=false by len descending.
-__global__ void k_item_key(const uint32_t* __restrict__ len, const uint8_t* __restrict__ sm,
-                           const uint32_t* __restrict__ perm, uint32_t* __restrict__ key, uint64_t n) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  uint32_t q = perm[i];
-  uint32_t L = len[q];
-  key[i] = sm[q] ? L : (0x80000000u | (0x7fffffffu - L));
-}
 
 // item boundaries over perm sorted by (pos, len, isaNext, idx)
 __global__ void k_item_flags(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ pos,
@@ -281,57 +271,8 @@ __global__ void k_sa_counts(const int32_t* __restrict__ sa, const uint32_t* __re
   headsSA[r] = slot[e] - slot[b];
 }
 
-// Ranks of FN:1432-1453 and the initial (first-symbol) order of the head
-// string for the suffix sort (FN:1455-1459).
-__global__ void k_ranks(const ItemsSoA it, uint32_t K, const uint32_t* __restrict__ perm,
-                        const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ isaRef,
-                        const uint32_t* __restrict__ itemRankBase, const uint32_t* __restrict__ headBase,
-                        uint32_t n, uint32_t E, int32_t* __restrict__ T, uint32_t* __restrict__ sa,
-                        uint32_t* __restrict__ grp) {
-  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= K) return;
-  uint32_t p = it.pos[q];
-  uint32_t cnt = it.count[q], f = it.first[q];
-  if (p == n - 1) {  // end phrases: one rank each, in document order
-    for (uint32_t m = 0; m < cnt; m++) {
-      uint32_t idx = perm[f + m];
-      T[idx] = (int32_t)(1 + m);
-      sa[1 + m] = idx;
-      grp[idx] = 1 + m;
-    }
-    return;
-  }
-  uint32_t r = isaRef[p];
-  uint32_t b = posBegin[p];
-  int32_t rank = (int32_t)(E + 2 + itemRankBase[r] + (q - b));
-  uint32_t g = 1 + headBase[r] + (it.slot[q] - it.slot[b]);
-  for (uint32_t m = 0; m < cnt; m++) {
-    uint32_t idx = perm[f + m];
-    T[idx] = rank;
-    sa[g + m] = idx;
-    grp[idx] = g;
-  }
-}
 
-// unresolved members: sa positions of items with >= 2 heads (not end phrases)
-__global__ void k_active_init(const ItemsSoA it, uint32_t K, uint32_t n, const uint32_t* __restrict__ isaRef,
-                              const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ headBase,
-                              const uint32_t* __restrict__ actOff, uint32_t* __restrict__ act) {
-  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= K) return;
-  uint32_t p = it.pos[q], cnt = it.count[q];
-  if (p == n - 1 || cnt < 2) return;
-  uint32_t b = posBegin[p];
-  uint32_t g = 1 + headBase[isaRef[p]] + (it.slot[q] - it.slot[b]);
-  uint32_t o = actOff[q];
-  for (uint32_t m = 0; m < cnt; m++) act[o + m] = g + m;
-}
 
-__global__ void k_active_count(const ItemsSoA it, uint32_t K, uint32_t n, uint32_t* __restrict__ c) {
-  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= K) return;
-  c[q] = (it.pos[q] == n - 1 || it.count[q] < 2) ? 0 : it.count[q];
-}
 
 // prefix doubling: key = (group of suffix, group of suffix + h)
 __global__ void k_dbl_keys(const uint32_t* __restrict__ act, const uint32_t* __restrict__ sa,
@@ -396,40 +337,6 @@ __global__ void k_map_order(const uint32_t* __restrict__ posBegin, const uint32_
 __global__ void k_dbl_gstart(const uint64_t* __restrict__ key, uint32_t U, uint32_t* __restrict__ flag) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u < U) flag[u] = (u == 0 || (key[u] >> 32) != (key[u - 1] >> 32)) ? 1u : 0u;
-}
-__global__ void k_dbl_small(const uint32_t* __restrict__ gs, uint32_t G, uint32_t U, const uint32_t* __restrict__ act,
-                            uint64_t* __restrict__ key, uint32_t* __restrict__ val, uint32_t* __restrict__ sa,
-                            uint32_t* __restrict__ grp, uint32_t* __restrict__ keep, uint32_t* __restrict__ big,
-                            uint32_t maxSmall) {
-  const uint32_t g = blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= G) return;
-  const uint32_t u0 = gs[g], u1 = g + 1 < G ? gs[g + 1] : U;
-  if (u1 - u0 > maxSmall) {
-    for (uint32_t u = u0; u < u1; u++) big[u] = 1;
-    return;
-  }
-  for (uint32_t a = u0 + 1; a < u1; a++) {  // insertion sort by (label, label of suffix + h)
-    const uint64_t kk = key[a];
-    const uint32_t vv = val[a];
-    uint32_t b = a;
-    while (b > u0 && key[b - 1] > kk) {
-      key[b] = key[b - 1];
-      val[b] = val[b - 1];
-      b--;
-    }
-    key[b] = kk;
-    val[b] = vv;
-  }
-  // the u-th member takes the group's u-th sa position; equal keys share the
-  // label of their first position; a member alone in its run is resolved
-  uint32_t rs = u0;
-  for (uint32_t u = u0; u < u1; u++) {
-    if (u > u0 && key[u] != key[u - 1]) rs = u;
-    const bool endRun = u + 1 == u1 || key[u + 1] != key[u];
-    sa[act[u]] = val[u];
-    grp[val[u]] = act[rs];
-    keep[u] = (rs == u && endRun) ? 0u : 1u;
-  }
 }
 // Unresolved members (items with >= 2 heads, end phrases excluded) in sa
 // position order, without a sort: per position p its count at rank ISA[p],
@@ -611,28 +518,7 @@ __global__ void k_scatter_u32(const uint32_t* __restrict__ src, const uint32_t* 
   if (b < n) dst[idx[b]] = src[b];
 }
 
-// FN:1468-1472: rank of each head and BWTheads (listOfChars in rank order)
-__global__ void k_head_ranks(const uint32_t* __restrict__ sa, const uint8_t* __restrict__ lchar, uint32_t H,
-                             uint32_t* __restrict__ headRank, uint8_t* __restrict__ bwtHeads) {
-  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= H) return;
-  uint32_t idx = sa[r + 1];
-  headRank[idx] = r;
-  bwtHeads[r] = lchar[idx];
-}
 
-// FN:1480-1494: next-head rank per member, keyed by item for the per-item sort
-__global__ void k_nhr_keys(const ItemsSoA it, uint32_t K, const uint32_t* __restrict__ perm,
-                           const uint32_t* __restrict__ headRank, const uint16_t* __restrict__ nexthead,
-                           uint64_t* __restrict__ key) {
-  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q >= K) return;
-  uint32_t cnt = it.count[q], f = it.first[q], s = it.slot[q];
-  for (uint32_t m = 0; m < cnt; m++) {
-    uint32_t idx = perm[f + m];
-    key[s + m] = ((uint64_t)q << 32) | headRank[idx + nexthead[idx]];
-  }
-}
 
 // ---- slot-major members (one thread per head, no per-item loops)
 // mark[slot[q]] = 1 for q >= 1; its inclusive scan is the item of each slot
@@ -779,10 +665,6 @@ __global__ void k_nhr_big_back(const unsigned long long* __restrict__ sorted, co
   if (u < B) nhr[slots[u]] = (uint32_t)sorted[u];
 }
 
-__global__ void k_low32(const uint64_t* __restrict__ key, uint32_t* __restrict__ out, uint64_t n) {
-  uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n) out[i] = (uint32_t)key[i];
-}
 
 // ------------------------------------------------------------ counterSmallerThanHead
 // FN:1523-1603.  Work unit (item q, target t = pos+1+k, k < untilNext): the
@@ -1177,7 +1059,7 @@ __device__ __forceinline__ uint32_t addc_mask(uint32_t acc, uint64_t m) {
   return r;
 }
 // unsigned compare of each lane, as a wave mask (llvm.amdgcn.icmp predicates)
-constexpr int kNE = 33, kUGT = 34, kUGE = 35, kULT = 36, kULE = 37;
+constexpr int kNE = 33, kUGT = 34, kULT = 36, kULE = 37;  // llvm.amdgcn.icmp predicates
 template <int P>
 __device__ __forceinline__ uint64_t ucmp(uint32_t a, uint32_t b) {
   return __builtin_amdgcn_uicmp(a, b, P);
@@ -1339,7 +1221,6 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
         r += e;
       }
       if (qn == 0) break;  // (the walk is done: an empty list never stops it)
-      if (A.slotCap & 2) continue;  // timing experiments only (CMSBWT_TGT_DEBUG): no searches
       // search pass over the listed queries, 64 at a time: first the three
       // longest items of the class, read from the target's owning lane
       // (ds_bpermute); what they do not settle goes to the wave's search
@@ -1430,7 +1311,6 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
       }
     }
     __syncthreads();
-    if (A.slotCap & 4) continue;  // timing experiments only: staging alone
     const uint32_t nS = nG[2 * wv], nF = nG[2 * wv + 1];
     walk(std::true_type{}, 0u, nS);
     walk(std::false_type{}, kTgtRec - nF, kTgtRec);
@@ -1525,122 +1405,10 @@ __global__ void k_bucket(const int32_t* __restrict__ countIncl, const uint8_t* _
 }
 
 // ------------------------------------------------------------ writer (FN:1631-1777)
-struct WriterArgs {
-  const int32_t* sa;
-  const uint8_t* bwt;
-  const int64_t* bucket;     // pos-indexed (the inversion is this gather)
-  const uint32_t* posBegin;
-  const uint32_t* slot;      // K+1
-  const uint32_t* count;
-  const uint32_t* headBase;  // per SA rank
-  const uint8_t* bwtHeads;
-  const unsigned long long* counter;
-  uint32_t n;
-  uint32_t E;
-  int rle;                   // 1: .rl_bwt remainder quirk (FN:1761-1770); 0: .bwt (FN:1678-1686)
-  // position-sharded merge: head characters by local slot, and only the
-  // units whose position lies in [P0, P1) produce segments (bwtSlot == null:
-  // one GPU, characters by head rank)
-  const uint8_t* bwtSlot;
-  uint32_t P0, P1;
-};
-
-template <bool EMIT>
-__device__ __forceinline__ uint64_t d_segments(const WriterArgs& A, uint32_t r, uint8_t* oc,
-                                               unsigned long long* on) {
-  const uint32_t p = (uint32_t)A.sa[r];
-  const uint8_t c = A.bwt[r];
-  const int64_t b = A.bucket[p];
-  uint64_t ns = 0;
-  if (b > 0) {
-    if (EMIT) { oc[0] = c; on[0] = (unsigned long long)b; }
-    return 1;
-  }
-  if (b == 0) return 0;
-  int64_t acc = b;
-  const uint32_t i0 = A.posBegin[p], i1 = A.posBegin[p + 1];
-  const uint32_t s0 = A.slot[i0];
-  const uint32_t hb = A.headBase[r];
-  for (uint32_t q = i0; q < i1; q++) {
-    const uint32_t sb = A.slot[q], se = sb + A.count[q];
-    for (uint32_t s = sb; s < se; s++) {
-      const unsigned long long cs = A.counter[s];
-      if (cs) {
-        if (EMIT) { oc[ns] = c; on[ns] = cs; }
-        ns++;
-        acc += (int64_t)cs;
-      }
-      if (EMIT) { oc[ns] = A.bwtHeads[hb + (s - s0)]; on[ns] = 1; }
-      ns++;
-      acc++;
-    }
-    if (A.rle && acc != 0) {
-      if (EMIT) { oc[ns] = c; on[ns] = (unsigned long long)(-acc); }
-      ns++;
-    }
-  }
-  if (!A.rle && acc < 0) {
-    if (EMIT) { oc[ns] = c; on[ns] = (unsigned long long)(-acc); }
-    ns++;
-  }
-  return ns;
-}
-
-// Segments of one writer unit, in output order, to f(char, count): units
-// [0, E) are the end phrases' BWT characters (rank 0's heads), unit E + r - 1
-// is SA rank r >= 1 (the same walk as d_segments).
-template <class F>
-__device__ __forceinline__ void d_unit_segments(const WriterArgs& A, uint32_t u, F&& f) {
-  if (A.bwtSlot) {  // sharded: the end phrases' unit belongs to the owner of position n-1
-    const uint32_t pu = u < A.E ? A.n - 1 : (uint32_t)A.sa[u - A.E + 1];
-    if (pu < A.P0 || pu >= A.P1) return;
-    if (u < A.E) { f(A.bwtSlot[A.slot[A.posBegin[A.n - 1]] + u], 1ull); return; }
-  }
-  if (u < A.E) { f(A.bwtHeads[u], 1ull); return; }
-  const uint32_t r = u - A.E + 1;
-  const uint32_t p = (uint32_t)A.sa[r];
-  const uint8_t c = A.bwt[r];
-  const int64_t b = A.bucket[p];
-  if (b > 0) { f(c, (unsigned long long)b); return; }
-  if (b == 0) return;
-  int64_t acc = b;
-  const uint32_t i0 = A.posBegin[p], i1 = A.posBegin[p + 1];
-  const uint32_t s0 = A.slot[i0];
-  const uint32_t hb = A.bwtSlot ? 0u : A.headBase[r];
-  for (uint32_t q = i0; q < i1; q++) {
-    const uint32_t sb = A.slot[q], se = sb + A.count[q];
-    for (uint32_t s = sb; s < se; s++) {
-      const unsigned long long cs = A.counter[s];
-      if (cs) { f(c, cs); acc += (int64_t)cs; }
-      f(A.bwtSlot ? A.bwtSlot[s] : A.bwtHeads[hb + (s - s0)], 1ull);
-      acc++;
-    }
-    if (A.rle && acc != 0) f(c, (unsigned long long)(-acc));  // FN:1761-1770 quirk
-  }
-  if (!A.rle && acc < 0) f(c, (unsigned long long)(-acc));
-}
-
-// Run writer, pass 1: per unit its run starts (counting its first segment),
-// symbols, first and last character.  hl = has << 16 | last << 8 | first.
-__global__ void k_wr_count(WriterArgs A, uint32_t U, uint32_t* __restrict__ runs, unsigned long long* __restrict__ sym,
-                           uint32_t* __restrict__ hl) {
-  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= U) return;
-  int prev = -1, first = -1;
-  uint32_t nr = 0;
-  unsigned long long ns = 0;
-  d_unit_segments(A, u, [&](uint8_t c, unsigned long long cnt) {
-    if (first < 0) first = c;
-    if ((int)c != prev) nr++;
-    prev = c;
-    ns += cnt;
-  });
-  runs[u] = nr;
-  sym[u] = ns;
-  hl[u] = first < 0 ? 0u : (1u << 16) | ((uint32_t)prev << 8) | (uint32_t)first;
-}
-// pass 2: a unit's first segment continues the previous non-empty unit's run
-// when the characters match (prevHL = exclusive "last non-empty" scan of hl)
+// Segments (character, count) in output order, grouped into runs: a unit /
+// element's run count includes its first segment; k_wr_adjust drops that one
+// when it continues the previous non-empty unit's run (prevHL = exclusive
+// "last non-empty" scan of hl = has << 16 | last << 8 | first)
 __global__ void k_wr_adjust(const uint32_t* __restrict__ hl, const uint32_t* __restrict__ prevHL, uint32_t U,
                             uint32_t* __restrict__ runs) {
   const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1648,26 +1416,7 @@ __global__ void k_wr_adjust(const uint32_t* __restrict__ hl, const uint32_t* __r
   const uint32_t a = hl[u], pv = prevHL[u];
   if ((a >> 16) && (pv >> 16) && (a & 0xff) == ((pv >> 8) & 0xff)) runs[u]--;
 }
-// pass 3: emit run starts (symbol offsets) and characters
-__global__ void k_wr_emit(WriterArgs A, uint32_t U, const unsigned long long* __restrict__ runOff,
-                          const unsigned long long* __restrict__ symOff, const uint32_t* __restrict__ prevHL,
-                          unsigned long long* __restrict__ runStart, uint8_t* __restrict__ runChar) {
-  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
-  if (u >= U) return;
-  const uint32_t pv = prevHL[u];
-  int prev = (pv >> 16) ? (int)((pv >> 8) & 0xff) : -1;
-  unsigned long long j = runOff[u], pos = symOff[u];
-  d_unit_segments(A, u, [&](uint8_t c, unsigned long long cnt) {
-    if ((int)c != prev) {
-      runStart[j] = pos;
-      runChar[j] = c;
-      j++;
-    }
-    prev = c;
-    pos += cnt;
-  });
-}
-// pass 4: 9-byte little-endian records (length u64, char)
+// 9-byte little-endian records (length u64, char), FN:1708-1709
 __global__ void k_wr_records(const unsigned long long* __restrict__ runStart, const uint8_t* __restrict__ runChar,
                              uint64_t R, unsigned long long total, uint8_t* __restrict__ out) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1679,14 +1428,13 @@ __global__ void k_wr_records(const unsigned long long* __restrict__ runStart, co
   o[8] = runChar[j];
 }
 
-// ---- element writer (one GPU): the same segments as d_unit_segments, one
-// thread per writer element instead of per SA rank.  Elements in output
-// order: the E end phrases (rank 0), then per SA rank r >= 1 its heads in
-// head-rank order (= slot order of its position), or one element when it has
-// none.  A rank's heads are contiguous in every array the thread reads
-// (counter and cum by slot, bwtHeads by head rank), so a wave reads
-// contiguous memory whatever the head count of its ranks; the per-rank loops
-// of k_wr_count/k_wr_emit diverged over 1..1000+ heads per thread.
+// ---- element writer: one thread per writer element instead of per SA rank.
+// Elements in output order: the E end phrases (rank 0), then per SA rank
+// r >= 1 its heads in head-rank order (= slot order of its position), or one
+// element when it has none.  A rank's heads are contiguous in every array the
+// thread reads (counter and cum by slot, bwtHeads by head rank), so a wave
+// reads contiguous memory whatever the head count of its ranks; the per-rank
+// loops of the round-1 writer diverged over 1..1000+ heads per thread.
 struct ElemArgs {
   const int32_t* sa;
   const uint8_t* bwt;
@@ -1704,6 +1452,9 @@ struct ElemArgs {
   const unsigned long long* info2;     // per SA rank: bucket (56-bit two's complement) | BWT char << 56
   uint32_t n, E, H;
   int rle;
+  // position-sharded merge: head characters by local slot (one GPU: null,
+  // characters by head rank from bwtHeads)
+  const uint8_t* bwtSlot;
 };
 
 template <class F>
@@ -1711,7 +1462,7 @@ __device__ __forceinline__ void d_elem_segments(const ElemArgs& A, uint32_t e, F
   const uint32_t r = A.rOf[e];
   const uint4 I = A.info1[r];  // the rank's fields, read once per element (k_el_info)
   const uint32_t k = e - I.x;
-  if (r == 0) { f(A.bwtHeads[k], 1ull); return; }  // end phrases (units u < E)
+  if (r == 0) { f(A.bwtSlot ? A.bwtSlot[I.z + k] : A.bwtHeads[k], 1ull); return; }  // end phrases (units u < E)
   const unsigned long long J = A.info2[r];
   const uint8_t c = (uint8_t)(J >> 56);
   const int64_t b = ((int64_t)(J << 8)) >> 8;
@@ -1725,7 +1476,7 @@ __device__ __forceinline__ void d_elem_segments(const ElemArgs& A, uint32_t e, F
   const uint32_t s0 = I.z, s = s0 + k;
   const unsigned long long cs = A.counter[s];
   if (cs) f(c, cs);
-  f(A.bwtHeads[I.w + k], 1ull);
+  f(A.bwtSlot ? A.bwtSlot[s] : A.bwtHeads[I.w + k], 1ull);
   const bool last = A.rle ? (s + 1 >= A.H || A.itemOfSlot[s + 1] != A.itemOfSlot[s]) : k + 1 == nh;
   if (last) {
     const int64_t acc = b + (int64_t)(A.cum[s] - (s0 ? A.cum[s0 - 1] : 0ull));
@@ -1807,53 +1558,138 @@ __global__ void k_el_wr_emit(ElemArgs A, uint32_t V, const unsigned long long* _
   });
 }
 
-__global__ void k_seg_count(WriterArgs A, unsigned long long* __restrict__ segN) {
-  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= A.n) return;
-  segN[r] = r == 0 ? 0 : d_segments<false>(A, r, nullptr, nullptr);
+// ---- element writer of the position-sharded merge (dist_merge.hip): the
+// elements of the SA ranks whose position this rank owns (P0 <= SA[r] < P1;
+// the E end phrases belong to the owner of position n-1), head characters by
+// local slot.  Elements of one SA rank form one writer unit; every element of
+// a unit with heads emits its head's character, so all of them are non-empty.
+__device__ __forceinline__ bool d_owns(uint32_t p, uint32_t P0, uint32_t P1) { return p >= P0 && p < P1; }
+
+__global__ void k_dm_el_count(const int32_t* __restrict__ sa, const uint32_t* __restrict__ posBegin,
+                              const uint32_t* __restrict__ slot, uint32_t n, uint32_t E, uint32_t P0, uint32_t P1,
+                              uint32_t* __restrict__ m) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  if (r == 0) { m[0] = d_owns(n - 1, P0, P1) ? E : 0u; return; }
+  const uint32_t p = (uint32_t)sa[r];
+  if (!d_owns(p, P0, P1)) { m[r] = 0; return; }
+  const uint32_t nh = slot[posBegin[p + 1]] - slot[posBegin[p]];
+  m[r] = max(nh, 1u);
 }
 
-__global__ void k_seg_emit(WriterArgs A, const unsigned long long* __restrict__ segOff, uint8_t* __restrict__ sc,
-                           unsigned long long* __restrict__ sn) {
-  uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r >= A.n) return;
+// k_el_info's fields from local slots: heads of rank r, slot base of its
+// position (for r = 0: of the end phrases' item at n-1)
+__global__ void k_dm_el_info(const int32_t* __restrict__ sa, const uint8_t* __restrict__ bwt,
+                             const int64_t* __restrict__ bucket, const uint32_t* __restrict__ posBegin,
+                             const uint32_t* __restrict__ slot, const uint32_t* __restrict__ elemBase, uint32_t n,
+                             uint32_t E, uint32_t P0, uint32_t P1, uint4* __restrict__ info1,
+                             unsigned long long* __restrict__ info2) {
+  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
+  if (r >= n) return;
+  uint32_t nh = 0, s0 = 0;
+  unsigned long long j = 0;
   if (r == 0) {
-    for (uint32_t d = 0; d < A.E; d++) { sc[d] = A.bwtHeads[d]; sn[d] = 1; }
-    return;
+    if (d_owns(n - 1, P0, P1)) { nh = E; s0 = slot[posBegin[n - 1]]; }
+  } else {
+    const uint32_t p = (uint32_t)sa[r];
+    if (d_owns(p, P0, P1)) {
+      const int64_t b = bucket[p];
+      nh = slot[posBegin[p + 1]] - slot[posBegin[p]];
+      if (b < 0 && nh) s0 = slot[posBegin[p]];
+      j = ((unsigned long long)b & 0x00ffffffffffffffull) | ((unsigned long long)bwt[r] << 56);
+    }
   }
-  uint64_t o = A.E + segOff[r];
-  d_segments<true>(A, r, sc + o, sn + o);
+  info1[r] = make_uint4(elemBase[r], nh, s0, 0u);
+  info2[r] = j;
 }
 
-__global__ void k_run_flags(const uint8_t* __restrict__ sc, uint64_t S, unsigned long long* __restrict__ flag) {
-  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= S) return;
-  flag[k] = (k == 0 || sc[k] != sc[k - 1]) ? 1ull : 0ull;
-}
-
-// runId = inclusive scan of flags (1-based); cum = inclusive scan of counts.
-__global__ void k_run_pack(const uint8_t* __restrict__ sc, const unsigned long long* __restrict__ runId,
-                           const unsigned long long* __restrict__ cum, uint64_t S,
-                           unsigned long long* __restrict__ runEnd, uint8_t* __restrict__ runChar) {
-  uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= S) return;
-  if (k + 1 == S || runId[k + 1] != runId[k]) {
-    uint64_t j = runId[k] - 1;
-    runEnd[j] = cum[k];
-    runChar[j] = sc[k];
+// runs of each element less one when its first segment continues the
+// previous element of the same unit (SA rank r >= 1)
+__global__ void k_dm_el_adj(const uint32_t* __restrict__ rOf, const uint32_t* __restrict__ hl,
+                            const uint32_t* __restrict__ runs, uint32_t V, uint32_t* __restrict__ adj) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= V) return;
+  const uint32_t a = hl[e];
+  uint32_t j = 0;
+  if (e > 0 && rOf[e] != 0 && rOf[e - 1] == rOf[e]) {
+    const uint32_t pv = hl[e - 1];
+    j = ((a >> 16) && (pv >> 16) && (a & 0xff) == ((pv >> 8) & 0xff)) ? 1u : 0u;
   }
+  adj[e] = runs[e] - j;
 }
 
-__global__ void k_run_records(const unsigned long long* __restrict__ runEnd, const uint8_t* __restrict__ runChar,
-                              uint64_t R, uint8_t* __restrict__ out) {
-  uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= R) return;
-  uint64_t len = runEnd[j] - (j ? runEnd[j - 1] : 0ull);
-  uint8_t* o = out + 9 * j;
-#pragma unroll
-  for (int b = 0; b < 8; b++) o[b] = (uint8_t)(len >> (8 * b));
-  o[8] = runChar[j];
+// writer units (hl << 32 | runs, symbols) from the elements: units u < E are
+// the end phrases (one element each), unit E + r - 1 the elements of SA rank
+// r; zero for units of other ranks.  runIn / symIn: inclusive scans over the
+// elements of adj and sym.
+__global__ void k_dm_el_units(const uint32_t* __restrict__ elemBase, const uint32_t* __restrict__ m,
+                              const unsigned long long* __restrict__ runIn, const unsigned long long* __restrict__ symIn,
+                              const uint32_t* __restrict__ hl, uint32_t n, uint32_t E, uint32_t U,
+                              int64_t* __restrict__ out) {
+  const uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
+  if (u >= U) return;
+  uint32_t e0, e1;
+  if (u < E) {
+    if (!m[0]) { out[u] = 0; out[(uint64_t)U + u] = 0; return; }
+    e0 = elemBase[0] + u;
+    e1 = e0 + 1;
+  } else {
+    const uint32_t r = u - E + 1;
+    if (!m[r]) { out[u] = 0; out[(uint64_t)U + u] = 0; return; }
+    e0 = elemBase[r];
+    e1 = e0 + m[r];
+  }
+  const unsigned long long rb = e0 ? runIn[e0 - 1] : 0ull, sb = e0 ? symIn[e0 - 1] : 0ull;
+  const uint32_t nr = (uint32_t)(runIn[e1 - 1] - rb);
+  const unsigned long long ns = symIn[e1 - 1] - sb;
+  const uint32_t hf = hl[e0], hlast = hl[e1 - 1];
+  const uint32_t h = (hf >> 16) ? ((1u << 16) | (hlast & 0xff00u) | (hf & 0xffu)) : 0u;
+  out[u] = (int64_t)(((uint64_t)h << 32) | nr);
+  out[(uint64_t)U + u] = (int64_t)ns;
 }
+
+// emission: an element's first run index and symbol offset from its unit's
+// (unitRunOff: global run index, or the rank-local stream index; the unit's
+// first segment continues the previous unit's run when `joined`), the
+// character before it from the previous element of its unit or, for a unit's
+// first element, from the previous non-empty unit (prevHL, over all ranks)
+__global__ void k_dm_el_emit(ElemArgs A, uint32_t V, const uint32_t* __restrict__ elemBase,
+                             const unsigned long long* __restrict__ runIn, const unsigned long long* __restrict__ symIn,
+                             const unsigned long long* __restrict__ unitRunOff,
+                             const unsigned long long* __restrict__ unitSymOff, const uint32_t* __restrict__ prevHL,
+                             const uint32_t* __restrict__ unitHL, const uint32_t* __restrict__ hl,
+                             unsigned long long* __restrict__ runStart, uint8_t* __restrict__ runChar) {
+  const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= V) return;
+  const uint32_t r = A.rOf[e];
+  const uint32_t u = r ? A.E + r - 1 : e - elemBase[0];
+  const uint32_t e0 = r ? elemBase[r] : e;
+  const uint32_t pu = prevHL[u], hu = unitHL[u];
+  int prev;
+  unsigned long long j = unitRunOff[u];
+  if (e == e0) {
+    prev = (pu >> 16) ? (int)((pu >> 8) & 0xff) : -1;
+  } else {
+    prev = (int)((hl[e - 1] >> 8) & 0xff);
+    const bool joined = (hu >> 16) && (pu >> 16) && (hu & 0xff) == ((pu >> 8) & 0xff);
+    j += runIn[e - 1] - (e0 ? runIn[e0 - 1] : 0ull) - (joined ? 1u : 0u);
+  }
+  unsigned long long pos = unitSymOff[u] + (e ? symIn[e - 1] : 0ull) - (e0 ? symIn[e0 - 1] : 0ull);
+  d_elem_segments(A, e, [&](uint8_t c, unsigned long long cnt) {
+    if ((int)c != prev) {
+      runStart[j] = pos;
+      runChar[j] = c;
+      j++;
+    }
+    prev = c;
+    pos += cnt;
+  });
+}
+
+
+
+
+
 
 __global__ void k_count_distinct(const uint32_t* __restrict__ v, uint32_t K, unsigned long long* __restrict__ out) {
   __shared__ unsigned int acc;
@@ -2010,10 +1846,6 @@ void mk_iota(uint32_t* p, uint64_t n, hipStream_t st) { if (n) hipLaunchKernelGG
 void mk_gather(const uint32_t* src, const uint32_t* perm, uint32_t* dst, uint64_t n, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_gather_u32, g1(n), dim3(256), 0, st, src, perm, dst, n);
 }
-void mk_item_key(const uint32_t* len, const uint8_t* sm, const uint32_t* perm, uint32_t* key, uint64_t n,
-                 hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_item_key, g1(n), dim3(256), 0, st, len, sm, perm, key, n);
-}
 void mk_item_flags(const uint32_t* perm, const HeadsSoA& h, uint32_t* flag, uint64_t H, hipStream_t st) {
   if (H) hipLaunchKernelGGL(k_item_flags, g1(H), dim3(256), 0, st, perm, h.pos, h.len, h.isa, flag, H);
 }
@@ -2114,21 +1946,6 @@ void mk_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t* s
                   uint32_t* itemsSA, uint32_t* headsSA, hipStream_t st) {
   hipLaunchKernelGGL(k_sa_counts, g1(n), dim3(256), 0, st, sa, posBegin, slot, n, E, itemsSA, headsSA);
 }
-void mk_ranks(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uint32_t* posBegin,
-              const uint32_t* isaRef, const uint32_t* itemRankBase, const uint32_t* headBase, uint32_t n,
-              uint32_t E, int32_t* T, uint32_t* sa, uint32_t* grp, hipStream_t st) {
-  if (K) hipLaunchKernelGGL(k_ranks, g1(K), dim3(256), 0, st, it, K, perm, posBegin, isaRef, itemRankBase,
-                            headBase, n, E, T, sa, grp);
-}
-void mk_active_count(const ItemsSoA& it, uint32_t K, uint32_t n, uint32_t* c, hipStream_t st) {
-  if (K) hipLaunchKernelGGL(k_active_count, g1(K), dim3(256), 0, st, it, K, n, c);
-}
-void mk_active_init(const ItemsSoA& it, uint32_t K, uint32_t n, const uint32_t* isaRef,
-                    const uint32_t* posBegin, const uint32_t* headBase, const uint32_t* actOff,
-                    uint32_t* act, hipStream_t st) {
-  if (K) hipLaunchKernelGGL(k_active_init, g1(K), dim3(256), 0, st, it, K, n, isaRef, posBegin, headBase,
-                            actOff, act);
-}
 void mk_dbl_keys(const uint32_t* act, const uint32_t* sa, const uint32_t* grp, uint32_t h, uint32_t U,
                  uint64_t* key, uint32_t* val, hipStream_t st) {
   if (U) hipLaunchKernelGGL(k_dbl_keys, g1(U), dim3(256), 0, st, act, sa, grp, h, U, key, val);
@@ -2147,10 +1964,6 @@ void mk_map_order(const uint32_t* posBegin, const uint32_t* len, const uint8_t* 
 }
 void mk_dbl_gstart(const uint64_t* key, uint32_t U, uint32_t* flag, hipStream_t st) {
   if (U) hipLaunchKernelGGL(k_dbl_gstart, g1(U), dim3(256), 0, st, key, U, flag);
-}
-void mk_dbl_small(const uint32_t* gs, uint32_t G, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val,
-                  uint32_t* sa, uint32_t* grp, uint32_t* keep, uint32_t* big, uint32_t maxSmall, hipStream_t st) {
-  if (G) hipLaunchKernelGGL(k_dbl_small, g1(G), dim3(256), 0, st, gs, G, U, act, key, val, sa, grp, keep, big, maxSmall);
 }
 void mk_act_count(const uint32_t* posBegin, const uint32_t* count, const uint32_t* isaRef, uint32_t n, uint32_t* cntR,
                   hipStream_t st) {
@@ -2175,17 +1988,6 @@ void mk_dbl_gather_big(const uint32_t* orig, uint32_t B, const uint32_t* act, co
 }
 void mk_scatter_u32(const uint32_t* src, const uint32_t* idx, uint32_t n, uint32_t* dst, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_scatter_u32, g1(n), dim3(256), 0, st, src, idx, n, dst);
-}
-void mk_head_ranks(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint32_t* headRank, uint8_t* bwtHeads,
-                   hipStream_t st) {
-  if (H) hipLaunchKernelGGL(k_head_ranks, g1(H), dim3(256), 0, st, sa, lchar, H, headRank, bwtHeads);
-}
-void mk_nhr_keys(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uint32_t* headRank,
-                 const uint16_t* nexthead, uint64_t* key, hipStream_t st) {
-  if (K) hipLaunchKernelGGL(k_nhr_keys, g1(K), dim3(256), 0, st, it, K, perm, headRank, nexthead, key);
-}
-void mk_low32(const uint64_t* key, uint32_t* out, uint64_t n, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_low32, g1(n), dim3(256), 0, st, key, out, n);
 }
 void mk_win_flags(const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t P0, uint32_t P1,
                   uint32_t winPos, uint32_t slotCap, uint32_t* flag, hipStream_t st) {
@@ -2221,8 +2023,7 @@ void mk_counter_tgt(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t
                     const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
                     unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st) {
   if (!nw) return;
-  CounterArgs A{it, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n,
-                (uint32_t)(getenv("CMSBWT_TGT_DEBUG") ? atoi(getenv("CMSBWT_TGT_DEBUG")) : 0)};
+  CounterArgs A{it, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n, 0u};
   hipLaunchKernelGGL(k_counter_tgt, dim3(nw), dim3(256), 0, st, A);
 }
 void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st) {
@@ -2231,33 +2032,12 @@ void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, h
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st) {
   hipLaunchKernelGGL(k_bucket, g1(n), dim3(256), 0, st, countIncl, hasHead, n, bucket);
 }
-static WriterArgs writer_args(const WriterIn& w) {
-  return WriterArgs{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.count, w.headBase, w.bwtHeads, w.counter,
-                    w.n, w.E, w.rle, w.bwtSlot, w.P0, w.P1};
-}
-void mk_seg_count(const WriterIn& w, unsigned long long* segN, hipStream_t st) {
-  WriterArgs A = writer_args(w);
-  hipLaunchKernelGGL(k_seg_count, g1(w.n), dim3(256), 0, st, A, segN);
-}
-void mk_seg_emit(const WriterIn& w, const unsigned long long* segOff, uint8_t* sc, unsigned long long* sn,
-                 hipStream_t st) {
-  WriterArgs A = writer_args(w);
-  hipLaunchKernelGGL(k_seg_emit, g1(w.n), dim3(256), 0, st, A, segOff, sc, sn);
-}
-void mk_wr_count(const WriterIn& w, uint32_t U, uint32_t* runs, unsigned long long* sym, uint32_t* hl, hipStream_t st) {
-  if (U) hipLaunchKernelGGL(k_wr_count, g1(U), dim3(256), 0, st, writer_args(w), U, runs, sym, hl);
-}
 void mk_wr_adjust(const uint32_t* hl, const uint32_t* prevHL, uint32_t U, uint32_t* runs, hipStream_t st) {
   if (U) hipLaunchKernelGGL(k_wr_adjust, g1(U), dim3(256), 0, st, hl, prevHL, U, runs);
 }
-void mk_wr_emit(const WriterIn& w, uint32_t U, const unsigned long long* runOff, const unsigned long long* symOff,
-                const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st) {
-  if (U) hipLaunchKernelGGL(k_wr_emit, g1(U), dim3(256), 0, st, writer_args(w), U, runOff, symOff, prevHL, runStart,
-                            runChar);
-}
 static ElemArgs elem_args(const ElemIn& w) {
   return ElemArgs{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.itemOfSlot, w.headBase, w.elemBase, w.rOf,
-                  w.bwtHeads, w.counter, w.cum, w.info1, w.info2, w.n, w.E, w.H, w.rle};
+                  w.bwtHeads, w.counter, w.cum, w.info1, w.info2, w.n, w.E, w.H, w.rle, w.bwtSlot};
 }
 void mk_el_info(const ElemIn& w, hipStream_t st) {
   if (w.n) hipLaunchKernelGGL(k_el_info, g1(w.n), dim3(256), 0, st, w.sa, w.bwt, w.bucket, w.posBegin, w.slot,
@@ -2277,6 +2057,30 @@ void mk_el_wr_emit(const ElemIn& w, uint32_t V, const unsigned long long* runOff
                    const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st) {
   if (V) hipLaunchKernelGGL(k_el_wr_emit, g1(V), dim3(256), 0, st, elem_args(w), V, runOff, symOff, prevHL, runStart,
                             runChar);
+}
+void mk_dm_el_count(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t E,
+                    uint32_t P0, uint32_t P1, uint32_t* m, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_dm_el_count, g1(n), dim3(256), 0, st, sa, posBegin, slot, n, E, P0, P1, m);
+}
+void mk_dm_el_info(const ElemIn& w, uint32_t P0, uint32_t P1, hipStream_t st) {
+  if (w.n) hipLaunchKernelGGL(k_dm_el_info, g1(w.n), dim3(256), 0, st, w.sa, w.bwt, w.bucket, w.posBegin, w.slot,
+                              w.elemBase, w.n, w.E, P0, P1, w.info1, w.info2);
+}
+void mk_dm_el_adj(const uint32_t* rOf, const uint32_t* hl, const uint32_t* runs, uint32_t V, uint32_t* adj,
+                  hipStream_t st) {
+  if (V) hipLaunchKernelGGL(k_dm_el_adj, g1(V), dim3(256), 0, st, rOf, hl, runs, V, adj);
+}
+void mk_dm_el_units(const uint32_t* elemBase, const uint32_t* m, const unsigned long long* runIn,
+                    const unsigned long long* symIn, const uint32_t* hl, uint32_t n, uint32_t E, uint32_t U,
+                    int64_t* out, hipStream_t st) {
+  if (U) hipLaunchKernelGGL(k_dm_el_units, g1(U), dim3(256), 0, st, elemBase, m, runIn, symIn, hl, n, E, U, out);
+}
+void mk_dm_el_emit(const ElemIn& w, uint32_t V, const unsigned long long* runIn, const unsigned long long* symIn,
+                   const unsigned long long* unitRunOff, const unsigned long long* unitSymOff, const uint32_t* prevHL,
+                   const uint32_t* unitHL, const uint32_t* hl, unsigned long long* runStart, uint8_t* runChar,
+                   hipStream_t st) {
+  if (V) hipLaunchKernelGGL(k_dm_el_emit, g1(V), dim3(256), 0, st, elem_args(w), V, w.elemBase, runIn, symIn,
+                            unitRunOff, unitSymOff, prevHL, unitHL, hl, runStart, runChar);
 }
 void mk_grp_seg(const uint32_t* posS, const uint32_t* hb, const HeadKV* kv, uint32_t H, int bN, int bL,
                 unsigned long long* key, uint32_t* perm, uint32_t* tsOut, uint8_t* smOut, uint32_t* bigList,
@@ -2319,17 +2123,6 @@ void mk_scatter_kp(const uint32_t* idx, uint32_t B, const unsigned long long* ke
 void mk_wr_records(const unsigned long long* runStart, const uint8_t* runChar, uint64_t R, unsigned long long total,
                    uint8_t* out, hipStream_t st) {
   if (R) hipLaunchKernelGGL(k_wr_records, g1(R), dim3(256), 0, st, runStart, runChar, R, total, out);
-}
-void mk_run_flags(const uint8_t* sc, uint64_t S, unsigned long long* flag, hipStream_t st) {
-  if (S) hipLaunchKernelGGL(k_run_flags, g1(S), dim3(256), 0, st, sc, S, flag);
-}
-void mk_run_pack(const uint8_t* sc, const unsigned long long* runId, const unsigned long long* cum, uint64_t S,
-                 unsigned long long* runEnd, uint8_t* runChar, hipStream_t st) {
-  if (S) hipLaunchKernelGGL(k_run_pack, g1(S), dim3(256), 0, st, sc, runId, cum, S, runEnd, runChar);
-}
-void mk_run_records(const unsigned long long* runEnd, const uint8_t* runChar, uint64_t R, uint8_t* out,
-                    hipStream_t st) {
-  if (R) hipLaunchKernelGGL(k_run_records, g1(R), dim3(256), 0, st, runEnd, runChar, R, out);
 }
 
 }  // namespace cmsbwt

@@ -6,27 +6,9 @@
 
 namespace cmsbwt {
 
-struct WriterIn {
-  const int32_t* sa;
-  const uint8_t* bwt;
-  const int64_t* bucket;
-  const uint32_t* posBegin;
-  const uint32_t* slot;
-  const uint32_t* count;
-  const uint32_t* headBase;
-  const uint8_t* bwtHeads;
-  const unsigned long long* counter;
-  uint32_t n;
-  uint32_t E;
-  int rle;
-  const uint8_t* bwtSlot = nullptr;  // sharded merge: head characters by local slot
-  uint32_t P0 = 0, P1 = 0;           // sharded merge: owned position range
-};
 
 void mk_iota(uint32_t* p, uint64_t n, hipStream_t st);
 void mk_gather(const uint32_t* src, const uint32_t* perm, uint32_t* dst, uint64_t n, hipStream_t st);
-void mk_item_key(const uint32_t* len, const uint8_t* sm, const uint32_t* perm, uint32_t* key, uint64_t n,
-                 hipStream_t st);
 void mk_item_flags(const uint32_t* perm, const HeadsSoA& h, uint32_t* flag, uint64_t H, hipStream_t st);
 void mk_group_key(const HeadsSoA& h, uint64_t H, int bN, int bL, unsigned long long* key, hipStream_t st);
 // grouping, position first (radix by pos, then per-position segments)
@@ -86,32 +68,25 @@ void mk_check_items(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t
                     unsigned long long* viol, hipStream_t st);
 void mk_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t E,
                   uint32_t* itemsSA, uint32_t* headsSA, hipStream_t st);
-void mk_ranks(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uint32_t* posBegin,
-              const uint32_t* isaRef, const uint32_t* itemRankBase, const uint32_t* headBase, uint32_t n,
-              uint32_t E, int32_t* T, uint32_t* sa, uint32_t* grp, hipStream_t st);
-void mk_active_count(const ItemsSoA& it, uint32_t K, uint32_t n, uint32_t* c, hipStream_t st);
-void mk_active_init(const ItemsSoA& it, uint32_t K, uint32_t n, const uint32_t* isaRef,
-                    const uint32_t* posBegin, const uint32_t* headBase, const uint32_t* actOff,
-                    uint32_t* act, hipStream_t st);
 void mk_dbl_keys(const uint32_t* act, const uint32_t* sa, const uint32_t* grp, uint32_t h, uint32_t U,
                  uint64_t* key, uint32_t* val, hipStream_t st);
 void mk_dbl_apply(const uint32_t* act, const uint64_t* key, const uint32_t* val, uint32_t U, uint32_t* sa,
                   uint32_t* lab, hipStream_t st);
 void mk_dbl_groups(const uint32_t* act, const uint64_t* key, const uint32_t* val, const uint32_t* labMax,
                    uint32_t U, uint32_t* grp, uint32_t* keep, hipStream_t st);
-void mk_head_ranks(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint32_t* headRank, uint8_t* bwtHeads,
-                   hipStream_t st);
-// map order of each position's items (one thread per position)
 // u32 plus scans over tiles of 2048 (tile sums, their scan, the tiles)
 uint64_t scan_tiles(uint64_t n);
 void mk_scan_sums(const uint32_t* in, uint64_t n, uint32_t* sums, hipStream_t st);
 void mk_scan_tiles(const uint32_t* in, uint32_t* out, uint64_t n, const uint32_t* tileOff, uint32_t init,
                    bool inclusive, hipStream_t st);
-// order-preserving compaction of flagged u32 values (tiles of 2048)
+// order-preserving compaction of flagged u32 values (tiles of 2048); `out`
+// must not alias `in` (k_sel_write reads in[] after other blocks may have
+// written their compacted values)
 uint32_t sel_tiles(uint32_t n);
 void mk_sel_count(const uint32_t* flags, uint32_t n, uint32_t* tileCnt, hipStream_t st);
 void mk_sel_write(const uint32_t* in, const uint32_t* flags, uint32_t n, const uint32_t* tileOff, uint32_t* out,
                   hipStream_t st);
+// map order of each position's items (one thread per position)
 void mk_map_order(const uint32_t* posBegin, const uint32_t* len, const uint8_t* sm, uint32_t n, uint32_t* order,
                   hipStream_t st);
 // per-group doubling round (small groups sorted by one thread each)
@@ -124,14 +99,9 @@ void mk_dbl_small2(const uint32_t* gflag, uint32_t U, const uint32_t* act, uint6
 void mk_dbl_rank(uint32_t U, const uint32_t* act, const uint64_t* key, const uint32_t* val, uint32_t* sa,
                  uint32_t* grp, uint32_t* keep, uint32_t* bigList, uint32_t maxSmall, hipStream_t st);
 void mk_dbl_gstart(const uint64_t* key, uint32_t U, uint32_t* flag, hipStream_t st);
-void mk_dbl_small(const uint32_t* gs, uint32_t G, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val,
-                  uint32_t* sa, uint32_t* grp, uint32_t* keep, uint32_t* big, uint32_t maxSmall, hipStream_t st);
 void mk_dbl_gather_big(const uint32_t* orig, uint32_t B, const uint32_t* act, const uint64_t* key, const uint32_t* val,
                        uint32_t* actB, uint64_t* keyB, uint32_t* valB, hipStream_t st);
 void mk_scatter_u32(const uint32_t* src, const uint32_t* idx, uint32_t n, uint32_t* dst, hipStream_t st);
-void mk_nhr_keys(const ItemsSoA& it, uint32_t K, const uint32_t* perm, const uint32_t* headRank,
-                 const uint16_t* nexthead, uint64_t* key, hipStream_t st);
-void mk_low32(const uint64_t* key, uint32_t* out, uint64_t n, hipStream_t st);
 void mk_win_flags(const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t P0, uint32_t P1,
                   uint32_t winPos, uint32_t slotCap, uint32_t* flag, hipStream_t st);
 void mk_win_starts(const uint32_t* flag, const uint32_t* winIncl, uint32_t n, uint32_t* winStart, hipStream_t st);
@@ -150,11 +120,9 @@ void mk_counter_tgt(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t
                     unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st);
 void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st);
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st);
-// run writer: units = E end phrases + SA ranks 1..n-1
-void mk_wr_count(const WriterIn& w, uint32_t U, uint32_t* runs, unsigned long long* sym, uint32_t* hl, hipStream_t st);
+// run writer: units = E end phrases + SA ranks 1..n-1 (sharded merge), or
+// elements (one GPU); a unit's / element's first run joins the previous one
 void mk_wr_adjust(const uint32_t* hl, const uint32_t* prevHL, uint32_t U, uint32_t* runs, hipStream_t st);
-void mk_wr_emit(const WriterIn& w, uint32_t U, const unsigned long long* runOff, const unsigned long long* symOff,
-                const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st);
 void mk_wr_records(const unsigned long long* runStart, const uint8_t* runChar, uint64_t R, unsigned long long total,
                    uint8_t* out, hipStream_t st);
 // element writer (one GPU): one thread per end phrase / head / head-less SA rank
@@ -175,6 +143,7 @@ struct ElemIn {
   unsigned long long* info2;
   uint32_t n, E, H;
   int rle;
+  const uint8_t* bwtSlot = nullptr;  // sharded merge: head characters by local slot
 };
 void mk_el_info(const ElemIn& w, hipStream_t st);
 void mk_el_count(const uint32_t* headBase, uint32_t n, uint32_t E, uint32_t H, uint32_t* m, hipStream_t st);
@@ -183,14 +152,20 @@ void mk_el_wr_count(const ElemIn& w, uint32_t V, uint32_t* runs, unsigned long l
                     hipStream_t st);
 void mk_el_wr_emit(const ElemIn& w, uint32_t V, const unsigned long long* runOff, const unsigned long long* symOff,
                    const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st);
-void mk_seg_count(const WriterIn& w, unsigned long long* segN, hipStream_t st);
-void mk_seg_emit(const WriterIn& w, const unsigned long long* segOff, uint8_t* sc, unsigned long long* sn,
-                 hipStream_t st);
-void mk_run_flags(const uint8_t* sc, uint64_t S, unsigned long long* flag, hipStream_t st);
-void mk_run_pack(const uint8_t* sc, const unsigned long long* runId, const unsigned long long* cum, uint64_t S,
-                 unsigned long long* runEnd, uint8_t* runChar, hipStream_t st);
-void mk_run_records(const unsigned long long* runEnd, const uint8_t* runChar, uint64_t R, uint8_t* out,
-                    hipStream_t st);
+// element writer of the position-sharded merge (elements of the owned SA
+// ranks, units summarised for the all-reduce, emission per element)
+void mk_dm_el_count(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t E,
+                    uint32_t P0, uint32_t P1, uint32_t* m, hipStream_t st);
+void mk_dm_el_info(const ElemIn& w, uint32_t P0, uint32_t P1, hipStream_t st);
+void mk_dm_el_adj(const uint32_t* rOf, const uint32_t* hl, const uint32_t* runs, uint32_t V, uint32_t* adj,
+                  hipStream_t st);
+void mk_dm_el_units(const uint32_t* elemBase, const uint32_t* m, const unsigned long long* runIn,
+                    const unsigned long long* symIn, const uint32_t* hl, uint32_t n, uint32_t E, uint32_t U,
+                    int64_t* out, hipStream_t st);
+void mk_dm_el_emit(const ElemIn& w, uint32_t V, const unsigned long long* runIn, const unsigned long long* symIn,
+                   const unsigned long long* unitRunOff, const unsigned long long* unitSymOff, const uint32_t* prevHL,
+                   const uint32_t* unitHL, const uint32_t* hl, unsigned long long* runStart, uint8_t* runChar,
+                   hipStream_t st);
 
 // dist_kernels.hip: position-sharded merge (multi-GPU)
 void mk_dm_owner(const uint32_t* vals, const uint32_t* idx, uint64_t n, const uint32_t* split, uint32_t world,
@@ -215,8 +190,9 @@ void mk_dm_dbl_apply(const uint32_t* aPerm, const uint32_t* act, const uint32_t*
                      uint32_t* keep, hipStream_t st);
 void mk_dm_pack_ranks(const uint32_t* perm, const uint32_t* grp, const uint16_t* nexthead, uint64_t n, uint32_t H,
                       int32_t* out, uint32_t* err, hipStream_t st);
+// head characters by slot (bwtSlot) and the next-head ranks in received order (nbi)
 void mk_dm_load_ranks(const int32_t* in, const uint32_t* Pm, const uint32_t* itemOfSlot, const ItemsSoA& it,
-                      const uint32_t* gItem, const uint8_t* lchar, uint32_t H, uint32_t* nhr, uint8_t* bwtSlot,
+                      const uint32_t* gItem, const uint8_t* lchar, uint32_t H, uint32_t* nbi, uint8_t* bwtSlot,
                       uint32_t* err, hipStream_t st);
 void mk_dm_halo_count(const ItemsSoA& it, uint32_t K, const uint32_t* split, uint32_t world, uint32_t rank,
                       uint32_t n, uint32_t* c, hipStream_t st);

@@ -1,279 +1,16 @@
-// ms_walk.hip — the matching-statistics walk and head finalisation on gfx950.
+// ms_walk.hip — the walk's bookkeeping around k_ms_walk2 (ms_walk2.hip) and
+// head finalisation on gfx950.
 //
-// Reference semantics (CMS-BWT-functions.cpp = FN):
-//   adjustInterval FN:11-25, contractLeft FN:34-43, computeMSFactorAt FN:45-88,
-//   binarySearchLB/RB FN:94-149, PSV/NSV rmq_tree.h:184-225, per-document walk
-//   FN:1151-1212, j-scan FN:1359-1385, buckets FN:1162-1185.
-//
-// Parallel decomposition: the MS triple (pos, len,
-// smaller) at a position is a function of the text suffix alone, so every
-// document is cut into chunks of `chunk` positions, one lane per chunk.  A
-// chunk [a, b) restarts from the SA root at a-1 (to learn pos(a-1) for the
-// head test at a) and walks exactly as the reference does.  Two hot loops of
-// the reference are replaced by equivalent logarithmic/wide forms:
-//   * the PLCP skip loop `while (len > PLCP[pos+1])` (FN:1176-1185) is a
-//     search for the first q >= pos+1 with PLCP[q] + q >= len + pos + 1;
-//     PLCP[q] + q is non-decreasing (the longest repeated prefix shrinks by at
-//     most one per position), so it is a galloping search;
-//   * the singleton-interval extension compares 8 bytes per step (LCE).
-// Per-position bucket updates become one run (pos, length) per head, turned
-// into counts by a difference array (no per-character atomics).
+// Reference semantics (CMS-BWT-functions.cpp = FN): per-document walk
+// FN:1151-1212 (pool records -> document order, end-of-document phrases),
+// j-scan FN:1359-1385 (k_finalize), buckets FN:1162-1185 (run difference
+// arrays through position bins).
 #include <algorithm>
 
 #include "device_common.h"
 #include "kernels.h"
 
 namespace cmsbwt {
-
-// ------------------------------------------------------------ PSV / NSV
-// psv(i, ub) = max{j <= i : lcp[j] < ub} or -1   (rmq_tree.h:184-205)
-__device__ __forceinline__ int32_t d_psv(const DevRef& R, int32_t i, int32_t ub) {
-  const int32_t* a = R.lcp;
-  int32_t bs = i & ~63;
-  for (int32_t j = i; j >= bs; --j)
-    if (a[j] < ub) return j;
-  uint32_t idx = (uint32_t)i >> 6;
-  int L = 0;
-  int64_t found = -1;
-  for (; L < R.nlvl; ++L) {
-    const int32_t* m = R.lvl[L];
-    int64_t start = idx & ~63u;
-    for (int64_t k = (int64_t)idx - 1; k >= start; --k)
-      if (m[k] < ub) { found = k; break; }
-    if (found >= 0 || start == 0) break;
-    idx >>= 6;
-  }
-  if (found < 0) return -1;
-  uint32_t b = (uint32_t)found;
-  for (int l = L - 1; l >= 0; --l) {
-    const int32_t* m = R.lvl[l];
-    int64_t hi = min((int64_t)b * 64 + 63, (int64_t)R.lvlLen[l] - 1);
-    for (int64_t k = hi; k >= (int64_t)b * 64; --k)
-      if (m[k] < ub) { b = (uint32_t)k; break; }
-  }
-  int64_t hi = min((int64_t)b * 64 + 63, (int64_t)R.n - 1);
-  for (int64_t k = hi; k >= (int64_t)b * 64; --k)
-    if (a[k] < ub) return (int32_t)k;
-  return -1;
-}
-
-// nsv(i, ub) = min{j >= i, j < n : lcp[j] < ub} or -1   (rmq_tree.h:208-225)
-__device__ __forceinline__ int32_t d_nsv(const DevRef& R, int32_t i, int32_t ub) {
-  const int32_t* a = R.lcp;
-  const int64_t n = R.n;
-  if ((int64_t)i >= n) return -1;
-  int64_t be = min((int64_t)(i | 63) + 1, n);
-  for (int64_t j = i; j < be; ++j)
-    if (a[j] < ub) return (int32_t)j;
-  uint32_t idx = (uint32_t)i >> 6;
-  int L = 0;
-  int64_t found = -1;
-  for (; L < R.nlvl; ++L) {
-    const int32_t* m = R.lvl[L];
-    int64_t end = min((int64_t)(idx | 63u) + 1, (int64_t)R.lvlLen[L]);
-    for (int64_t k = (int64_t)idx + 1; k < end; ++k)
-      if (m[k] < ub) { found = k; break; }
-    if (found >= 0 || end == (int64_t)R.lvlLen[L]) break;
-    idx >>= 6;
-  }
-  if (found < 0) return -1;
-  uint32_t b = (uint32_t)found;
-  for (int l = L - 1; l >= 0; --l) {
-    const int32_t* m = R.lvl[l];
-    int64_t end = min((int64_t)b * 64 + 64, (int64_t)R.lvlLen[l]);
-    for (int64_t k = (int64_t)b * 64; k < end; ++k)
-      if (m[k] < ub) { b = (uint32_t)k; break; }
-  }
-  int64_t end = min((int64_t)b * 64 + 64, n);
-  for (int64_t k = (int64_t)b * 64; k < end; ++k)
-    if (a[k] < ub) return (int32_t)k;
-  return -1;
-}
-
-// FN:11-25
-__device__ __forceinline__ void d_adjust(const DevRef& R, int32_t lo, int32_t hi, int32_t off,
-                                         int32_t& nl, int32_t& nr) {
-  int32_t p = d_psv(R, lo, off);
-  nl = p == -1 ? 0 : p;
-  int32_t q = d_nsv(R, hi + 1, off);
-  nr = q == -1 ? (int32_t)R.n - 1 : q - 1;
-}
-
-// FN:34-43
-__device__ __forceinline__ void d_contract(const DevRef& R, int32_t& lo, int32_t& hi, int32_t off) {
-  uint32_t sl = (uint32_t)R.sa[lo], sh = (uint32_t)R.sa[hi];
-  if (sl == R.n - 1 || sh == R.n - 1) { lo = 0; hi = (int32_t)R.n - 1; return; }
-  d_adjust(R, (int32_t)R.isa[sl + 1], (int32_t)R.isa[sh + 1], off, lo, hi);
-}
-
-// First m in [lo, hi+1) with x[SA[m]+off] >= c (FN:94-120 returns this index
-// when the symbol is present, else -(this index)-1).
-__device__ __forceinline__ int32_t d_lower(const DevRef& R, int32_t lo, int32_t hi, uint32_t off, uint8_t c) {
-  int32_t a = lo, b = hi + 1;
-  while (a < b) {
-    int32_t m = (a + b) >> 1;
-    if (R.x[(uint32_t)R.sa[m] + off] < c) a = m + 1; else b = m;
-  }
-  return a;
-}
-// First m in [lo, hi+1) with x[SA[m]+off] > c (FN:123-149 returns this - 1).
-__device__ __forceinline__ int32_t d_upper(const DevRef& R, int32_t lo, int32_t hi, uint32_t off, uint8_t c) {
-  int32_t a = lo, b = hi + 1;
-  while (a < b) {
-    int32_t m = (a + b) >> 1;
-    if (R.x[(uint32_t)R.sa[m] + off] <= c) a = m + 1; else b = m;
-  }
-  return a;
-}
-
-// 8 bytes starting at an arbitrary address (both buffers are padded).
-__device__ __forceinline__ uint64_t d_load8(const uint8_t* p) {
-  uintptr_t a = (uintptr_t)p;
-  const uint64_t* w = (const uint64_t*)(a & ~(uintptr_t)7);
-  uint32_t s = (uint32_t)(a & 7) * 8;
-  uint64_t lo = w[0];
-  if (s == 0) return lo;
-  uint64_t hi = w[1];
-  return (lo >> s) | (hi << (64 - s));
-}
-
-// Longest common extension of x[q..] and t[j..]: stops at the first mismatch,
-// which always exists (the document separator 0x02 is absent from x).
-__device__ __forceinline__ uint32_t d_lce(const uint8_t* xq, const uint8_t* tj) {
-  uint64_t d = d_load8(xq) ^ d_load8(tj);
-  if (d) return (uint32_t)(__builtin_ctzll(d) >> 3);
-  uint32_t k = 8;
-  while (true) {  // 32 bytes per step, loads issued together
-    uint64_t d0 = d_load8(xq + k) ^ d_load8(tj + k);
-    uint64_t d1 = d_load8(xq + k + 8) ^ d_load8(tj + k + 8);
-    uint64_t d2 = d_load8(xq + k + 16) ^ d_load8(tj + k + 16);
-    uint64_t d3 = d_load8(xq + k + 24) ^ d_load8(tj + k + 24);
-    if (d0) return k + (uint32_t)(__builtin_ctzll(d0) >> 3);
-    if (d1) return k + 8 + (uint32_t)(__builtin_ctzll(d1) >> 3);
-    if (d2) return k + 16 + (uint32_t)(__builtin_ctzll(d2) >> 3);
-    if (d3) return k + 24 + (uint32_t)(__builtin_ctzll(d3) >> 3);
-    k += 32;
-  }
-}
-
-// Smallest s >= 0 with len - s <= PLCP[base + s]  (FN:1176 loop exit).
-// With q = base + s the condition is PLCP[q] + q >= base + len =: T, and
-// PLCP[q] + q is non-decreasing, so the answer is the first q in [base, T]
-// crossing T.  PLCP is short outside long repeats, so the crossing almost
-// always lies in the 16 entries just below T: probe that window with
-// independent loads first, gallop from `base` only when it does not.
-__device__ __forceinline__ uint32_t d_skip(const DevRef& R, uint32_t base, uint32_t len) {
-  const int32_t* P = R.plcp;
-  if ((int64_t)len <= (int64_t)P[base]) return 0;
-  const int64_t T = (int64_t)base + len;
-  if (len > 16) {
-    const int64_t w0 = T - 16;  // > base
-    if ((int64_t)P[w0] + w0 < T) {  // crossing inside (w0, T]: count entries below T
-      uint32_t c = 0;
-#pragma unroll
-      for (int k = 1; k <= 16; k++) c += ((int64_t)P[w0 + k] + w0 + k < T) ? 1u : 0u;
-      return (uint32_t)(w0 + 1 + c - base);
-    }
-  }
-  uint32_t lo = 0, hi, step = 1;
-  while (true) {
-    uint64_t t = (uint64_t)lo + step;
-    if (t >= len) { hi = len; break; }
-    if ((int64_t)len - (int64_t)t <= (int64_t)P[base + (uint32_t)t]) { hi = (uint32_t)t; break; }
-    lo = (uint32_t)t;
-    step <<= 1;
-  }
-  while (hi - lo > 1) {
-    uint32_t mid = lo + ((hi - lo) >> 1);
-    if ((int64_t)len - (int64_t)mid <= (int64_t)P[base + mid]) hi = mid; else lo = mid;
-  }
-  return hi;
-}
-
-// ------------------------------------------------------------ MS walk kernel
-__global__ void __launch_bounds__(256) k_ms_walk(DevRef R, const uint8_t* __restrict__ text,
-                                                 const uint64_t* __restrict__ docOff,
-                                                 const Chunk* __restrict__ chunks, uint32_t nchunks,
-                                                 const uint32_t* __restrict__ laneChunk,
-                                                 Pool pool, uint32_t* __restrict__ chunkCount) {
-  const uint32_t lane_id = blockIdx.x * blockDim.x + threadIdx.x;
-  if (lane_id >= nchunks) return;
-  const uint32_t cid = laneChunk[lane_id];
-  const Chunk ch = chunks[cid];
-  const uint8_t* t = text + docOff[ch.doc];
-  const uint32_t a = ch.a, b = ch.b;
-  const uint32_t n = R.n;
-  uint32_t count = 0, blk = 0xffffffffu, fill = kPoolB, seq = 0;
-
-  uint32_t i = a > 0 ? a - 1 : 0;
-  uint32_t len = 0, pos = n - 1;
-  int32_t lb = 0, rb = (int32_t)n - 1;
-  uint64_t prevPos = (uint64_t)-2;
-  bool smaller = false;
-  while (i < b) {
-    // ---- computeMSFactorAt (FN:45-88)
-    {
-      uint32_t off = len, j = i + off;
-      int32_t nlb = lb, nrb = rb;
-      while (true) {
-        if (nlb == nrb) {
-          uint32_t q = (uint32_t)R.sa[nlb];
-          uint32_t m = d_lce(R.x + q + off, t + j);
-          off += m;
-          j += m;
-          smaller = (int8_t)R.x[q + off] > (int8_t)t[j];
-          pos = q;
-          break;
-        }
-        uint8_t c = t[j];
-        int32_t l2 = d_lower(R, nlb, nrb, off, c);
-        if (l2 > nrb || R.x[(uint32_t)R.sa[l2] + off] != c) {
-          int32_t mm = l2;
-          smaller = true;
-          if (mm == nrb + 1) { mm = nrb; smaller = false; }
-          pos = (uint32_t)R.sa[mm];
-          break;
-        }
-        int32_t r2 = d_upper(R, l2, nrb, off, c) - 1;
-        nlb = l2; nrb = r2;
-        lb = nlb; rb = nrb;
-        off++; j++;
-      }
-      len = off;
-    }
-    // ---- head test and record (FN:1154-1171)
-    if (i >= a && (uint64_t)pos != prevPos + 1) {
-      if (fill == kPoolB) {
-        blk = atomicAdd(pool.used, 1u);
-        fill = 0;
-        if (blk < pool.capBlocks) { pool.blkChunk[blk] = cid; pool.blkSeq[blk] = seq; }
-        seq++;
-      }
-      if (blk < pool.capBlocks) {
-        HeadRec r;
-        r.start = i;
-        r.pos = pos;
-        r.len = len;
-        r.flags = smaller ? 1u : 0u;
-        pool.rec[(uint64_t)blk * kPoolB + fill] = r;
-      }
-      fill++;
-      count++;
-    }
-    len--;
-    if (lb == rb) {  // FN:1175-1189
-      uint32_t s = d_skip(R, pos + 1, len);
-      i += s; len -= s; pos += s;
-      int32_t v = (int32_t)R.isa[pos + 1];
-      d_adjust(R, v, v, (int32_t)len, lb, rb);
-    } else {         // FN:1190-1194
-      d_contract(R, lb, rb, (int32_t)len);
-    }
-    i++;
-    prevPos = pos;
-  }
-  chunkCount[cid] = count;
-}
 
 // ------------------------------------------------------------ pool -> idx order
 __global__ void k_chunk_with_end(const Chunk* __restrict__ chunks, const uint32_t* __restrict__ chunkCount,
@@ -477,14 +214,6 @@ __global__ __launch_bounds__(1024) void k_run_bin_emit(const uint32_t* __restric
 }
 
 // ------------------------------------------------------------ host launchers
-void launch_ms_walk(const DevRef& R, const uint8_t* text, const uint64_t* docOff, const Chunk* chunks,
-                    uint32_t nchunks, const uint32_t* laneChunk, const Pool& pool, uint32_t* chunkCount,
-                    hipStream_t st) {
-  if (!nchunks) return;
-  hipLaunchKernelGGL(k_ms_walk, dim3((nchunks + 255) / 256), dim3(256), 0, st, R, text, docOff, chunks,
-                     nchunks, laneChunk, pool, chunkCount);
-}
-
 void launch_chunk_with_end(const Chunk* chunks, const uint32_t* chunkCount, uint32_t nch, unsigned long long* out,
                            hipStream_t st) {
   if (nch) hipLaunchKernelGGL(k_chunk_with_end, dim3((nch + 255) / 256), dim3(256), 0, st, chunks, chunkCount, nch, out);

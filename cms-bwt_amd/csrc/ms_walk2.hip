@@ -253,17 +253,11 @@ struct Walk2Args {
   unsigned long long* stats;  // STATS builds: per-phase lane-steps, wave-steps, ...
 };
 
-#ifndef CMSBWT_COOP_J
-#define CMSBWT_COOP_J 4
-#endif
-constexpr uint32_t kCoopJ = CMSBWT_COOP_J;  // 16-B pieces per thread per cooperative round
-#ifndef CMSBWT_COOP_ADAPT
-#define CMSBWT_COOP_ADAPT 1
-#endif
-constexpr bool kCoopAdapt = CMSBWT_COOP_ADAPT;  // first round 1 KiB per slot, then doubling
-
+constexpr uint32_t kCoopJ = 4;  // 16-B pieces per thread per cooperative round
+// waves per SIMD of the walk (Makefile W2WAVES; measured 3 -> 16.50 ms,
+// 4 -> 16.44-16.68, 5 -> 16.9, 6 -> 31.3 with register spills)
 #ifndef CMSBWT_W2_WAVES
-#define CMSBWT_W2_WAVES 6
+#define CMSBWT_W2_WAVES 4
 #endif
 template <bool STATS>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CMSBWT_W2_WAVES, 8)))
@@ -1031,7 +1025,7 @@ k_ms_walk2(Walk2Args A) {
       // rounds double up to kCoopJ pieces (a lane's remaining match is
       // usually shorter than 1 KiB: no over-read on the common case)
       uint32_t run = 0, open = (1u << S) - 1;  // open: slots still comparing
-      uint32_t jr = kCoopAdapt ? (S < kCoopJ ? S : kCoopJ) : kCoopJ;
+      uint32_t jr = S < kCoopJ ? S : kCoopJ;
       while (open) {
         uint32_t mine = 16, mj = 0, cc = 0;  // this thread's first mismatch: piece, offset, chars
         // one round of JR pieces (fixed-size arrays: no register spills)
@@ -1052,8 +1046,8 @@ k_ms_walk2(Walk2Args A) {
           }
         };
         if ((open >> g) & 1) {
-          if (kCoopJ >= 4 && jr == 4) cmp_round(std::integral_constant<uint32_t, (kCoopJ >= 4 ? 4u : 1u)>{});
-          else if (kCoopJ >= 2 && jr == 2) cmp_round(std::integral_constant<uint32_t, (kCoopJ >= 2 ? 2u : 1u)>{});
+          if (jr == 4) cmp_round(std::integral_constant<uint32_t, 4u>{});
+          else if (jr == 2) cmp_round(std::integral_constant<uint32_t, 2u>{});
           else cmp_round(std::integral_constant<uint32_t, 1u>{});
         }
         if (STATS && lane == 0) atomicAdd(&sc[31], 1ull);

@@ -144,21 +144,23 @@ int cmsbwt_walk_import(cmsbwt_ctx* ctx, uint64_t heads, uint64_t ndocs, uint64_t
  * head-string group labels [1 + k*H/world, 1 + (k+1)*H/world).  Every
  * pointer is DEVICE memory of this context's GPU; the caller moves data
  * between the calls (cmsbwt/dist.py: all-to-all / all-reduce over RCCL):
- *   ms_walk; all-reduce "diff" (sum) and "hashead" (max) -> dm_begin
+ *   ms_walk; dm_begin
  *   dm_route_heads -> counts; dm_pack_heads -> 5 int32/head; all-to-all
- *   dm_group(recv) -> sa_counts[2n]; all-reduce(sum) -> dm_labels -> back
- *   (1 word per received head); reverse all-to-all -> dm_dbl_init
+ *   dm_group(recv) -> buf[3n+1] (items, heads per SA rank; run difference
+ *     array); all-reduce(sum) -> dm_labels -> back (1 word per received
+ *     head); reverse all-to-all -> dm_dbl_init
  *   while (all-reduced active > 0): dm_dbl_route(h) -> counts;
  *     dm_dbl_pack -> 2 words/element; all-to-all; dm_dbl_sort -> result;
  *     reverse all-to-all -> dm_dbl_apply; h *= 2
  *   dm_pack_ranks -> 2 words/head; all-to-all (head counts) -> dm_load_ranks
  *   dm_route_halo -> counts; dm_pack_halo -> 6 words/item + nhr words;
  *     all-to-all -> dm_counter -> {bad, good, nothing, violations, errors, items}
- *   dm_units -> int64[2*(E+n-1)]; all-reduce(sum) -> dm_emit -> nlocal;
+ *   dm_units -> int64[2*(E+n-1)]; all-reduce(sum) -> dm_emit -> nlocal
+ *     (rank 0: 0, its runs are placed directly);
  *   dm_copy_stream; gather to rank 0 -> dm_finish (rank 0) -> runs.
  * flags bit 0: every shard reported stats.order_invariant. */
 int cmsbwt_dm_begin(cmsbwt_ctx* ctx, uint32_t world, uint32_t rank, uint64_t heads_total, uint64_t docs_total,
-                    uint32_t flags, const int32_t* diff, const uint8_t* hashead, int rle);
+                    uint32_t flags, int rle);
 int cmsbwt_dm_route_heads(cmsbwt_ctx* ctx, uint64_t* counts);
 int cmsbwt_dm_pack_heads(cmsbwt_ctx* ctx, int32_t* out);
 int cmsbwt_dm_group(cmsbwt_ctx* ctx, const int32_t* recv, uint64_t nrecv, uint32_t* sa_counts);
@@ -181,6 +183,12 @@ int cmsbwt_dm_copy_stream(cmsbwt_ctx* ctx, uint64_t* starts, uint8_t* chars);
  * {heads, keys, ndocs, chars, bad, good, nothing, violations} over all ranks */
 int cmsbwt_dm_finish(cmsbwt_ctx* ctx, const uint64_t* const* starts, const uint8_t* const* chars,
                      const uint64_t* counts, const uint64_t* gstats);
+
+/* Self-test of the device scan / compaction primitives against host results
+ * (what = "exscan" | "inscan" | "select"; offset = element offset of both
+ * buffers, inplace = scan with out == in).  *mismatches = 0 when equal. */
+int cmsbwt_selftest(cmsbwt_ctx* ctx, const char* what, uint64_t n, uint64_t offset, int inplace,
+                    uint64_t* mismatches);
 
 /* Host-only helpers (no GPU needed), exposed for tests of the host logic:
  * the collection reader (FN:1138-1275) and the reference suffix array

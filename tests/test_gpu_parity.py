@@ -159,6 +159,19 @@ def test_walk_table_paths(engine, oracle, tmp_path, case, env):
     _compare(engine, oracle, tmp_path, case, env=env)
 
 
+@pytest.mark.parametrize("env", [{"CMSBWT_ROCPRIM_SCAN": "1"}, {"CMSBWT_ROCPRIM_SELECT": "1"},
+                                 {"CMSBWT_W2_STATS": "1", "CMSBWT_DBL_STATS": "1", "CMSBWT_COUNTER_STATS": "1",
+                                  "CMSBWT_TIMING": "1"},
+                                 {"CMSBWT_HOST_INDEX": "1"}],
+                         ids=["rocprim_scans", "rocprim_select", "instrumented", "host_index"])
+@pytest.mark.parametrize("case", cases.small_cases()[:4] + cases.small_cases()[-1:], ids=lambda c: c[0])
+def test_fallback_and_instrumented_paths(engine, oracle, tmp_path, case, env):
+    """rocPRIM scans / compaction instead of the tile kernels, the statistics
+    builds (the walk's STATS instantiation, doubling/counter counters, index
+    timing) and the host-built index all leave every stage bit-exact."""
+    _compare(engine, oracle, tmp_path, case, env=env)
+
+
 @pytest.mark.parametrize("case", cases.large_cases(), ids=lambda c: c[0])
 def test_large_reference_path(engine, oracle, tmp_path, case):
     _compare(engine, oracle, tmp_path, case, rle=True)
@@ -200,6 +213,28 @@ def test_bench_workload_generated_in_hbm_matches_files(engine, oracle, tmp_path)
     engine.load_synth(seed, 1, C, p, leading_empty_doc=True)
     engine.step(rle=True)
     assert engine.runs_bytes() == open(pre + "_o.rl_bwt", "rb").read()
+
+
+def test_bench_workload_full_size_golden(engine):
+    """bench.py's headline step at full size (synth.h: 10 MB ref + 1000 copies
+    @0.1 %, generated in HBM) equals the oracle's .rl_bwt on the same workload
+    written as FASTA by gen_synth (golden synth_c3: sha256, heads, Rank and
+    counter statistics; the oracle took 1675 s on one core)."""
+    import hashlib
+    import json
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(__file__)))
+    import bench
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["synth_c3"]
+    L, C, p, seed = g["args"]
+    engine.load_reference_bytes(bench.synth_reference(L, seed))
+    engine.load_synth(seed, 1, C, p, leading_empty_doc=True)
+    engine.step(rle=True)
+    st = engine.stats()
+    assert (st.heads, st.keys, st.rank, st.runs) == (g["headNumber"], g["keys"], g["Rank"], g["rl_runs"])
+    assert (st.counter_bad, st.counter_good, st.counter_nothing) == \
+        (g["counterBad"], g["counterGood"], g["counterDoNothing"])
+    assert hashlib.sha256(engine.runs_bytes()).hexdigest() == g["rl_bwt_sha256"]
 
 
 def test_repeated_steps_identical(engine, tmp_path):
