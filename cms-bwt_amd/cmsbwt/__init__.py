@@ -108,6 +108,8 @@ def load_library() -> ctypes.CDLL:
         "cmsbwt_load_reference": (I32, [P, VP, U64]),
         "cmsbwt_load_collection_file": (I32, [P, ctypes.c_char_p, U64]),
         "cmsbwt_load_collection": (I32, [P, VP, VP, U64]),
+        "cmsbwt_load_collection_file_range": (I32, [P, ctypes.c_char_p, ctypes.c_uint32, ctypes.c_uint32]),
+        "cmsbwt_host_shard_bounds": (I32, [ctypes.c_char_p, ctypes.c_uint32, VP]),
         "cmsbwt_load_collection_synth": (I32, [P, U64, U64, U64, ctypes.c_double, I32]),
         "cmsbwt_ms_walk": (I32, [P]),
         "cmsbwt_merge": (I32, [P, I32]),
@@ -157,7 +159,7 @@ EXPORTED = [
     "cmsbwt_load_collection", "cmsbwt_load_collection_synth", "cmsbwt_ms_walk", "cmsbwt_merge",
     "cmsbwt_step", "cmsbwt_get_stats", "cmsbwt_num_runs", "cmsbwt_copy_runs", "cmsbwt_write_output",
     "cmsbwt_copy_array", "cmsbwt_host_read_collection", "cmsbwt_host_suffix_array", "cmsbwt_walk_import",
-    "cmsbwt_selftest",
+    "cmsbwt_selftest", "cmsbwt_load_collection_file_range", "cmsbwt_host_shard_bounds",
     "cmsbwt_dm_begin", "cmsbwt_dm_route_heads", "cmsbwt_dm_pack_heads", "cmsbwt_dm_group", "cmsbwt_dm_labels",
     "cmsbwt_dm_dbl_init", "cmsbwt_dm_dbl_route", "cmsbwt_dm_dbl_pack", "cmsbwt_dm_dbl_sort", "cmsbwt_dm_dbl_apply",
     "cmsbwt_dm_pack_ranks", "cmsbwt_dm_load_ranks", "cmsbwt_dm_route_halo", "cmsbwt_dm_pack_halo",
@@ -234,6 +236,11 @@ class Engine:
 
     def load_collection_file(self, path: str, prefix: int = UINT64_MAX):
         self._chk(self._lib.cmsbwt_load_collection_file(self._ctx, path.encode(), prefix))
+
+    def load_collection_file_range(self, path: str, rank: int, world: int):
+        """This rank's documents of the collection file (byte-range shards,
+        cmsbwt_host_shard_bounds), read on the device."""
+        self._chk(self._lib.cmsbwt_load_collection_file_range(self._ctx, path.encode(), rank, world))
 
     def load_collection(self, docs):
         import numpy as np
@@ -413,6 +420,17 @@ def host_read_collection(path: str, prefix: int = UINT64_MAX):
         raise CmsBwtError(rc, f"cannot read {path}")
     raw = text.raw
     return [raw[int(off[k]):int(off[k + 1])] for k in range(nd.value)], sn.value
+
+
+def host_shard_bounds(path: str, world: int):
+    """Byte bounds of the collection shards (no GPU needed)."""
+    import numpy as np
+    lib = load_library()
+    out = np.zeros(world + 1, dtype=np.uint64)
+    rc = lib.cmsbwt_host_shard_bounds(path.encode(), world, out.ctypes.data)
+    if rc:
+        raise CmsBwtError(rc, f"cannot shard {path}")
+    return [int(x) for x in out]
 
 
 def host_suffix_array(s: bytes):

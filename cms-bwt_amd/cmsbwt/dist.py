@@ -172,6 +172,18 @@ class Transport:
         self.sync()
         return t
 
+    def counts_and_sum(self, send_counts, value):
+        """counts() plus the sum of `value` over all ranks, in one exchange."""
+        if self.world == 1:
+            return list(send_counts), int(value)
+        t = torch.tensor([[c, value] for c in send_counts], dtype=torch.int64)
+        out = torch.empty_like(t)
+        if not self.staged and self.device.type != "cpu":
+            t, out = t.to(self.device), out.to(self.device)
+        dist.all_to_all_single(out, t)
+        v = out.tolist()
+        return [int(a) for a, _ in v], sum(int(b) for _, b in v)
+
     def allgather_ints(self, vals):
         """[per-rank list of ints] for a list of ints of equal length."""
         if self.world == 1:
@@ -216,24 +228,24 @@ def sharded_merge(eng, x: Transport, rle: bool = True):
     eng.dm_group(recv.data_ptr(), Hp, sa.data_ptr())
     del recv
     x.allreduce(sa, "sum")
-    back = x.empty(Hp, i32)
+    back = x.empty(Hp, i64)  # label | unresolved << 32 (labels use all 32 bits)
     eng.dm_labels(sa.data_ptr(), back.data_ptr())
     del sa
     labels = x.a2a(back, rc, hc)
     U = eng.dm_dbl_init(labels.data_ptr())
     del back, labels
-    # 3. prefix doubling of the head string
+    # 3. prefix doubling of the head string (one count exchange per round
+    # also sums the unresolved members over ranks)
     h = 1
     while True:
-        tot = x.allgather_ints([U])
-        if sum(t[0] for t in tot) == 0:
-            break
         c = eng.dm_dbl_route(h, world)
+        r, active = x.counts_and_sum(c, U)
+        if active == 0:
+            break
         send = x.empty((U, 2), i32)
         eng.dm_dbl_pack(send.data_ptr())
-        r = x.counts(c)
         recv = x.a2a(send, c, r)
-        res = x.empty(sum(r), i32)
+        res = x.empty(sum(r), i64)
         eng.dm_dbl_sort(recv.data_ptr(), sum(r), res.data_ptr())
         back = x.a2a(res, r, c)
         U = eng.dm_dbl_apply(back.data_ptr())

@@ -83,12 +83,13 @@ __global__ void k_dm_sa_counts(const int32_t* __restrict__ sa, const uint32_t* _
 
 // Initial group label of every member (its item's first sa position in the
 // head-string suffix array, FN:1432-1453): end phrases get 1 + m, others
-// 1 + headBase[ISA[p]] + (slot offset inside p).  Bit 31: unresolved (item
-// with >= 2 members).  Written in received order for the return trip.
+// 1 + headBase[ISA[p]] + (slot offset inside p).  Bit 32: unresolved (item
+// with >= 2 members; labels use all 32 bits).  Written in received order for
+// the return trip.
 __global__ void k_dm_group_labels(const ItemsSoA it, const uint32_t* __restrict__ itemOfSlot,
                                   const uint32_t* __restrict__ Pm, uint32_t H, const uint32_t* __restrict__ posBegin,
                                   const uint32_t* __restrict__ isaRef, const uint32_t* __restrict__ headBase,
-                                  uint32_t n, uint32_t* __restrict__ back, uint32_t* __restrict__ gItem) {
+                                  uint32_t n, unsigned long long* __restrict__ back, uint32_t* __restrict__ gItem) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= H) return;
   const uint32_t q = itemOfSlot[s], sq = it.slot[q], m = s - sq, p = it.pos[q];
@@ -103,17 +104,18 @@ __global__ void k_dm_group_labels(const ItemsSoA it, const uint32_t* __restrict_
     g = gq;
     act = it.count[q] >= 2 ? 1u : 0u;
   }
-  back[Pm[s]] = g | (act << 31);
+  back[Pm[s]] = (unsigned long long)g | ((unsigned long long)act << 32);
 }
 
 // doc side: labels arrive in send order
-__global__ void k_dm_grp_init(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ in, uint64_t n,
+__global__ void k_dm_grp_init(const uint32_t* __restrict__ perm, const unsigned long long* __restrict__ in, uint64_t n,
                               uint32_t* __restrict__ grp, uint32_t* __restrict__ actFlag) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  const uint32_t i = perm[j], v = in[j];
-  grp[i] = v & 0x7fffffffu;
-  actFlag[i] = v >> 31;
+  const uint32_t i = perm[j];
+  const unsigned long long v = in[j];
+  grp[i] = (uint32_t)v;
+  actFlag[i] = (uint32_t)(v >> 32);
 }
 
 // doubling keys (group of suffix, group of suffix + h), send order; a
@@ -132,12 +134,69 @@ __global__ void k_dm_dbl_pack(const uint32_t* __restrict__ aPerm, const uint32_t
   out[2 * j + 1] = (int32_t)g2;
 }
 
-__global__ void k_dm_dbl_keys(const int32_t* __restrict__ in, uint64_t n, unsigned long long* __restrict__ key,
-                              uint32_t* __restrict__ val) {
+
+// label-range owner, first pass: members keyed by their label's offset in
+// the owned range [G0, G1) (the sort needs bits_for(G1 - G0) bits, not the
+// full (label, label2) pair), carrying label2 << 32 | received index
+__global__ void k_dm_dbl_lkeys(const int32_t* __restrict__ in, uint64_t n, uint32_t G0, uint32_t* __restrict__ key,
+                               unsigned long long* __restrict__ val) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  key[j] = ((unsigned long long)(uint32_t)in[2 * j] << 32) | (uint32_t)in[2 * j + 1];
-  val[j] = (uint32_t)j;
+  key[j] = (uint32_t)in[2 * j] - G0;
+  val[j] = ((unsigned long long)(uint32_t)in[2 * j + 1] << 32) | (uint32_t)j;
+}
+
+// second pass over the members sorted by label: a group (equal labels) of at
+// most kDblSmall members is ranked by counting over an LDS copy of the block's
+// members with a halo; its new label is label + #members with a smaller
+// label2 (the sa position where its equal-key run starts, as k_dm_dbl_result),
+// unresolved when another member has the same label2.  Larger groups are
+// listed (bigList[0] = count) for the full-key sort.
+constexpr uint32_t kDblBlock = 256, kDblSmall = 32, kDblHalo = kDblSmall;
+__global__ void __launch_bounds__(kDblBlock) k_dm_dbl_rank(const uint32_t* __restrict__ key,
+                                                           const unsigned long long* __restrict__ val, uint64_t n,
+                                                           uint32_t G0, unsigned long long* __restrict__ res,
+                                                           uint32_t* __restrict__ bigList) {
+  __shared__ uint32_t kL[kDblBlock + 2 * kDblHalo], l2L[kDblBlock + 2 * kDblHalo];
+  const uint64_t u0 = (uint64_t)blockIdx.x * kDblBlock;
+  const int64_t base = (int64_t)u0 - kDblHalo;
+  for (uint32_t i = threadIdx.x; i < kDblBlock + 2 * kDblHalo; i += blockDim.x) {
+    const int64_t j = base + i;
+    if (j >= 0 && j < (int64_t)n) {
+      kL[i] = key[j];
+      l2L[i] = (uint32_t)(val[j] >> 32);
+    }
+  }
+  __syncthreads();
+  const uint64_t u = u0 + threadIdx.x;
+  if (u >= n) return;
+  const uint32_t me = threadIdx.x + kDblHalo, k = kL[me], v = l2L[me];
+  uint32_t lo = me, hi = me + 1;
+  while (lo > 0 && base + lo > 0 && kL[lo - 1] == k && me - lo <= kDblSmall) lo--;
+  while (hi < kDblBlock + 2 * kDblHalo && base + (int64_t)hi < (int64_t)n && kL[hi] == k && hi - me <= kDblSmall) hi++;
+  if (hi - lo > kDblSmall) {  // (a group reaching past the halo has more than kDblSmall members)
+    bigList[1 + atomicAdd(bigList, 1u)] = (uint32_t)u;
+    return;
+  }
+  uint32_t less = 0, eq = 0;
+  for (uint32_t j = lo; j < hi; j++) {
+    const uint32_t w = l2L[j];
+    less += w < v ? 1u : 0u;
+    eq += (w == v && j != me) ? 1u : 0u;
+  }
+  res[(uint32_t)val[u]] = (unsigned long long)(k + G0 + less) | (eq ? (1ull << 32) : 0ull);
+}
+
+// big groups: their members' full (label, label2) keys for the sort path
+__global__ void k_dm_dbl_bigkeys(const uint32_t* __restrict__ list, uint32_t B, const uint32_t* __restrict__ key,
+                                 const unsigned long long* __restrict__ val, uint32_t G0,
+                                 unsigned long long* __restrict__ k64, uint32_t* __restrict__ v2) {
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= B) return;
+  const uint32_t u = list[b];
+  const unsigned long long v = val[u];
+  k64[b] = ((unsigned long long)(key[u] + G0) << 32) | (v >> 32);
+  v2[b] = (uint32_t)v;
 }
 
 __global__ void k_dm_dbl_marks(const unsigned long long* __restrict__ key, uint64_t n, uint32_t* __restrict__ gs,
@@ -150,26 +209,27 @@ __global__ void k_dm_dbl_marks(const unsigned long long* __restrict__ key, uint6
 }
 
 // new label = g + (first index of the equal-key run - first index of group
-// g), i.e. the sa position the run starts at; bit 31 = still unresolved
+// g), i.e. the sa position the run starts at; bit 32 = still unresolved
 __global__ void k_dm_dbl_result(const unsigned long long* __restrict__ key, const uint32_t* __restrict__ val,
                                 const uint32_t* __restrict__ gsMax, const uint32_t* __restrict__ ksMax, uint64_t n,
-                                uint32_t* __restrict__ res) {
+                                unsigned long long* __restrict__ res) {
   const uint64_t u = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= n) return;
   const unsigned long long k = key[u];
   const uint32_t label = (uint32_t)(k >> 32) + (ksMax[u] - gsMax[u]);
   const bool alone = ksMax[u] == (uint32_t)u && (u + 1 == n || key[u + 1] != k);
-  res[val[u]] = label | (alone ? 0u : 0x80000000u);
+  res[val[u]] = (unsigned long long)label | (alone ? 0ull : (1ull << 32));
 }
 
 __global__ void k_dm_dbl_apply(const uint32_t* __restrict__ aPerm, const uint32_t* __restrict__ act,
-                               const uint32_t* __restrict__ back, uint64_t n, uint32_t* __restrict__ grp,
+                               const unsigned long long* __restrict__ back, uint64_t n, uint32_t* __restrict__ grp,
                                uint32_t* __restrict__ keep) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
-  const uint32_t u = aPerm[j], v = back[j];
-  grp[act[u]] = v & 0x7fffffffu;
-  keep[u] = v >> 31;
+  const uint32_t u = aPerm[j];
+  const unsigned long long v = back[j];
+  grp[act[u]] = (uint32_t)v;
+  keep[u] = (uint32_t)(v >> 32);
 }
 
 // head rank and next-head rank (FN:1468-1494) of every head, heads send order
@@ -346,12 +406,12 @@ void mk_dm_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t
 }
 void mk_dm_group_labels(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
                         const uint32_t* posBegin, const uint32_t* isaRef, const uint32_t* headBase, uint32_t n,
-                        uint32_t* back, uint32_t* gItem, hipStream_t st) {
+                        unsigned long long* back, uint32_t* gItem, hipStream_t st) {
   if (H)
     hipLaunchKernelGGL(k_dm_group_labels, g1d(H), dim3(256), 0, st, it, itemOfSlot, Pm, H, posBegin, isaRef,
                        headBase, n, back, gItem);
 }
-void mk_dm_grp_init(const uint32_t* perm, const uint32_t* in, uint64_t n, uint32_t* grp, uint32_t* actFlag,
+void mk_dm_grp_init(const uint32_t* perm, const unsigned long long* in, uint64_t n, uint32_t* grp, uint32_t* actFlag,
                     hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_dm_grp_init, g1d(n), dim3(256), 0, st, perm, in, n, grp, actFlag);
 }
@@ -359,17 +419,27 @@ void mk_dm_dbl_pack(const uint32_t* aPerm, const uint32_t* act, const uint32_t* 
                     uint32_t H, int32_t* out, uint32_t* err, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_dm_dbl_pack, g1d(n), dim3(256), 0, st, aPerm, act, grp, h, n, H, out, err);
 }
-void mk_dm_dbl_keys(const int32_t* in, uint64_t n, unsigned long long* key, uint32_t* val, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_dm_dbl_keys, g1d(n), dim3(256), 0, st, in, n, key, val);
+void mk_dm_dbl_lkeys(const int32_t* in, uint64_t n, uint32_t G0, uint32_t* key, unsigned long long* val,
+                     hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_dm_dbl_lkeys, g1d(n), dim3(256), 0, st, in, n, G0, key, val);
+}
+void mk_dm_dbl_rank(const uint32_t* key, const unsigned long long* val, uint64_t n, uint32_t G0,
+                    unsigned long long* res, uint32_t* bigList, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_dm_dbl_rank, dim3((unsigned)((n + kDblBlock - 1) / kDblBlock)), dim3(kDblBlock), 0, st,
+                            key, val, n, G0, res, bigList);
+}
+void mk_dm_dbl_bigkeys(const uint32_t* list, uint32_t B, const uint32_t* key, const unsigned long long* val,
+                       uint32_t G0, unsigned long long* k64, uint32_t* v2, hipStream_t st) {
+  if (B) hipLaunchKernelGGL(k_dm_dbl_bigkeys, g1d(B), dim3(256), 0, st, list, B, key, val, G0, k64, v2);
 }
 void mk_dm_dbl_marks(const unsigned long long* key, uint64_t n, uint32_t* gs, uint32_t* ks, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_dm_dbl_marks, g1d(n), dim3(256), 0, st, key, n, gs, ks);
 }
 void mk_dm_dbl_result(const unsigned long long* key, const uint32_t* val, const uint32_t* gsMax,
-                      const uint32_t* ksMax, uint64_t n, uint32_t* res, hipStream_t st) {
+                      const uint32_t* ksMax, uint64_t n, unsigned long long* res, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_dm_dbl_result, g1d(n), dim3(256), 0, st, key, val, gsMax, ksMax, n, res);
 }
-void mk_dm_dbl_apply(const uint32_t* aPerm, const uint32_t* act, const uint32_t* back, uint64_t n, uint32_t* grp,
+void mk_dm_dbl_apply(const uint32_t* aPerm, const uint32_t* act, const unsigned long long* back, uint64_t n, uint32_t* grp,
                      uint32_t* keep, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_dm_dbl_apply, g1d(n), dim3(256), 0, st, aPerm, act, back, n, grp, keep);
 }

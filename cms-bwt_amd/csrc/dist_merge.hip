@@ -64,7 +64,9 @@ void Engine::dm_begin(uint32_t world, uint32_t rank, uint64_t heads_total, uint6
                       int rle) {
   if (!walked) throw InputError{CMSBWT_EARG, "run ms_walk first"};
   if (world < 1 || world > 64 || rank >= world) throw InputError{CMSBWT_EARG, "bad world/rank"};
-  if (heads_total >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^31-1 heads (int32 ranks, FN:1436)"};
+  // head indices, group labels and ranks are uint32 (labels 1 .. H + 1): the
+  // reference's int32 limit (FN:1436-1437, 1456) is lifted to 2^32 - 2
+  if (heads_total >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^32-2 heads (uint32 head indices)"};
   if (heads_total == 0)  // as Engine::merge: FN:1359-1385 is undefined without heads
     throw InputError{CMSBWT_EINPUT, "collection has no documents (reference behaviour undefined, FN:1359-1385)"};
   const uint32_t n = R.n;
@@ -112,7 +114,7 @@ void Engine::dm_pack_heads(int32_t* out) {
 // ---- 2. items of the owned positions (received in global idx order:
 // ranks in order, each in document order) and per-SA-rank counts
 void Engine::dm_group(const int32_t* recv, uint64_t nrecv, uint32_t* saCounts) {
-  if (nrecv >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "too many heads on one rank"};
+  if (nrecv >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many heads on one rank"};
   const uint32_t n = R.n;
   const uint32_t Hp = dm.Hp = (uint32_t)nrecv;
   dm.rPos.alloc(Hp); dm.rLen.alloc(Hp); dm.rIsa.alloc(Hp); dm.rTon.alloc(Hp);
@@ -154,7 +156,7 @@ void Engine::dm_group(const int32_t* recv, uint64_t nrecv, uint32_t* saCounts) {
   sync();
 }
 
-void Engine::dm_labels(const uint32_t* saCounts, uint32_t* back) {
+void Engine::dm_labels(const uint32_t* saCounts, unsigned long long* back) {
   const uint32_t n = R.n;
   // the difference array summed over ranks (head flags stay this rank's)
   HIPCHK(hipMemcpyAsync(diff.p, saCounts + 2ull * n, ((uint64_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
@@ -168,7 +170,7 @@ void Engine::dm_labels(const uint32_t* saCounts, uint32_t* back) {
 }
 
 // ---- 3. prefix doubling of the head string
-uint64_t Engine::dm_dbl_init(const uint32_t* labels) {
+uint64_t Engine::dm_dbl_init(const unsigned long long* labels) {
   dm.grp.alloc(H);
   dm.act.alloc(H);
   dm.U = 0;
@@ -201,26 +203,41 @@ void Engine::dm_dbl_pack(int32_t* out) {
   dm_check_err("doubling keys");
 }
 
-void Engine::dm_dbl_sort(const int32_t* recv, uint64_t nrecv, uint32_t* res) {
+// label-range owner: new labels of the received (label, label2) pairs.  The
+// members are sorted by label only (bits of the owned label range), groups of
+// <= 32 members ranked by counting in LDS (k_dm_dbl_rank); the members of
+// larger groups go through the full-key sort.
+void Engine::dm_dbl_sort(const int32_t* recv, uint64_t nrecv, unsigned long long* res) {
   if (!nrecv) return;
   if (nrecv >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "doubling group larger than 2^32"};
-  DBuf<unsigned long long> key, key2;
-  DBuf<uint32_t> val, val2, gs, ks, gsM, ksM;
-  key.alloc(nrecv); key2.alloc(nrecv); val.alloc(nrecv); val2.alloc(nrecv);
-  mk_dm_dbl_keys(recv, nrecv, key.p, val.p, st);
-  sort_pairs(key.p, key2.p, val.p, val2.p, nrecv, 32 + bits_for(dm.Htot));
+  const uint32_t G0 = dm.Gsplit[dm.rank], G1 = dm.Gsplit[dm.rank + 1];
+  DBuf<uint32_t> key, key2, big;
+  DBuf<unsigned long long> val, val2;
+  key.alloc(nrecv); key2.alloc(nrecv); val.alloc(nrecv); val2.alloc(nrecv); big.alloc(nrecv + 1);
+  mk_dm_dbl_lkeys(recv, nrecv, G0, key.p, val.p, st);
+  sort_pairs(key.p, key2.p, val.p, val2.p, nrecv, bits_for(G1 > G0 ? G1 - G0 - 1 : 0));
   key.release();
   val.release();
-  gs.alloc(nrecv); ks.alloc(nrecv); gsM.alloc(nrecv); ksM.alloc(nrecv);
-  mk_dm_dbl_marks(key2.p, nrecv, gs.p, ks.p, st);
-  inscan(gs.p, gsM.p, nrecv, rocprim::maximum<uint32_t>());
-  inscan(ks.p, ksM.p, nrecv, rocprim::maximum<uint32_t>());
-  mk_dm_dbl_result(key2.p, val2.p, gsM.p, ksM.p, nrecv, res, st);
+  HIPCHK(hipMemsetAsync(big.p, 0, 4, st));
+  mk_dm_dbl_rank(key2.p, val2.p, nrecv, G0, res, big.p, st);
+  const uint32_t B = read1(big.p);
+  if (B) {
+    DBuf<unsigned long long> k64, k64b;
+    DBuf<uint32_t> v, vb, gs, ks, gsM, ksM;
+    k64.alloc(B); k64b.alloc(B); v.alloc(B); vb.alloc(B);
+    mk_dm_dbl_bigkeys(big.p + 1, B, key2.p, val2.p, G0, k64.p, v.p, st);
+    sort_pairs(k64.p, k64b.p, v.p, vb.p, B, 32 + bits_for(dm.Htot));
+    gs.alloc(B); ks.alloc(B); gsM.alloc(B); ksM.alloc(B);
+    mk_dm_dbl_marks(k64b.p, B, gs.p, ks.p, st);
+    inscan(gs.p, gsM.p, B, rocprim::maximum<uint32_t>());
+    inscan(ks.p, ksM.p, B, rocprim::maximum<uint32_t>());
+    mk_dm_dbl_result(k64b.p, vb.p, gsM.p, ksM.p, B, res, st);
+  }
   HIPCHK(hipGetLastError());
   sync();
 }
 
-uint64_t Engine::dm_dbl_apply(const uint32_t* back) {
+uint64_t Engine::dm_dbl_apply(const unsigned long long* back) {
   if (!dm.U) return 0;
   DBuf<uint32_t> keep, act2;
   keep.alloc(dm.U);

@@ -913,7 +913,7 @@ struct Engine {
   // pread of the file into pinned buffers by `nt` threads, each DMAing its
   // chunks to dst on its own stream (double-buffered: reading chunk c+2T
   // overlaps the copy of chunk c).
-  void stream_file(int fd, uint64_t fsz, uint8_t* dst) {
+  void stream_file(int fd, uint64_t base, uint64_t fsz, uint8_t* dst) {
     const uint32_t nt = std::max(1u, std::min(64u, env_u32("CMSBWT_READ_THREADS", 8)));
     ensure_pinned(nt, (uint64_t)std::max(1u, env_u32("CMSBWT_READ_CHUNK_MB", 32)) << 20);
     const uint64_t CH = pinnedBytes;
@@ -937,7 +937,7 @@ struct Engine {
             const uint64_t off = c * CH, want = std::min(CH, fsz - off);
             uint64_t got = 0;
             while (got < want) {
-              ssize_t r = pread(fd, buf + got, want - got, (off_t)(off + got));
+              ssize_t r = pread(fd, buf + got, want - got, (off_t)(base + off + got));
               if (r <= 0) { err = 1; break; }
               got += (uint64_t)r;
             }
@@ -956,8 +956,10 @@ struct Engine {
   }
 
   // Same Collection as read_collection(path, UINT64_MAX) + upload_collection
-  // (tests/test_gpu_parity.py::test_gpu_reader_*), produced in HBM.
-  void load_collection_file_gpu(const std::string& path) {
+  // (tests/test_gpu_parity.py::test_gpu_reader_*), produced in HBM.  With a
+  // byte range: the documents of bytes [off, off + len) of the file, which
+  // must start at a document start (shard_bounds).
+  void load_collection_file_gpu(const std::string& path, uint64_t fileOff = 0, uint64_t sliceLen = ~0ull) {
     if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
     auto t0 = std::chrono::steady_clock::now();
     reset_collection();
@@ -965,12 +967,13 @@ struct Engine {
     if (fd < 0) throw InputError{CMSBWT_EIO, "Error opening file of sequence (" + path + ")"};
     struct stat sbuf;
     if (fstat(fd, &sbuf) != 0) { close(fd); throw InputError{CMSBWT_EIO, "cannot stat " + path}; }
-    const uint64_t fsz = (uint64_t)sbuf.st_size;
+    fileOff = std::min<uint64_t>(fileOff, (uint64_t)sbuf.st_size);
+    const uint64_t fsz = std::min<uint64_t>(sliceLen, (uint64_t)sbuf.st_size - fileOff);  // bytes of this slice
     const uint64_t ntiles = (fsz + kRdTile - 1) / kRdTile;
     DBuf<uint8_t> raw;
     raw.alloc(ntiles * kRdTile + kRdTile);  // tiles read whole; '\n'/'>' lookups one past len
     try {
-      stream_file(fd, fsz, raw.p);
+      stream_file(fd, fileOff, fsz, raw.p);
     } catch (...) {
       close(fd);
       throw;
@@ -1186,7 +1189,9 @@ struct Engine {
     exscan(withEnd.p, chunkBase.p, 0ull, nch);
     {
       const unsigned long long tot = read1(chunkBase.p + (nch - 1)) + read1(withEnd.p + (nch - 1));
-      if (tot >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^31-1 heads (int32 ranks, FN:1436)"};
+      // uint32 head indices and labels (1 .. H + 1): the reference's int32
+      // limit (FN:1436-1437, 1456) is lifted to 2^32 - 2 heads
+      if (tot >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^32-2 heads (uint32 head indices)"};
       H = (uint32_t)tot;
     }
     if (chars) {  // head density for the next walk's pool
@@ -2026,7 +2031,7 @@ struct Engine {
 
   void walk_import(uint64_t heads, uint64_t nd, uint64_t nchars, uint32_t flags, const void* const* a) {
     if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
-    if (heads >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^31-1 heads"};
+    if (heads >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^32-2 heads (uint32 head indices)"};
     walked = merged = false;
     H = (uint32_t)heads;
     hStart.alloc(H); hPos.alloc(H); hLen.alloc(H); hIsa.alloc(H); hTonext.alloc(H);
@@ -2166,12 +2171,12 @@ struct Engine {
   void dm_route_heads(uint64_t* counts);
   void dm_pack_heads(int32_t* out);
   void dm_group(const int32_t* recv, uint64_t nrecv, uint32_t* saCounts);
-  void dm_labels(const uint32_t* saCounts, uint32_t* back);
-  uint64_t dm_dbl_init(const uint32_t* labels);
+  void dm_labels(const uint32_t* saCounts, unsigned long long* back);
+  uint64_t dm_dbl_init(const unsigned long long* labels);
   void dm_dbl_route(uint64_t h, uint64_t* counts);
   void dm_dbl_pack(int32_t* out);
-  void dm_dbl_sort(const int32_t* recv, uint64_t nrecv, uint32_t* res);
-  uint64_t dm_dbl_apply(const uint32_t* back);
+  void dm_dbl_sort(const int32_t* recv, uint64_t nrecv, unsigned long long* res);
+  uint64_t dm_dbl_apply(const unsigned long long* back);
   void dm_pack_ranks(int32_t* out);
   void dm_load_ranks(const int32_t* recv);
   void dm_route_halo(uint64_t* itemCounts, uint64_t* wordCounts);

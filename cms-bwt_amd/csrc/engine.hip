@@ -102,6 +102,29 @@ int cmsbwt_load_collection_file(cmsbwt_ctx* ctx, const char* path, uint64_t pref
   });
 }
 
+int cmsbwt_load_collection_file_range(cmsbwt_ctx* ctx, const char* path, uint32_t rank, uint32_t world) {
+  if (!ctx || !path || world == 0 || rank >= world) return CMSBWT_EARG;
+  return guard(ctx, [&] {
+    std::vector<uint64_t> b;
+    uint64_t fsz = 0;
+    std::string err;
+    if (!cmsbwt::shard_bounds(path, world, b, fsz, err)) throw cmsbwt::InputError{CMSBWT_EIO, err};
+    ctx->e->load_collection_file_gpu(path, b[rank], b[rank + 1] - b[rank]);
+    ctx->e->stats.coll_file_bytes = fsz;
+    ctx->e->stats.sn_initial = fsz;
+  });
+}
+
+int cmsbwt_host_shard_bounds(const char* path, uint32_t world, uint64_t* bounds) {
+  if (!path || !bounds || world == 0) return CMSBWT_EARG;
+  std::vector<uint64_t> b;
+  uint64_t fsz = 0;
+  std::string err;
+  if (!cmsbwt::shard_bounds(path, world, b, fsz, err)) return CMSBWT_EIO;
+  for (uint32_t k = 0; k <= world; k++) bounds[k] = b[k];
+  return CMSBWT_OK;
+}
+
 int cmsbwt_load_collection(cmsbwt_ctx* ctx, const uint8_t* text, const uint64_t* doc_off, uint64_t ndocs) {
   if (!ctx || !doc_off) return CMSBWT_EARG;
   return guard(ctx, [&] {
@@ -397,13 +420,13 @@ int cmsbwt_dm_group(cmsbwt_ctx* ctx, const int32_t* recv, uint64_t nrecv, uint32
   if (!ctx || !sa_counts) return CMSBWT_EARG;
   return guard(ctx, [&] { ctx->e->dm_group(recv, nrecv, sa_counts); });
 }
-int cmsbwt_dm_labels(cmsbwt_ctx* ctx, const uint32_t* sa_counts, uint32_t* back) {
+int cmsbwt_dm_labels(cmsbwt_ctx* ctx, const uint32_t* sa_counts, uint64_t* back) {
   if (!ctx || !sa_counts) return CMSBWT_EARG;
-  return guard(ctx, [&] { ctx->e->dm_labels(sa_counts, back); });
+  return guard(ctx, [&] { ctx->e->dm_labels(sa_counts, (unsigned long long*)back); });
 }
-int cmsbwt_dm_dbl_init(cmsbwt_ctx* ctx, const uint32_t* labels, uint64_t* active) {
+int cmsbwt_dm_dbl_init(cmsbwt_ctx* ctx, const uint64_t* labels, uint64_t* active) {
   if (!ctx || !active) return CMSBWT_EARG;
-  return guard(ctx, [&] { *active = ctx->e->dm_dbl_init(labels); });
+  return guard(ctx, [&] { *active = ctx->e->dm_dbl_init((const unsigned long long*)labels); });
 }
 int cmsbwt_dm_dbl_route(cmsbwt_ctx* ctx, uint64_t h, uint64_t* counts) {
   if (!ctx || !counts) return CMSBWT_EARG;
@@ -413,13 +436,13 @@ int cmsbwt_dm_dbl_pack(cmsbwt_ctx* ctx, int32_t* out) {
   if (!ctx) return CMSBWT_EARG;
   return guard(ctx, [&] { ctx->e->dm_dbl_pack(out); });
 }
-int cmsbwt_dm_dbl_sort(cmsbwt_ctx* ctx, const int32_t* recv, uint64_t nrecv, uint32_t* result) {
+int cmsbwt_dm_dbl_sort(cmsbwt_ctx* ctx, const int32_t* recv, uint64_t nrecv, uint64_t* result) {
   if (!ctx) return CMSBWT_EARG;
-  return guard(ctx, [&] { ctx->e->dm_dbl_sort(recv, nrecv, result); });
+  return guard(ctx, [&] { ctx->e->dm_dbl_sort(recv, nrecv, (unsigned long long*)result); });
 }
-int cmsbwt_dm_dbl_apply(cmsbwt_ctx* ctx, const uint32_t* back, uint64_t* active) {
+int cmsbwt_dm_dbl_apply(cmsbwt_ctx* ctx, const uint64_t* back, uint64_t* active) {
   if (!ctx || !active) return CMSBWT_EARG;
-  return guard(ctx, [&] { *active = ctx->e->dm_dbl_apply(back); });
+  return guard(ctx, [&] { *active = ctx->e->dm_dbl_apply((const unsigned long long*)back); });
 }
 int cmsbwt_dm_pack_ranks(cmsbwt_ctx* ctx, int32_t* out) {
   if (!ctx) return CMSBWT_EARG;

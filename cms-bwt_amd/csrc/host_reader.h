@@ -20,4 +20,16 @@ struct Collection {
 // file_size: ftello of the collection (FN:221-223); prefix = -p.
 bool read_collection(const std::string& path, uint64_t prefix, Collection& c, std::string& err);
 
+// Byte-range shards of the collection for `world` ranks: rank k reads
+// [bounds[k], bounds[k+1]) and walks the documents closed inside it (plus the
+// tail document for the last rank).  bounds[k] is the first byte after the
+// last document-ending line (empty or '>', newline-terminated; FN:1138-1139)
+// that starts before k * size / world, so every slice begins at a document
+// start and reading the slices in rank order gives the documents of the
+// whole file, in order (no -p: its cut depends on the bytes before it).
+bool shard_bounds(const std::string& path, uint32_t world, std::vector<uint64_t>& bounds, uint64_t& fsz,
+                  std::string& err);
+// bounds[k] for B = k * size / world (~0 on a read error)
+uint64_t shard_start(int fd, uint64_t fsz, uint64_t B);
+
 }  // namespace cmsbwt

@@ -177,16 +177,22 @@ void mk_dm_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t
                      uint32_t* out, hipStream_t st);
 void mk_dm_group_labels(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
                         const uint32_t* posBegin, const uint32_t* isaRef, const uint32_t* headBase, uint32_t n,
-                        uint32_t* back, uint32_t* gItem, hipStream_t st);
-void mk_dm_grp_init(const uint32_t* perm, const uint32_t* in, uint64_t n, uint32_t* grp, uint32_t* actFlag,
+                        unsigned long long* back, uint32_t* gItem, hipStream_t st);
+void mk_dm_grp_init(const uint32_t* perm, const unsigned long long* in, uint64_t n, uint32_t* grp, uint32_t* actFlag,
                     hipStream_t st);
 void mk_dm_dbl_pack(const uint32_t* aPerm, const uint32_t* act, const uint32_t* grp, uint32_t h, uint64_t n,
                     uint32_t H, int32_t* out, uint32_t* err, hipStream_t st);
-void mk_dm_dbl_keys(const int32_t* in, uint64_t n, unsigned long long* key, uint32_t* val, hipStream_t st);
+// label owner: sort by label offset, rank small groups in LDS, list big ones
+void mk_dm_dbl_lkeys(const int32_t* in, uint64_t n, uint32_t G0, uint32_t* key, unsigned long long* val,
+                     hipStream_t st);
+void mk_dm_dbl_rank(const uint32_t* key, const unsigned long long* val, uint64_t n, uint32_t G0,
+                    unsigned long long* res, uint32_t* bigList, hipStream_t st);
+void mk_dm_dbl_bigkeys(const uint32_t* list, uint32_t B, const uint32_t* key, const unsigned long long* val,
+                       uint32_t G0, unsigned long long* k64, uint32_t* v2, hipStream_t st);
 void mk_dm_dbl_marks(const unsigned long long* key, uint64_t n, uint32_t* gs, uint32_t* ks, hipStream_t st);
 void mk_dm_dbl_result(const unsigned long long* key, const uint32_t* val, const uint32_t* gsMax,
-                      const uint32_t* ksMax, uint64_t n, uint32_t* res, hipStream_t st);
-void mk_dm_dbl_apply(const uint32_t* aPerm, const uint32_t* act, const uint32_t* back, uint64_t n, uint32_t* grp,
+                      const uint32_t* ksMax, uint64_t n, unsigned long long* res, hipStream_t st);
+void mk_dm_dbl_apply(const uint32_t* aPerm, const uint32_t* act, const unsigned long long* back, uint64_t n, uint32_t* grp,
                      uint32_t* keep, hipStream_t st);
 void mk_dm_pack_ranks(const uint32_t* perm, const uint32_t* grp, const uint16_t* nexthead, uint64_t n, uint32_t H,
                       int32_t* out, uint32_t* err, hipStream_t st);

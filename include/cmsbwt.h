@@ -96,6 +96,11 @@ int cmsbwt_load_reference(cmsbwt_ctx* ctx, const uint8_t* ref, uint64_t len);
 /* Collection reader (FN:1138-1275): getline semantics, '>'/blank lines split
  * documents, unterminated last line dropped, -p cut.  Uploads to HBM. */
 int cmsbwt_load_collection_file(cmsbwt_ctx* ctx, const char* coll_path, uint64_t prefix);
+/* Rank `rank` of `world`'s share of the collection file (multi-GPU ingest,
+ * no -p): the documents closed inside bytes [bounds[rank], bounds[rank+1])
+ * of cmsbwt_host_shard_bounds, read with the same getline semantics
+ * (FN:1138-1147); the ranks' documents, in rank order, are the file's. */
+int cmsbwt_load_collection_file_range(cmsbwt_ctx* ctx, const char* coll_path, uint32_t rank, uint32_t world);
 /* Documents from host memory: doc k = text[doc_off[k] .. doc_off[k+1]). */
 int cmsbwt_load_collection(cmsbwt_ctx* ctx, const uint8_t* text, const uint64_t* doc_off,
                            uint64_t ndocs);
@@ -147,10 +152,11 @@ int cmsbwt_walk_import(cmsbwt_ctx* ctx, uint64_t heads, uint64_t ndocs, uint64_t
  *   ms_walk; dm_begin
  *   dm_route_heads -> counts; dm_pack_heads -> 5 int32/head; all-to-all
  *   dm_group(recv) -> buf[3n+1] (items, heads per SA rank; run difference
- *     array); all-reduce(sum) -> dm_labels -> back (1 word per received
- *     head); reverse all-to-all -> dm_dbl_init
+ *     array); all-reduce(sum) -> dm_labels -> back (label | unresolved << 32
+ *     per received head); reverse all-to-all -> dm_dbl_init
  *   while (all-reduced active > 0): dm_dbl_route(h) -> counts;
- *     dm_dbl_pack -> 2 words/element; all-to-all; dm_dbl_sort -> result;
+ *     dm_dbl_pack -> 2 words/element; all-to-all; dm_dbl_sort -> result
+ *     (label | unresolved << 32);
  *     reverse all-to-all -> dm_dbl_apply; h *= 2
  *   dm_pack_ranks -> 2 words/head; all-to-all (head counts) -> dm_load_ranks
  *   dm_route_halo -> counts; dm_pack_halo -> 6 words/item + nhr words;
@@ -164,12 +170,12 @@ int cmsbwt_dm_begin(cmsbwt_ctx* ctx, uint32_t world, uint32_t rank, uint64_t hea
 int cmsbwt_dm_route_heads(cmsbwt_ctx* ctx, uint64_t* counts);
 int cmsbwt_dm_pack_heads(cmsbwt_ctx* ctx, int32_t* out);
 int cmsbwt_dm_group(cmsbwt_ctx* ctx, const int32_t* recv, uint64_t nrecv, uint32_t* sa_counts);
-int cmsbwt_dm_labels(cmsbwt_ctx* ctx, const uint32_t* sa_counts, uint32_t* back);
-int cmsbwt_dm_dbl_init(cmsbwt_ctx* ctx, const uint32_t* labels, uint64_t* active);
+int cmsbwt_dm_labels(cmsbwt_ctx* ctx, const uint32_t* sa_counts, uint64_t* back);
+int cmsbwt_dm_dbl_init(cmsbwt_ctx* ctx, const uint64_t* labels, uint64_t* active);
 int cmsbwt_dm_dbl_route(cmsbwt_ctx* ctx, uint64_t h, uint64_t* counts);
 int cmsbwt_dm_dbl_pack(cmsbwt_ctx* ctx, int32_t* out);
-int cmsbwt_dm_dbl_sort(cmsbwt_ctx* ctx, const int32_t* recv, uint64_t nrecv, uint32_t* result);
-int cmsbwt_dm_dbl_apply(cmsbwt_ctx* ctx, const uint32_t* back, uint64_t* active);
+int cmsbwt_dm_dbl_sort(cmsbwt_ctx* ctx, const int32_t* recv, uint64_t nrecv, uint64_t* result);
+int cmsbwt_dm_dbl_apply(cmsbwt_ctx* ctx, const uint64_t* back, uint64_t* active);
 int cmsbwt_dm_pack_ranks(cmsbwt_ctx* ctx, int32_t* out);
 int cmsbwt_dm_load_ranks(cmsbwt_ctx* ctx, const int32_t* recv);
 int cmsbwt_dm_route_halo(cmsbwt_ctx* ctx, uint64_t* item_counts, uint64_t* word_counts);
@@ -198,6 +204,10 @@ int cmsbwt_host_read_collection(const char* path, uint64_t prefix, uint8_t* text
                                 uint64_t* text_len, uint64_t* doc_off, uint64_t doc_cap, uint64_t* ndocs,
                                 uint64_t* sn);
 int cmsbwt_host_suffix_array(const uint8_t* s, uint64_t n, int32_t* sa_out);
+/* Byte bounds (world + 1 entries) of the collection shards: bounds[k] is the
+ * first byte after the last document-ending line (empty or '>') that starts
+ * before k * size / world; bounds[0] = 0, bounds[world] = size. */
+int cmsbwt_host_shard_bounds(const char* coll_path, uint32_t world, uint64_t* bounds);
 
 #ifdef __cplusplus
 }

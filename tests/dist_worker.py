@@ -162,6 +162,26 @@ def gpu_position_sharded(rank, world, port, work):
     dist.destroy_process_group()
 
 
+def gpu_sharded_files(rank, world, port, work):
+    """Ranks sharing one GPU: each loads its byte range of the collection file
+    (cmsbwt_load_collection_file_range) and the sharded step runs over gloo;
+    rank 0 writes its runs and statistics."""
+    import cmsbwt
+    import cmsbwt.dist as cdist
+    dist = _init(rank, world, port)
+    cfg = json.load(open(os.path.join(work, "cfg.json")))
+    eng = cmsbwt.Engine(0)
+    eng.initialize_reference(cfg["ref"])
+    eng.load_collection_file_range(cfg["coll"], rank, world)
+    x = cdist.Transport("cuda:0")
+    cdist.sharded_step(eng, "cuda:0", rle=cfg["rle"], xfer=x)
+    if rank == 0:
+        open(os.path.join(work, "runs0.bin"), "wb").write(eng.runs_bytes())
+        json.dump(eng.stats().as_dict(), open(os.path.join(work, "stats.json"), "w"))
+    eng.close()
+    dist.destroy_process_group()
+
+
 if __name__ == "__main__":
     fn, rank, world, port, work = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5]
     globals()[fn](rank, world, port, work)

@@ -128,3 +128,57 @@ def test_gpu_reader_rejects_foreign_byte_like_host(engine, tmp_path):
         os.environ.pop("CMSBWT_HOST_READER")
     assert e1.value.code == e2.value.code == 3
     assert str(e1.value) == str(e2.value)
+
+
+# ---- byte-range sharded ingest (cmsbwt_load_collection_file_range): each
+# rank reads its slice of the file; the ranks' documents in rank order must be
+# the whole file's (the getline semantics of FN:1138-1147 per slice)
+def _range_docs(engine, path, rank, world):
+    engine.load_collection_file_range(path, rank, world)
+    text = engine.array("coll_text").tobytes()
+    off = engine.array("coll_off")
+    return [text[int(off[k]):int(off[k + 1]) - 1] for k in range(len(off) - 1)]
+
+
+def _check_shards(engine, path, world):
+    want, _ = cmsbwt.host_read_collection(path)
+    got = []
+    for k in range(world):
+        got += _range_docs(engine, path, k, world)
+    assert len(got) == len(want), f"{len(got)} vs {len(want)} documents at world {world}"
+    assert got == want
+
+
+@pytest.mark.parametrize("world", [2, 3, 8])
+@pytest.mark.parametrize("case", [c for c in cases.small_cases() if c[3] == cases.UINT64_MAX], ids=lambda c: c[0])
+def test_sharded_loader_small_cases(engine, tmp_path, case, world):
+    d, rp, cp, _ = cases.materialise(tmp_path, case)
+    engine.initialize_reference(rp)
+    _check_shards(engine, cp, world)
+
+
+@pytest.mark.parametrize("seed,tail", [(1, b""), (2, b"ACGTACG"), (3, b">unterminated header"), (4, b"\n")])
+def test_sharded_loader_random_structure(engine, tmp_path, seed, tail):
+    rng = np.random.default_rng(seed)
+    body = _random_structured(rng, 700) + tail
+    if seed == 2:
+        body = b"ACGT\n" + body
+    cp = str(tmp_path / "c.fa")
+    with open(cp, "wb") as f:
+        f.write(body)
+    engine.initialize_reference(_ref_file(tmp_path))
+    for world in (3, 7):
+        _check_shards(engine, cp, world)
+
+
+@pytest.mark.parametrize("body", [b"", b"ACGT", b">", b"\n", b"\n\n\n", b">a\n", b"A\n", b">x\nACGT\n>y\n",
+                                  b"A" * 16383 + b"\n" + b">" + b"B" * 16384 + b"\nCC\n"],
+                         ids=["empty", "no_newline", "gt_only", "nl", "nl3", "hdr", "one", "two_hdr", "tile_edge"])
+def test_sharded_loader_degenerate(engine, tmp_path, body):
+    """More ranks than documents: ranks own no document (empty slices)."""
+    cp = str(tmp_path / "c.fa")
+    with open(cp, "wb") as f:
+        f.write(body.replace(b"B", b"A"))
+    engine.initialize_reference(_ref_file(tmp_path))
+    for world in (3, 5):
+        _check_shards(engine, cp, world)

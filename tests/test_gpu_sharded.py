@@ -135,3 +135,28 @@ def test_gather_step_device_tensors_rccl(oracle, tmp_path, case):
     spawn("gpu_gather_device", 1, work)
     for it in range(2):
         assert open(os.path.join(work, f"runs{it}.bin"), "rb").read() == want, f"step {it}"
+
+
+def test_sharded_eight_ranks_config2_files_golden(tmp_path):
+    """BASELINE config 4's shape at config 2's size: 8 ranks (gloo, sharing the
+    test GPU), each reading its byte range of the 1 GB FASTA collection
+    (10 MB ref + 100 copies @0.1 %, App. B run t3) and running the
+    position-sharded merge.  headNumber equals the reference's recorded
+    10,057,656; the .rl_bwt equals the golden sha256."""
+    import hashlib
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import gen_np
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))
+    pre = str(tmp_path / "t3")
+    gen_np.gen(10_000_000, 100, 0.001, 3, pre)
+    work = str(tmp_path)
+    json.dump({"ref": pre + ".ref.fa", "coll": pre + ".coll.fa", "rle": True},
+              open(os.path.join(work, "cfg.json"), "w"))
+    spawn("gpu_sharded_files", 8, work, timeout=600)
+    st = json.load(open(os.path.join(work, "stats.json")))
+    assert st["heads"] == g["survey"]["t3"]["headNumber"] == 10057656
+    assert st["rank"] == g["t3"]["Rank"]
+    assert (st["counter_bad"], st["counter_good"], st["counter_nothing"]) == \
+        (g["t3"]["counterBad"], g["t3"]["counterGood"], g["t3"]["counterDoNothing"])
+    assert hashlib.sha256(open(os.path.join(work, "runs0.bin"), "rb").read()).hexdigest() == g["t3"]["rl_bwt_sha256"]

@@ -136,3 +136,26 @@ def test_suffix_array_sais(built, seed):
         assert np.array_equal(cmsbwt.host_suffix_array(s), _naive_sa(s))
     s = b"ACGT" * 300 + b"\x01\x00"
     assert np.array_equal(cmsbwt.host_suffix_array(s), _naive_sa(s))
+
+
+@pytest.mark.parametrize("world", [1, 2, 3, 5, 8])
+def test_shard_bounds_split_at_document_ends(built, tmp_path, world):
+    """cmsbwt_host_shard_bounds (multi-GPU ingest): bounds are monotone, start
+    at 0, end at the file size, and parsing each slice with the reference's
+    reader semantics (cases.py_read_docs, FN:1138-1275) and concatenating in
+    rank order gives the whole file's documents."""
+    import cmsbwt
+    rng = np.random.default_rng(world)
+    bodies = [c[2] for c in cases.small_cases() if c[3] == cases.UINT64_MAX]
+    bodies += [b"", b"ACGT", b">", b"\n\n\n", b">x\nACGT\n>y\n", b"AC\nGT\n\n\nTT\n>h\nAAA",
+               b">" + b"h" * 5000 + b"\n" + b"ACGT" * 3000 + b"\n>" + b"g" * 7000]
+    for i, body in enumerate(bodies):
+        p = tmp_path / f"c{i}.fa"
+        p.write_bytes(body)
+        b = cmsbwt.host_shard_bounds(str(p), world)
+        assert b[0] == 0 and b[-1] == len(body) and all(x <= y for x, y in zip(b, b[1:]))
+        want, _ = cases.py_read_docs(body)
+        got = []
+        for k in range(world):
+            got += cases.py_read_docs(body[b[k]:b[k + 1]])[0]
+        assert got == want, (i, world, b)
