@@ -67,6 +67,21 @@ __global__ void k_dm_unpack_heads(const int32_t* __restrict__ in, uint64_t n, He
   h.lchar[j] = (uint8_t)((uint32_t)o[4] >> 8);
 }
 
+// run buckets (FN:1162-1171) of the received heads when the grouping did not
+// take the position-first sort (composite key wider than 64 bits): head j
+// covers [pos, pos + toNext + 1) (an end phrase: [n-1, n)); diff and hasHead
+// zeroed on entry
+__global__ void k_dm_runs(const uint32_t* __restrict__ pos, const uint32_t* __restrict__ tonext, uint64_t H,
+                          uint32_t n, int32_t* __restrict__ diff, uint8_t* __restrict__ hasHead) {
+  const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (j >= H) return;
+  const uint32_t p = pos[j];
+  const uint64_t e = (uint64_t)p + tonext[j] + 1;
+  atomicAdd(&diff[p], 1);
+  if (e <= n) atomicAdd(&diff[e], -1);
+  hasHead[p] = 1;
+}
+
 // per SA rank: this rank's items and heads of position SA[r] (zero for
 // positions it does not own; SA rank 0 = position n-1 holds the E end phrases)
 __global__ void k_dm_sa_counts(const int32_t* __restrict__ sa, const uint32_t* __restrict__ posBegin,
@@ -83,12 +98,12 @@ __global__ void k_dm_sa_counts(const int32_t* __restrict__ sa, const uint32_t* _
 
 // Initial group label of every member (its item's first sa position in the
 // head-string suffix array, FN:1432-1453): end phrases get 1 + m, others
-// 1 + headBase[ISA[p]] + (slot offset inside p).  Bit 32: unresolved (item
-// with >= 2 members; labels use all 32 bits).  Written in received order for
-// the return trip.
+// gBase[p] + slot[q] (gBase from k_pos_rank_base: 1 + headBase[ISA[p]] minus
+// the slot of p's first item; slots ascend with p, so it is read in order).
+// Bit 32: unresolved (item with >= 2 members; labels use all 32 bits).
+// Written in received order for the return trip.
 __global__ void k_dm_group_labels(const ItemsSoA it, const uint32_t* __restrict__ itemOfSlot,
-                                  const uint32_t* __restrict__ Pm, uint32_t H, const uint32_t* __restrict__ posBegin,
-                                  const uint32_t* __restrict__ isaRef, const uint32_t* __restrict__ headBase,
+                                  const uint32_t* __restrict__ Pm, uint32_t H, const uint32_t* __restrict__ gBase,
                                   uint32_t n, unsigned long long* __restrict__ back, uint32_t* __restrict__ gItem) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= H) return;
@@ -98,16 +113,15 @@ __global__ void k_dm_group_labels(const ItemsSoA it, const uint32_t* __restrict_
     g = 1 + m;
     if (m == 0) gItem[q] = 1;
   } else {
-    // members occupy sa positions gq .. gq + count - 1; their group label is gq
-    const uint32_t gq = 1 + headBase[isaRef[p]] + (sq - it.slot[posBegin[p]]);
-    if (m == 0) gItem[q] = gq;
-    g = gq;
+    // members occupy sa positions g .. g + count - 1; their group label is g
+    g = gBase[p] + sq;
+    if (m == 0) gItem[q] = g;
     act = it.count[q] >= 2 ? 1u : 0u;
   }
   back[Pm[s]] = (unsigned long long)g | ((unsigned long long)act << 32);
 }
 
-// doc side: labels arrive in send order
+// doc side: labels arrive in send order; flags stay in send order
 __global__ void k_dm_grp_init(const uint32_t* __restrict__ perm, const unsigned long long* __restrict__ in, uint64_t n,
                               uint32_t* __restrict__ grp, uint32_t* __restrict__ actFlag) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -115,7 +129,7 @@ __global__ void k_dm_grp_init(const uint32_t* __restrict__ perm, const unsigned 
   const uint32_t i = perm[j];
   const unsigned long long v = in[j];
   grp[i] = (uint32_t)v;
-  actFlag[i] = (uint32_t)(v >> 32);
+  actFlag[j] = (uint32_t)(v >> 32);  // send order
 }
 
 // doubling keys (group of suffix, group of suffix + h), send order; a
@@ -247,28 +261,24 @@ __global__ void k_dm_pack_ranks(const uint32_t* __restrict__ perm, const uint32_
   out[2 * j + 1] = (int32_t)nv;
 }
 
-// position side: nhr in slot order (sorted per item afterwards), and the
-// head characters by slot: the member with head rank hr sits at slot
-// slot[q] + hr - (gItem[q] - 1) of its item, which is where the writer reads
-// BWTheads[hr] (FN:1742-1752)
+// position side: the head characters by slot (the member with head rank hr
+// sits at slot slot[q] + hr - (gItem[q] - 1) of its item, which is where the
+// writer reads BWTheads[hr], FN:1742-1752) and the next-head ranks in slot
+// order (ranked inside their items by k_nhr_rank); one read of the received
+// rank pair per slot
 __global__ void k_dm_load_ranks(const int32_t* __restrict__ in, const uint32_t* __restrict__ Pm,
                                 const uint32_t* __restrict__ itemOfSlot, const ItemsSoA it,
                                 const uint32_t* __restrict__ gItem, const uint8_t* __restrict__ lchar, uint32_t H,
-                                uint8_t* __restrict__ bwtSlot, uint32_t* __restrict__ err) {
+                                uint32_t* __restrict__ nbiS, uint8_t* __restrict__ bwtSlot,
+                                uint32_t* __restrict__ err) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= H) return;
   const uint32_t r = Pm[s], q = itemOfSlot[s];
-  const uint32_t hr = (uint32_t)in[2 * r];
-  const uint32_t k = hr - (gItem[q] - 1);
+  const uint2 w = *(const uint2*)(in + 2ull * r);
+  nbiS[s] = w.y;
+  const uint32_t k = w.x - (gItem[q] - 1);
   if (k < it.count[q]) bwtSlot[it.slot[q] + k] = lchar[r];
   else atomicOr(err, 4u);
-}
-
-// next-head rank of every received head, in received order (k_nhr_rank
-// ranks them inside their items through Pm)
-__global__ void k_dm_nbi(const int32_t* __restrict__ in, uint32_t H, uint32_t* __restrict__ nbi) {
-  const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
-  if (r < H) nbi[r] = (uint32_t)in[2 * r + 1];
 }
 
 // ---- halo: items reaching past this rank's last position into later ranks
@@ -400,16 +410,17 @@ void mk_dm_pack_heads(const uint32_t* perm, const HeadsSoA& h, uint64_t n, int32
 void mk_dm_unpack_heads(const int32_t* in, uint64_t n, const HeadsSoA& h, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_dm_unpack_heads, g1d(n), dim3(256), 0, st, in, n, h);
 }
+void mk_dm_runs(const uint32_t* pos, const uint32_t* tonext, uint64_t H, uint32_t n, int32_t* diff, uint8_t* hasHead,
+                hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_dm_runs, g1d(H), dim3(256), 0, st, pos, tonext, H, n, diff, hasHead);
+}
 void mk_dm_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t Eown,
                      uint32_t* out, hipStream_t st) {
   hipLaunchKernelGGL(k_dm_sa_counts, g1d(n), dim3(256), 0, st, sa, posBegin, slot, n, Eown, out);
 }
 void mk_dm_group_labels(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
-                        const uint32_t* posBegin, const uint32_t* isaRef, const uint32_t* headBase, uint32_t n,
-                        unsigned long long* back, uint32_t* gItem, hipStream_t st) {
-  if (H)
-    hipLaunchKernelGGL(k_dm_group_labels, g1d(H), dim3(256), 0, st, it, itemOfSlot, Pm, H, posBegin, isaRef,
-                       headBase, n, back, gItem);
+                        const uint32_t* gBase, uint32_t n, unsigned long long* back, uint32_t* gItem, hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_dm_group_labels, g1d(H), dim3(256), 0, st, it, itemOfSlot, Pm, H, gBase, n, back, gItem);
 }
 void mk_dm_grp_init(const uint32_t* perm, const unsigned long long* in, uint64_t n, uint32_t* grp, uint32_t* actFlag,
                     hipStream_t st) {
@@ -451,8 +462,8 @@ void mk_dm_load_ranks(const int32_t* in, const uint32_t* Pm, const uint32_t* ite
                       const uint32_t* gItem, const uint8_t* lchar, uint32_t H, uint32_t* nbi, uint8_t* bwtSlot,
                       uint32_t* err, hipStream_t st) {
   if (!H) return;
-  hipLaunchKernelGGL(k_dm_load_ranks, g1d(H), dim3(256), 0, st, in, Pm, itemOfSlot, it, gItem, lchar, H, bwtSlot, err);
-  hipLaunchKernelGGL(k_dm_nbi, g1d(H), dim3(256), 0, st, in, H, nbi);
+  hipLaunchKernelGGL(k_dm_load_ranks, g1d(H), dim3(256), 0, st, in, Pm, itemOfSlot, it, gItem, lchar, H, nbi, bwtSlot,
+                     err);
 }
 void mk_dm_halo_count(const ItemsSoA& it, uint32_t K, const uint32_t* split, uint32_t world, uint32_t rank,
                       uint32_t n, uint32_t* c, hipStream_t st) {

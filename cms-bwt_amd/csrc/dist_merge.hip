@@ -127,7 +127,14 @@ void Engine::dm_group(const int32_t* recv, uint64_t nrecv, uint32_t* saCounts) {
   // range) with the per-SA-rank counts, in saCounts[2n .. 3n]
   runsValid = false;
   group_items(r, Hp, n, dm.IS);
-  if (!runsValid) throw InputError{CMSBWT_EINTERNAL, "internal: run buckets not built by the grouping"};
+  if (!runsValid) {  // grouped by the composite-key sorts (keys wider than 64 bits): count them here
+    diff.alloc((uint64_t)n + 1);
+    diff.zero(st);
+    hasHead.alloc(n);
+    hasHead.zero(st);
+    mk_dm_runs(dm.rPos.p, dm.rTon.p, Hp, n, diff.p, hasHead.p, st);
+    runsValid = true;
+  }
   const uint32_t K = dm.IS.K;
   ItemsSoA S = dm.IS.soa();
   dm.viol = 0;
@@ -163,8 +170,12 @@ void Engine::dm_labels(const uint32_t* saCounts, unsigned long long* back) {
   dm.headBase.alloc(n);
   exscan(saCounts + n, dm.headBase.p, 0u, n);
   dm.gItem.alloc(std::max<uint32_t>(dm.IS.K, 1));
-  mk_dm_group_labels(dm.IS.soa(), dm.itemOfSlot.p, dm.Pm.p, dm.Hp, dm.IS.posBegin.p, disa.p, dm.headBase.p, n, back,
-                     dm.gItem.p, st);
+  {
+    DBuf<uint32_t> gBase;
+    gBase.alloc(n);
+    mk_pos_rank_base(dm.IS.posBegin.p, dm.IS.slot.p, disa.p, nullptr, dm.headBase.p, n, 0, nullptr, gBase.p, st);
+    mk_dm_group_labels(dm.IS.soa(), dm.itemOfSlot.p, dm.Pm.p, dm.Hp, gBase.p, n, back, dm.gItem.p, st);
+  }
   HIPCHK(hipGetLastError());
   sync();
 }
@@ -175,12 +186,12 @@ uint64_t Engine::dm_dbl_init(const unsigned long long* labels) {
   dm.act.alloc(H);
   dm.U = 0;
   if (H) {
-    DBuf<uint32_t> flag, io;
+    // unresolved members listed in send order (the doubling does not depend
+    // on the order of act): one scatter per head, the labels
+    DBuf<uint32_t> flag;
     flag.alloc(H);
-    io.alloc(H);
     mk_dm_grp_init(dm.hPerm.p, labels, H, dm.grp.p, flag.p, st);
-    mk_iota(io.p, H, st);
-    dm.U = select_flagged(io.p, flag.p, dm.act.p, H);
+    dm.U = select_flagged(dm.hPerm.p, flag.p, dm.act.p, H);
   }
   return dm.U;
 }
@@ -268,7 +279,7 @@ void Engine::dm_load_ranks(const int32_t* recv) {
     nbi.alloc(std::max<uint32_t>(Hp, 1));
     mk_dm_load_ranks(recv, dm.Pm.p, dm.itemOfSlot.p, S, dm.gItem.p, dm.rCh.p, Hp, nbi.p, dm.bwtSlot.p, dm.err.p, st);
     if (Hp) {
-      mk_nhr_rank(dm.Pm.p, nbi.p, dm.itemOfSlot.p, Hp, dm.nhr.p, st);
+      mk_nhr_rank(nullptr, nbi.p, dm.itemOfSlot.p, Hp, dm.nhr.p, st);  // nbi in slot order
       sort_nhr_items(S, dm.IS.K, dm.itemOfSlot.p, dm.nhr.p, Hp, true);
     }
   }

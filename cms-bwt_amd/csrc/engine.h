@@ -1142,9 +1142,12 @@ struct Engine {
     // walk with the measured size, so only the first walk of a denser
     // workload pays twice (1 % SNP collections have ~10 % heads)
     if (!densityLearned && nch >= 4096) sample_density(nch);
-    // every launched lane may end holding kPoolBatch - 1 reserved blocks it
-    // never started (config 3: 393 K lanes x 15 x 256 B = 1.5 GB)
-    const uint64_t slack = (uint64_t)std::min<uint32_t>(kWalkLanes, nch) * (kPoolBatch - 1);
+    // lanes launched: the resident ones (chunks come from queues, so a lane
+    // beyond them would only wait for a CU); each may end holding up to
+    // kPoolBatch - 1 reserved blocks it never started (config 3: 262 K lanes
+    // x 15 x 16 heads x 16 B = 1.0 GB of slack against 1.6 GB of heads)
+    const uint32_t lanes = (uint32_t)std::min<uint64_t>({(uint64_t)kWalkLanes, resident_lanes(), (uint64_t)nch});
+    const uint64_t slack = (uint64_t)lanes * (kPoolBatch - 1);
     uint64_t cap = (uint64_t)nch + slack + (uint64_t)((double)chars * poolDensity * 1.1) / kPoolB + 1024;
     DBuf<HeadRec> rec;
     DBuf<uint32_t> blkChunk, blkSeq;
@@ -1160,7 +1163,7 @@ struct Engine {
       Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
       HIPCHK(hipEventRecord(ev0, st));
       launch_ms_walk2(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.bandOrder.p, plan.bandStart.p, plan.nbands,
-                      nextChunk.p, pool, chunkCount.p, kWalkLanes, w2stats.p, st);
+                      nextChunk.p, pool, chunkCount.p, lanes, w2stats.p, st);
       HIPCHK(hipGetLastError());
       HIPCHK(hipEventRecord(ev1, st));
       usedBlocks = read1(used.p);

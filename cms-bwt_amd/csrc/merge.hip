@@ -611,7 +611,7 @@ __global__ void __launch_bounds__(256) k_nhr_rank(const uint32_t* __restrict__ P
   const int64_t base = (int64_t)s0 - kNhrHalo;
   for (uint32_t i = threadIdx.x; i < kNhrBlock + 2 * kNhrHalo; i += blockDim.x) {
     const int64_t j = base + i;
-    if (j >= 0 && j < (int64_t)H) { vL[i] = nbi[Pm[j]]; qL2[i] = itemOfSlot[j]; }
+    if (j >= 0 && j < (int64_t)H) { vL[i] = nbi[Pm ? Pm[j] : (uint32_t)j]; qL2[i] = itemOfSlot[j]; }
   }
   __syncthreads();
   const uint32_t s = s0 + threadIdx.x;

@@ -51,7 +51,8 @@ void mk_head_chars(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint8_t
 void mk_nhr_idx(const uint32_t* headRank, uint32_t sub, const uint16_t* nexthead, uint32_t H, uint32_t* nbi,
                 hipStream_t st);
 void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigList, hipStream_t st);
-// next-head rank of each slot's member ranked inside its item (items <= kSmallSeg)
+// next-head rank of each slot's member ranked inside its item (items <= kSmallSeg);
+// nbi in document order read through Pm, or already in slot order (Pm null)
 void mk_nhr_rank(const uint32_t* Pm, const uint32_t* nbi, const uint32_t* itemOfSlot, uint32_t H, uint32_t* nhr,
                  hipStream_t st);
 void mk_nhr_big_list(const ItemsSoA& it, uint32_t K, uint32_t* bigList, hipStream_t st);
@@ -173,11 +174,12 @@ void mk_dm_owner(const uint32_t* vals, const uint32_t* idx, uint64_t n, const ui
 void mk_dm_bounds(const uint32_t* sorted, uint64_t n, uint32_t world, uint32_t* bounds, hipStream_t st);
 void mk_dm_pack_heads(const uint32_t* perm, const HeadsSoA& h, uint64_t n, int32_t* out, hipStream_t st);
 void mk_dm_unpack_heads(const int32_t* in, uint64_t n, const HeadsSoA& h, hipStream_t st);
+void mk_dm_runs(const uint32_t* pos, const uint32_t* tonext, uint64_t H, uint32_t n, int32_t* diff, uint8_t* hasHead,
+                hipStream_t st);
 void mk_dm_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t Eown,
                      uint32_t* out, hipStream_t st);
 void mk_dm_group_labels(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
-                        const uint32_t* posBegin, const uint32_t* isaRef, const uint32_t* headBase, uint32_t n,
-                        unsigned long long* back, uint32_t* gItem, hipStream_t st);
+                        const uint32_t* gBase, uint32_t n, unsigned long long* back, uint32_t* gItem, hipStream_t st);
 void mk_dm_grp_init(const uint32_t* perm, const unsigned long long* in, uint64_t n, uint32_t* grp, uint32_t* actFlag,
                     hipStream_t st);
 void mk_dm_dbl_pack(const uint32_t* aPerm, const uint32_t* act, const uint32_t* grp, uint32_t h, uint64_t n,
@@ -196,9 +198,9 @@ void mk_dm_dbl_apply(const uint32_t* aPerm, const uint32_t* act, const unsigned 
                      uint32_t* keep, hipStream_t st);
 void mk_dm_pack_ranks(const uint32_t* perm, const uint32_t* grp, const uint16_t* nexthead, uint64_t n, uint32_t H,
                       int32_t* out, uint32_t* err, hipStream_t st);
-// head characters by slot (bwtSlot) and the next-head ranks in received order (nbi)
+// head characters by slot (bwtSlot) and the next-head ranks in slot order (nbiS)
 void mk_dm_load_ranks(const int32_t* in, const uint32_t* Pm, const uint32_t* itemOfSlot, const ItemsSoA& it,
-                      const uint32_t* gItem, const uint8_t* lchar, uint32_t H, uint32_t* nbi, uint8_t* bwtSlot,
+                      const uint32_t* gItem, const uint8_t* lchar, uint32_t H, uint32_t* nbiS, uint8_t* bwtSlot,
                       uint32_t* err, hipStream_t st);
 void mk_dm_halo_count(const ItemsSoA& it, uint32_t K, const uint32_t* split, uint32_t world, uint32_t rank,
                       uint32_t n, uint32_t* c, hipStream_t st);

@@ -105,6 +105,18 @@ __device__ __forceinline__ uint4 ldu16(uintptr_t a) {
   const u4u v = *GPTR(u4u, a);
   return make_uint4(v.x, v.y, v.z, v.w);
 }
+// non-temporal forms for bytes read once (the text of long extensions, the
+// prefix-table probes): measured 15.12 -> 14.96 ms with both (r03 A/B)
+__device__ __forceinline__ uint4 ldu16_nt(uintptr_t a) {
+  typedef uint32_t u4u __attribute__((ext_vector_type(4), aligned(1)));
+  const u4u v = __builtin_nontemporal_load(GPTR(u4u, a));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+__device__ __forceinline__ uint2 ld8_nt(uintptr_t a) {
+  typedef uint32_t u2u __attribute__((ext_vector_type(2), aligned(4)));
+  const u2u v = __builtin_nontemporal_load(GPTR(u2u, a));
+  return make_uint2(v.x, v.y);
+}
 // slot loads of one step (`use` bits)
 enum : uint32_t {
   U0B = 1,    // byte at A
@@ -119,6 +131,7 @@ enum : uint32_t {
   U5Q = 512,  // 16 B at A + 48
   U0E = 1024, // 8 B at A
   U2E = 2048, // 8 B at B
+  UREG = 4096, // (no load) the probe's next window comes from the skip's 32 text bytes
 };
 // First differing byte of two 16-byte strings: 16 if equal.
 __device__ __forceinline__ uint32_t diff16(const uint4& x, const uint4& t, uint8_t& xc, uint8_t& tc) {
@@ -254,6 +267,12 @@ struct Walk2Args {
 };
 
 constexpr uint32_t kCoopJ = 4;  // 16-B pieces per thread per cooperative round
+// pending long extensions served together (r03 A/B, walk kernel: 1 -> 15.12 ms,
+// 4 -> 14.74 ms: a round trip of the wave serves four slots instead of ~2)
+#ifndef CMSBWT_COOP_MIN
+#define CMSBWT_COOP_MIN 4
+#endif
+constexpr uint32_t kCoopMin = CMSBWT_COOP_MIN;
 // waves per SIMD of the walk (Makefile W2WAVES; measured 3 -> 16.50 ms,
 // 4 -> 16.44-16.68, 5 -> 16.9, 6 -> 31.3 with register spills)
 #ifndef CMSBWT_W2_WAVES
@@ -296,6 +315,11 @@ k_ms_walk2(Walk2Args A) {
   // code of its first wm <= K symbols in wcode
   uint4 tw = make_uint4(0, 0, 0, 0);
   uint32_t twAt = 0xffffffffu, wcode = 0, wm = 0;
+  // the 32 text bytes t[t32At ..) the last skip step loaded around the match
+  // end: the probes of the next positions (a mismatch region) take their
+  // windows from them instead of loading the text again
+  uint4 t32a = make_uint4(0, 0, 0, 0), t32b = t32a;
+  uint32_t t32At = 0xfffffff0u;
   // emission
   // pool blocks are reserved kPoolBatch at a time (blk .. blkEnd) and kept
   // across this lane's chunks; blocks never started keep blkChunk = ~0
@@ -375,8 +399,12 @@ k_ms_walk2(Walk2Args A) {
     ad0 = (uintptr_t)(R.pfx + pfxL[m] + 2 * code);
     use = U0E;
     if (R.pfxExact) {
-      ad2 = T + i + 1;
-      use |= U2Q;
+      if (i + 1 - t32At <= 16u) {
+        use |= UREG;
+      } else {
+        ad2 = T + i + 1;
+        use |= U2Q;
+      }
     } else if (len > 0) {
       ad2 = (uintptr_t)(R.pfx + pfxL[len] + 2 * (code >> (Bb * (m - len))));
       use |= U2E;
@@ -524,6 +552,7 @@ k_ms_walk2(Walk2Args A) {
           prevPos = 0xfffffffeu;  // prevPos + 1 never equals a position
           smaller = false;
           twAt = 0xffffffffu;
+          t32At = 0xfffffff0u;  // (another document's bytes)
           if (R.pfx) {
             phase = PH_PFX_TEXT;
             ad0 = T + i;
@@ -656,7 +685,7 @@ k_ms_walk2(Walk2Args A) {
     if (use & U3Q) v3 = ldu16(ad2 + 16);
     if (use & U4Q) v4 = ldu16(ad0 + 32);
     if (use & U5Q) v5 = ldu16(ad0 + 48);
-    if (use & U0E) { const uint2 w = ld8(ad0); v0.x = w.x; v0.y = w.y; }
+    if (use & U0E) { const uint2 w = ld8_nt(ad0); v0.x = w.x; v0.y = w.y; }
     if (use & U2E) { const uint2 w = ld8(ad2); v2.x = w.x; v2.y = w.y; }
     // PLCP skip (FN:1176-1185): the exit inside the 16-entry window below
     // the match end, if it is there (skS = the skip, or ~0u)
@@ -681,14 +710,21 @@ k_ms_walk2(Walk2Args A) {
     // the text window this step loaded (one call site: the code is emitted once)
     {
       const bool wa = phase == PH_PFX_TEXT || phase == PH_SKTXT;
-      const bool ws = phase == PH_SKIP1 && skS != 0xffffffffu && R.pfxExact && R.pfx && len - skS < R.kmerK;
+      const bool sk = phase == PH_SKIP1 && R.pfxExact && R.pfx;  // the skip loaded 32 text bytes
+      const bool ws = sk && skS != 0xffffffffu && len - skS < R.kmerK;
+      const bool wr = (use & UREG) != 0;
+      if (sk) {
+        t32a = v2;
+        t32b = v3;
+        t32At = skip_text_base();
+      }
       if (wa || ws || (phase == PH_PFX_PROBE && R.pfxExact)) {
         uint4 vv = make_uint4(wa ? v0.x : v2.x, wa ? v0.y : v2.y, wa ? v0.z : v2.z, wa ? v0.w : v2.w);
         uint32_t at = phase == PH_PFX_TEXT ? i : i + 1;
-        if (ws) {  // bytes o..o+15 of the 32 loaded (v2, v3), o = next position - base
-          at = i + skS + 1;
-          const uint32_t o = at - skip_text_base();
-          uint32_t d[8] = {v2.x, v2.y, v2.z, v2.w, v3.x, v3.y, v3.z, v3.w};
+        if (ws || wr) {  // bytes o..o+15 of the 32 skip bytes, o = next position - their base
+          if (ws) at = i + skS + 1;
+          const uint32_t o = at - t32At;
+          uint32_t d[8] = {t32a.x, t32a.y, t32a.z, t32a.w, t32b.x, t32b.y, t32b.z, t32b.w};
           if (o & 16) { d[0] = d[4]; d[1] = d[5]; d[2] = d[6]; d[3] = d[7]; d[4] = d[5] = d[6] = d[7] = 0; }
           if (o & 8) { d[0] = d[2]; d[1] = d[3]; d[2] = d[4]; d[3] = d[5]; d[4] = d[6]; d[5] = d[7]; }
           if (o & 4) { d[0] = d[1]; d[1] = d[2]; d[2] = d[3]; d[3] = d[4]; d[4] = d[5]; }
@@ -1004,8 +1040,11 @@ k_ms_walk2(Walk2Args A) {
     // kCoopJ 16-byte pieces per round, piece j of thread k at byte
     // 16 (k + W j), so a slot covers 16 W kCoopJ contiguous bytes per round
     // (4 KiB for a single lane).  A slot ends at its first mismatch.
+    // Pending lanes wait (idle, no load) until kCoopMin of them can share the
+    // wave's round trips, unless no other lane of the wave is still walking.
     uint64_t coop = __ballot(phase == PH_LCE_COOP);
-    while (coop) {
+    const bool drain = coop == __ballot(phase != PH_DONE);
+    while (coop && (drain || (uint32_t)__popcll(coop) >= kCoopMin)) {
       const uint32_t P = (uint32_t)__popcll(coop);
       const uint32_t S = P >= 4 ? 4u : P >= 2 ? 2u : 1u;
       const uint32_t lgW = S == 4 ? 4u : S == 2 ? 5u : 6u;
@@ -1036,7 +1075,7 @@ k_ms_walk2(Walk2Args A) {
           for (uint32_t j = 0; j < JR; j++) {
             const uint32_t o = run + 16 * (k + (j << lgW));
             xv[j] = ldu16(xa + o);
-            tv[j] = ldu16(ta + o);
+            tv[j] = ldu16_nt(ta + o);
           }
 #pragma unroll
           for (int j = (int)JR - 1; j >= 0; j--) {

@@ -176,7 +176,10 @@ def gpu_sharded_files(rank, world, port, work):
     x = cdist.Transport("cuda:0")
     cdist.sharded_step(eng, "cuda:0", rle=cfg["rle"], xfer=x)
     if rank == 0:
-        open(os.path.join(work, "runs0.bin"), "wb").write(eng.runs_bytes())
+        if cfg.get("out"):  # the output file itself (plain .bwt expanded on the device)
+            eng.write_output(cfg["out"], rle=cfg["rle"])
+        else:
+            open(os.path.join(work, "runs0.bin"), "wb").write(eng.runs_bytes())
         json.dump(eng.stats().as_dict(), open(os.path.join(work, "stats.json"), "w"))
     eng.close()
     dist.destroy_process_group()

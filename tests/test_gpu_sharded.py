@@ -44,6 +44,29 @@ def test_sharded_world1_matches_oracle(engine, oracle, tmp_path, case, rle):
     assert (st.counter_bad, st.counter_good, st.counter_nothing) == (ost["bad"], ost["good"], ost["nothing"])
 
 
+@pytest.mark.parametrize("env", ["CMSBWT_GROUP3", "CMSBWT_GROUP64"])
+@pytest.mark.parametrize("case", [c for c in cases.small_cases() if c[0] in ("copies_5k_1pct", "tiny_docs",
+                                                                         "copies_20k_multiline")],
+                         ids=lambda c: c[0])
+def test_sharded_world1_composite_key_grouping(engine, oracle, tmp_path, case, env):
+    """The grouping paths other than the position-first sort (taken when
+    2 * bits(n) + bits(max len) > 64, e.g. config 5's 100 MB reference with
+    long matches): the sharded merge then counts the run buckets of the
+    received heads itself (k_dm_runs); bytes equal the oracle's."""
+    import cmsbwt.dist as cdist
+    d, rp, cp, prefix, ost, want = _oracle_files(oracle, tmp_path, case, True)
+    os.environ[env] = "1"
+    try:
+        engine.initialize_reference(rp)
+        engine.load_collection_file(cp, prefix)
+        cdist.sharded_step(engine, "cuda:0", rle=True, xfer=cdist.Transport("cuda:0", 1, 0))
+    finally:
+        del os.environ[env]
+    assert engine.runs_bytes() == want
+    st = engine.stats()
+    assert (st.heads, st.keys, st.rank) == (ost["heads"], ost["keys"], ost["rank"])
+
+
 def _multi(oracle, tmp_path, case, world, rle, steps=1):
     d, rp, cp, prefix, ost, want = _oracle_files(oracle, tmp_path, case, rle)
     docs, _ = cases.py_read_docs(open(cp, "rb").read(), prefix)
@@ -160,3 +183,31 @@ def test_sharded_eight_ranks_config2_files_golden(tmp_path):
     assert (st["counter_bad"], st["counter_good"], st["counter_nothing"]) == \
         (g["t3"]["counterBad"], g["t3"]["counterGood"], g["t3"]["counterDoNothing"])
     assert hashlib.sha256(open(os.path.join(work, "runs0.bin"), "rb").read()).hexdigest() == g["t3"]["rl_bwt_sha256"]
+
+
+def test_sharded_four_ranks_config5_proxy_plain_golden(tmp_path):
+    """BASELINE config 5's shape (100 MB reference, 1 % SNP, plain .bwt) on the
+    multi-GPU path: 4 ranks (gloo, sharing the test GPU) read their byte ranges
+    of the c5p proxy's FASTA (4 copies, numpy generator seed 5) and run the
+    position-sharded merge; rank 0 writes the plain .bwt, whose sha256 equals
+    the oracle's (golden c5p), with the oracle's head / rank / counter counts."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(__file__), "golden"))
+    import gen_np
+    from test_gpu_parity import _sha_file
+    g = json.load(open(os.path.join(os.path.dirname(__file__), "golden", "golden.json")))["c5p"]
+    L, C, p, seed, _ = g["args"]
+    pre = str(tmp_path / "c5p")
+    gen_np.gen(L, C, p, seed, pre)
+    work = str(tmp_path)
+    out = str(tmp_path / "c5p_out")
+    json.dump({"ref": pre + ".ref.fa", "coll": pre + ".coll.fa", "rle": False, "out": out},
+              open(os.path.join(work, "cfg.json"), "w"))
+    spawn("gpu_sharded_files", 4, work, timeout=600)
+    st = json.load(open(os.path.join(work, "stats.json")))
+    assert st["heads"] == g["headNumber"]
+    assert st["rank"] == g["Rank"]
+    assert (st["counter_bad"], st["counter_good"], st["counter_nothing"]) == \
+        (g["counterBad"], g["counterGood"], g["counterDoNothing"])
+    assert os.path.getsize(out + ".bwt") == g["bwt_bytes"]
+    assert _sha_file(out + ".bwt") == g["bwt_sha256"]
