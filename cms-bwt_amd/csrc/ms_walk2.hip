@@ -269,10 +269,7 @@ struct Walk2Args {
 constexpr uint32_t kCoopJ = 4;  // 16-B pieces per thread per cooperative round
 // pending long extensions served together (r03 A/B, walk kernel: 1 -> 15.12 ms,
 // 4 -> 14.74 ms: a round trip of the wave serves four slots instead of ~2)
-#ifndef CMSBWT_COOP_MIN
-#define CMSBWT_COOP_MIN 4
-#endif
-constexpr uint32_t kCoopMin = CMSBWT_COOP_MIN;
+constexpr uint32_t kCoopMin = 4;  // (3: 14.58 ms, 5: 15.6, 6: 16.1, 8: 17.1: pending lanes idle longer)
 // waves per SIMD of the walk (Makefile W2WAVES; measured 3 -> 16.50 ms,
 // 4 -> 16.44-16.68, 5 -> 16.9, 6 -> 31.3 with register spills)
 #ifndef CMSBWT_W2_WAVES
