@@ -69,7 +69,8 @@ class Stats(ctypes.Structure):
         [(k, ctypes.c_uint64) for k in ("ref_file_bytes", "ref_read_size", "coll_file_bytes", "sn_initial")] + \
         [(k, ctypes.c_int64) for k in ("first_rank_to_head", "last_rank_to_head")] + \
         [(k, ctypes.c_double) for k in ("t_augment_ms", "t_sa_ms", "t_isa_ms", "t_lcp_ms", "t_rmq_ms", "t_bwt_ms",
-                                        "t_ranks_ms", "t_libsais_int_ms", "t_counter_ms")]
+                                        "t_ranks_ms", "t_libsais_int_ms", "t_counter_ms")] + \
+        [("host_queries", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

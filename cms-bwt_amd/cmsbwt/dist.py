@@ -204,7 +204,7 @@ def sharded_step(eng, device, rle: bool = True, xfer: Transport = None):
 
 
 def sharded_merge(eng, x: Transport, rle: bool = True):
-    from . import CMSBWT_EINPUT, CMSBWT_EORDER, CmsBwtError
+    from . import CMSBWT_EINPUT, CmsBwtError
     world, rank = x.world, x.rank
     st = eng.stats()
     H, n = int(st.heads), int(st.n)
@@ -271,7 +271,22 @@ def sharded_merge(eng, x: Transport, rle: bool = True):
     if errs:
         raise CmsBwtError(CMSBWT_EINPUT, "counter target beyond the reference (reference UB)")
     if viol:
-        raise CmsBwtError(CMSBWT_EORDER, f"MatchInSet comparator is not a strict weak order on this input ({viol})")
+        # match.h:27-33 is not a strict weak order on this input (DESIGN.md
+        # §5).  The std::map replay that reproduces the reference's layout
+        # runs in the one-GPU merge, so the step is redone as a gather step:
+        # walk again, every head to rank 0, merge there.
+        eng.ms_walk()
+        if world == 1:
+            eng.merge(rle)
+            return Htot, E, chars
+        dev = "cpu" if x.staged else x.device
+        st = eng.stats()
+        local = export_walk(eng, dev)
+        combined, totals = gather_walk(local, (st.heads, st.ndocs, st.chars, st.order_invariant), dev, 0)
+        if rank == 0:
+            import_walk(eng, combined, totals)
+            eng.merge(rle)
+        return Htot, E, chars
     # 6. writer units, emission, gather to rank 0
     Uw = E + n - 1
     units = x.empty(2 * Uw, i64)

@@ -142,7 +142,7 @@ void Engine::dm_group(const int32_t* recv, uint64_t nrecv, uint32_t* saCounts) {
     DBuf<unsigned long long> v;
     v.alloc(1);
     v.zero(st);
-    mk_check_items(S, dm.IS.posBegin.p, dm.IS.posF.p, K, v.p, st);
+    mk_check_items(S, dm.IS.posBegin.p, dm.IS.posF.p, K, v.p, nullptr, st);
     dm.viol = read1(v.p);
   }
   // slot-major members: item of each slot, received index of each slot

@@ -40,6 +40,7 @@
 #include "host_index.h"
 #include "host_reader.h"
 #include "kernels.h"
+#include "map_replay.h"
 #include "merge_kernels.h"
 #include "synth.h"
 
@@ -1497,7 +1498,18 @@ struct Engine {
   // window from the left in its crossing list (items before P0 included).
   void counter_phase(const ItemsSoA& S, uint32_t K, const uint32_t* posBegin, const uint32_t* posF,
                      const uint32_t* nhrP, unsigned long long* counterP, unsigned long long* cstatsP, uint32_t n,
-                     uint32_t P0, uint32_t P1, bool check) {
+                     uint32_t P0, uint32_t P1, bool check, const HostRoute* hr = nullptr) {
+    // checked queries without a host route: nothing masked, ambiguity only counted
+    HostRoute none;
+    DBuf<uint8_t> noneMask, noneAmb;
+    DBuf<unsigned long long> noneCnt;
+    if (check && !hr) {
+      noneMask.alloc(n); noneMask.zero(st);
+      noneAmb.alloc(n);
+      noneCnt.alloc(1); noneCnt.zero(st);
+      none = HostRoute{noneMask.p, noneAmb.p, nullptr, noneCnt.p, 0};
+      hr = &none;
+    }
     // windows over reference positions
     DBuf<uint32_t> wflag, wincl, winStart, crossCnt, crossOff, crossList;
     wflag.alloc(n);
@@ -1537,7 +1549,7 @@ struct Engine {
       mk_counter_tgt(S, posBegin, posF, nhrP, winStart.p, nw, crossOff.p, crossList.p, counterP, cstatsP, n, st);
     else
       mk_counter_win(S, posBegin, posF, nhrP, winStart.p, nw, crossOff.p, crossList.p, counterP, cstatsP, n,
-                     slotCap, check, st);
+                     slotCap, check ? hr : nullptr, st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev1, st));
     sync();
@@ -1546,6 +1558,115 @@ struct Engine {
     counter_kernel_ms = ms;
     windows = nw;
     crossings = ncross;
+  }
+
+  // ---- comparator-ambiguity fallback (map_replay.h)
+  template <class T_>
+  std::vector<T_> down(const T_* d, uint64_t k) {
+    std::vector<T_> v(k);
+    if (k) HIPCHK(hipMemcpyAsync(v.data(), d, k * sizeof(T_), hipMemcpyDeviceToHost, st));
+    sync();
+    return v;
+  }
+  template <class T_>
+  void up(DBuf<T_>& b, const std::vector<T_>& v) {
+    b.alloc(v.size());
+    if (!v.empty()) HIPCHK(hipMemcpyAsync(b.p, v.data(), v.size() * sizeof(T_), hipMemcpyHostToDevice, st));
+    sync();
+  }
+  HostItems download_items(ItemSet& IS, uint32_t n) {
+    HostItems I;
+    const uint32_t k = IS.K;
+    I.pos = down(IS.pos.p, k); I.len = down(IS.len.p, k); I.isa = down(IS.isa.p, k);
+    I.until = down(IS.until.p, k); I.count = down(IS.count.p, k); I.first = down(IS.first.p, k);
+    I.small = down(IS.small.p, k);
+    I.P = down(IS.P.p, H);
+    I.posBegin = down(IS.posBegin.p, (uint64_t)n + 1);
+    return I;
+  }
+  // Rebuild the items of the flagged positions from a host std::map replay of
+  // their insertions (FN:1401-1414); every array derived from the items is
+  // recomputed (K may change).
+  void replay_item_positions(ItemSet& IS, const HeadsSoA& h, const uint8_t* maskD, uint32_t n) {
+    HostItems I = download_items(IS, n);
+    replay_items(I, down(maskD, n), down(h.smaller, H), down(h.tonext, H));
+    const uint32_t k = (uint32_t)I.pos.size();
+    up(IS.pos, I.pos); up(IS.len, I.len); up(IS.isa, I.isa); up(IS.until, I.until);
+    up(IS.count, I.count); up(IS.first, I.first); up(IS.small, I.small); up(IS.P, I.P);
+    IS.K = k;
+    IS.slot.alloc((uint64_t)k + 1);
+    IS.sk.alloc(k);
+    ItemsSoA SS = IS.soa();
+    mk_item_sk(SS, k, st);
+    exscan(IS.count.p, IS.slot.p, 0u, k);
+    uint32_t hh = H;
+    HIPCHK(hipMemcpyAsync(IS.slot.p + k, &hh, 4, hipMemcpyHostToDevice, st));
+    mk_pos_begin(IS.pos.p, k, n, IS.posBegin.p, st);
+    mk_pos_f(IS.pos.p, IS.small.p, IS.posBegin.p, k, n, IS.posF.p, st);
+    sync();  // hh is a stack variable
+  }
+  // Checked counter (FN:1523-1603): the device answers every query whose
+  // target is unmasked and unambiguous; a pass that meets an ambiguous query
+  // masks its target and the counters are recomputed, so every query into a
+  // masked target is answered by the host replay (host_queries).  Returns the
+  // ambiguous queries of the first pass; cs receives the final statistics.
+  uint64_t hostQueries = 0;
+  uint64_t counter_checked(ItemSet& IS, const HeadsSoA& h, DBuf<uint32_t>& nhr, DBuf<uint8_t>& hostMask,
+                           DBuf<unsigned long long>& cstats, uint32_t n, unsigned long long* cs) {
+    ItemsSoA S = IS.soa();
+    const uint32_t k = IS.K;
+    DBuf<uint8_t> amb;
+    amb.alloc(n);
+    amb.zero(st);
+    DBuf<unsigned long long> hcnt;
+    hcnt.alloc(1);
+    uint64_t cap = 1ull << 16, nq = 0, firstViol = 0;
+    DBuf<uint32_t> hlist;
+    hlist.alloc(2 * cap);
+    for (int pass = 0;; pass++) {
+      if (pass > 3) throw InputError{CMSBWT_EINTERNAL, "internal: checked counter did not settle"};
+      counter.zero(st);
+      cstats.zero(st);
+      hcnt.zero(st);
+      HostRoute hr{hostMask.p, amb.p, hlist.p, hcnt.p, cap};
+      counter_phase(S, k, IS.posBegin.p, IS.posF.p, nhr.p, counter.p, cstats.p, n, 0, n, true, &hr);
+      HIPCHK(hipMemcpyAsync(cs, cstats.p, 8 * sizeof(unsigned long long), hipMemcpyDeviceToHost, st));
+      nq = read1(hcnt.p);
+      if (pass == 0) firstViol = cs[3];
+      if (cs[3]) {  // targets with ambiguous queries join the host replay
+        mk_or_mask(hostMask.p, amb.p, n, st);
+        continue;
+      }
+      if (nq > cap) {
+        cap = nq;
+        hlist.alloc(2 * cap);
+        continue;
+      }
+      break;
+    }
+    hostQueries = nq;
+    if (nq) {
+      HostItems I = download_items(IS, n);
+      const std::vector<uint32_t> lst = down(hlist.p, 2 * nq);
+      std::vector<std::pair<uint32_t, uint32_t>> q(nq);
+      for (uint64_t i = 0; i < nq; i++) q[i] = {lst[2 * i], lst[2 * i + 1]};
+      bool mismatch = false;
+      HostQueryOut o = host_queries(I, down(IS.slot.p, (uint64_t)k + 1), down(nhr.p, H), down(h.smaller, H),
+                                    std::move(q), &mismatch);
+      if (mismatch) throw InputError{CMSBWT_EINTERNAL, "internal: replayed std::map differs from the device items"};
+      std::vector<uint32_t> as(o.adds.size());
+      std::vector<unsigned long long> av(o.adds.size());
+      for (size_t i = 0; i < o.adds.size(); i++) { as[i] = o.adds[i].first; av[i] = o.adds[i].second; }
+      DBuf<uint32_t> das;
+      DBuf<unsigned long long> dav;
+      up(das, as);
+      up(dav, av);
+      mk_counter_adds(das.p, dav.p, (uint32_t)as.size(), counter.p, st);
+      sync();
+      cs[0] += o.bad;
+      cs[1] += o.good;
+    }
+    return firstViol;
   }
 
   void merge(int rle) {
@@ -1573,7 +1694,25 @@ struct Engine {
     DBuf<unsigned long long> cstats;
     cstats.alloc(8);
     cstats.zero(st);
-    if (!orderInvariant || env_u32("CMSBWT_FORCE_CHECK", 0)) mk_check_items(S, posBegin.p, posF.p, K, cstats.p + 3, st);
+    // Comparator ambiguity (match.h:27-33): positions whose
+    // items break the map-order invariant get their std::map layout replayed
+    // on the host, and every counter query into them is answered there.
+    // CMSBWT_FORCE_REPLAY=1 routes every position through that path (tests).
+    const bool forceReplay = env_u32("CMSBWT_FORCE_REPLAY", 0) != 0;
+    const bool check = !orderInvariant || forceReplay || env_u32("CMSBWT_FORCE_CHECK", 0) != 0;
+    DBuf<uint8_t> hostMask;  // positions answered by the host replay
+    uint64_t itemViol = 0;
+    if (check) {
+      hostMask.alloc(n);
+      HIPCHK(hipMemsetAsync(hostMask.p, forceReplay ? 1 : 0, n, st));
+      mk_check_items(S, posBegin.p, posF.p, K, cstats.p + 3, hostMask.p, st);
+      itemViol = read1(cstats.p + 3);
+      if (itemViol || forceReplay) {
+        replay_item_positions(IS, h, hostMask.p, n);
+        K = IS.K;
+        S = IS.soa();
+      }
+    }
 
     // ---- ranks (FN:1432-1453)
     HIPCHK(hipEventRecord(evm[0], st));
@@ -1727,26 +1866,27 @@ struct Engine {
       HIPCHK(rocprim::reduce(nullptr, b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
       HIPCHK(rocprim::reduce(scratch(b), b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
       W = read1(wsum.p);
-      const bool check = !orderInvariant || env_u32("CMSBWT_FORCE_CHECK", 0) != 0;
       HIPCHK(hipEventRecord(evm[4], st));
-      counter_phase(S, K, posBegin.p, posF.p, nhr.p, counter.p, cstats.p, n, 0, n, check);
+      if (!check) counter_phase(S, K, posBegin.p, posF.p, nhr.p, counter.p, cstats.p, n, 0, n, false);
       HIPCHK(hipEventRecord(evm[5], st));
     }
     unsigned long long cs[8];
-    HIPCHK(hipMemcpyAsync(cs, cstats.p, sizeof(cs), hipMemcpyDeviceToHost, st));
-    sync();
+    uint64_t queryViol = 0;
+    if (check) {
+      queryViol = counter_checked(IS, h, nhr, hostMask, cstats, n, cs);
+    } else {
+      HIPCHK(hipMemcpyAsync(cs, cstats.p, sizeof(cs), hipMemcpyDeviceToHost, st));
+      sync();
+    }
     if (env_u32("CMSBWT_COUNTER_STATS", 0))
       fprintf(stderr, "[counter] bad %llu good %llu nothing %llu windows %u crossings %u searched %llu\n", cs[0], cs[1],
               cs[2], windows, crossings, cs[5]);
     stats.counter_bad = cs[0];
     stats.counter_good = cs[1];
     stats.counter_nothing = cs[2];
-    stats.order_violations = cs[3];
+    stats.order_violations = itemViol + queryViol;
+    stats.host_queries = hostQueries;
     if (cs[4]) throw InputError{CMSBWT_EINPUT, "counter target beyond the reference (reference UB)"};
-    if (cs[3]) throw InputError{CMSBWT_EORDER,
-                                "MatchInSet comparator is not a strict weak order on this input (" +
-                                    std::to_string(cs[3]) + " ambiguous comparisons); std::map layout would "
-                                    "depend on insertion history"};
     W_work = W;
     stats.counter_kernel_ms = counter_kernel_ms;
     stats.counter_work = W;

@@ -242,7 +242,7 @@ __global__ void k_pos_f(const uint32_t* __restrict__ ipos, const uint8_t* __rest
 // std::map's layout depends on insertion history.
 __global__ void k_check_items(const ItemsSoA it, const uint32_t* __restrict__ posBegin,
                               const uint32_t* __restrict__ posF, uint32_t K,
-                              unsigned long long* __restrict__ violations) {
+                              unsigned long long* __restrict__ violations, uint8_t* __restrict__ amb) {
   uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= K || !it.smaller[q]) return;
   uint32_t p = it.pos[q], L = it.len[q];
@@ -254,7 +254,10 @@ __global__ void k_check_items(const ItemsSoA it, const uint32_t* __restrict__ po
     uint32_t m = (lo + hi) >> 1;
     if (it.len[m] > L) lo = m + 1; else hi = m;
   }
-  if (lo < e && it.len[lo] == L && it.isa[lo] <= it.isa[q]) atomicAdd(violations, 1ull);
+  if (lo < e && it.len[lo] == L && it.isa[lo] <= it.isa[q]) {
+    atomicAdd(violations, 1ull);
+    if (amb) amb[p] = 1;  // this position's map layout is replayed on the host
+  }
 }
 
 // per SA rank: items and heads of position SA[r] (r = 0 -> position n-1 is
@@ -694,9 +697,10 @@ struct CounterArgs {
   const uint32_t* crossOff;  // nw + 1
   const uint32_t* crossList;
   unsigned long long* counter;
-  unsigned long long* stats; // bad, good, nothing, violations, errors
+  unsigned long long* stats; // bad, good, nothing, violations, errors, searched, ambiguous queries
   uint32_t n;
   uint32_t slotCap;          // windows with more slots use global atomics
+  HostRoute hr;              // CHECK only: targets answered by the host std::map replay
 };
 
 struct QueryStats {  // per lane; a lane serves far fewer than 2^32 queries per window
@@ -725,9 +729,18 @@ __device__ __forceinline__ uint32_t d_lower_u64(const unsigned long long* a, uin
 // positions either from LDS (staged window) or from global memory.
 template <bool CHECK, class View, class AddFn>
 __device__ __forceinline__ void d_counter_query_L(const View& V, uint32_t L, uint32_t qi, bool S, uint32_t cq,
-                                                  uint32_t slq, uint32_t t, QueryStats& qs, AddFn add) {
+                                                  uint32_t slq, uint32_t t, QueryStats& qs, AddFn add,
+                                                  const HostRoute* hr = nullptr) {
   const uint32_t b0 = V.begin(t), b1 = V.begin(t + 1);
   if (b0 == b1) { qs.nothing++; return; }  // bucket >= 0: no heads at t (FN:1530)
+  if (CHECK && hr->mask[t]) {  // answered by the host's std::map replay of t
+    const unsigned long long e = atomicAdd(hr->cnt, 1ull);
+    if (e < hr->cap) {
+      hr->list[2 * e] = slq;
+      hr->list[2 * e + 1] = t;
+    }
+    return;
+  }
   const uint32_t f = V.fbeg(t);
   const unsigned long long kT = ((unsigned long long)L << 32) | qi;
   const unsigned long long kF = ((unsigned long long)(~L) << 32) | qi;
@@ -743,13 +756,19 @@ __device__ __forceinline__ void d_counter_query_L(const View& V, uint32_t L, uin
     ans = lower(b0, f, kT);
     if (CHECK) {  // an F item with len == L and isa < I breaks monotonicity
       uint32_t l3 = lower(f, b1, (unsigned long long)(~L) << 32);
-      if (l3 < b1 && (uint32_t)~(V.sk(l3) >> 32) == L && (uint32_t)V.sk(l3) < qi) qs.viol++;
+      if (l3 < b1 && (uint32_t)~(V.sk(l3) >> 32) == L && (uint32_t)V.sk(l3) < qi) {
+        qs.viol++;
+        hr->amb[t] = 1;
+      }
     }
   } else {
     if (CHECK) {  // a T item with len == L and isa >= I breaks monotonicity
       uint32_t l3 = (unsigned long long)L + 1 > 0xffffffffull ? f
                                                               : lower(b0, f, (unsigned long long)(L + 1u) << 32);
-      if (l3 > b0 && (uint32_t)(V.sk(l3 - 1) >> 32) == L && (uint32_t)V.sk(l3 - 1) >= qi) qs.viol++;
+      if (l3 > b0 && (uint32_t)(V.sk(l3 - 1) >> 32) == L && (uint32_t)V.sk(l3 - 1) >= qi) {
+        qs.viol++;
+        hr->amb[t] = 1;
+      }
     }
     ans = lower(f, b1, kF);
   }
@@ -786,8 +805,8 @@ __device__ __forceinline__ void d_counter_query_L(const View& V, uint32_t L, uin
 template <bool CHECK, class View, class AddFn>
 __device__ __forceinline__ void d_counter_query(const View& V, uint32_t ql, uint32_t qi, bool S, uint32_t cq,
                                                 uint32_t slq, uint32_t k, uint32_t t, QueryStats& qs,
-                                                AddFn add) {
-  d_counter_query_L<CHECK>(V, ql - 1 - k, qi, S, cq, slq, t, qs, add);  // uint32 wrap as FN:1532
+                                                AddFn add, const HostRoute* hr = nullptr) {
+  d_counter_query_L<CHECK>(V, ql - 1 - k, qi, S, cq, slq, t, qs, add, hr);  // uint32 wrap as FN:1532
 }
 
 // item/position views: global memory, or the block's staged window in LDS
@@ -1000,8 +1019,8 @@ __global__ void __launch_bounds__(512) k_counter_win(CounterArgs A) {
           const uint32_t t = t0 + lane;
           if (t <= hi) {
             const uint32_t k = t - p - 1;
-            if (lds) d_counter_query<CHECK>(LV, ql, qi, S, cq, slq, k, t, qs, addLds);
-            else d_counter_query<CHECK>(GV, ql, qi, S, cq, slq, k, t, qs, addGlb);
+            if (lds) d_counter_query<CHECK>(LV, ql, qi, S, cq, slq, k, t, qs, addLds, &A.hr);
+            else d_counter_query<CHECK>(GV, ql, qi, S, cq, slq, k, t, qs, addGlb, &A.hr);
           }
         }
       }
@@ -1939,8 +1958,8 @@ void mk_pos_f(const uint32_t* ipos, const uint8_t* ism, const uint32_t* posBegin
   hipLaunchKernelGGL(k_pos_f, g1(n), dim3(256), 0, st, ipos, ism, posBegin, K, n, posF);
 }
 void mk_check_items(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, uint32_t K,
-                    unsigned long long* viol, hipStream_t st) {
-  if (K) hipLaunchKernelGGL(k_check_items, g1(K), dim3(256), 0, st, it, posBegin, posF, K, viol);
+                    unsigned long long* viol, uint8_t* amb, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_check_items, g1(K), dim3(256), 0, st, it, posBegin, posF, K, viol, amb);
 }
 void mk_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t E,
                   uint32_t* itemsSA, uint32_t* headsSA, hipStream_t st) {
@@ -2011,20 +2030,36 @@ void mk_item_sk(const ItemsSoA& it, uint32_t K, hipStream_t st) {
 }
 void mk_counter_win(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
                     const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
-                    unsigned long long* counter, unsigned long long* stats, uint32_t n, uint32_t slotCap, bool check,
-                    hipStream_t st) {
+                    unsigned long long* counter, unsigned long long* stats, uint32_t n, uint32_t slotCap,
+                    const HostRoute* hr, hipStream_t st) {
   if (!nw) return;
   CounterArgs A{it, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n,
-                std::min(slotCap, kWinSlots)};
-  if (check) hipLaunchKernelGGL(k_counter_win<true>, dim3(nw), dim3(512), 0, st, A);
+                std::min(slotCap, kWinSlots), hr ? *hr : HostRoute{}};
+  if (hr) hipLaunchKernelGGL(k_counter_win<true>, dim3(nw), dim3(512), 0, st, A);
   else hipLaunchKernelGGL(k_counter_win<false>, dim3(nw), dim3(512), 0, st, A);
 }
 void mk_counter_tgt(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
                     const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
                     unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st) {
   if (!nw) return;
-  CounterArgs A{it, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n, 0u};
+  CounterArgs A{it, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n, 0u, HostRoute{}};
   hipLaunchKernelGGL(k_counter_tgt, dim3(nw), dim3(256), 0, st, A);
+}
+__global__ void k_counter_adds(const uint32_t* __restrict__ slot, const unsigned long long* __restrict__ add, uint32_t m,
+                               unsigned long long* __restrict__ counter) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < m) atomicAdd(&counter[slot[i]], add[i]);
+}
+void mk_counter_adds(const uint32_t* slot, const unsigned long long* add, uint32_t m, unsigned long long* counter,
+                     hipStream_t st) {
+  if (m) hipLaunchKernelGGL(k_counter_adds, g1(m), dim3(256), 0, st, slot, add, m, counter);
+}
+__global__ void k_or_mask(uint8_t* __restrict__ mask, const uint8_t* __restrict__ other, uint32_t n) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) mask[i] |= other[i];
+}
+void mk_or_mask(uint8_t* mask, const uint8_t* other, uint32_t n, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_or_mask, g1(n), dim3(256), 0, st, mask, other, n);
 }
 void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st) {
   if (K) hipLaunchKernelGGL(k_count_distinct, dim3(std::min<unsigned>(2048, g1(K).x)), dim3(256), 0, st, v, K, out);

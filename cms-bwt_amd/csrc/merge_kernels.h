@@ -65,8 +65,10 @@ void mk_item_permute(const ItemsSoA& in, const uint32_t* order, const ItemsSoA& 
 void mk_pos_begin(const uint32_t* ipos, uint32_t K, uint32_t n, uint32_t* posBegin, hipStream_t st);
 void mk_pos_f(const uint32_t* ipos, const uint8_t* ism, const uint32_t* posBegin, uint32_t K, uint32_t n,
               uint32_t* posF, hipStream_t st);
+// positions whose items break the map-order invariant: counted into *viol and,
+// when amb is given, marked amb[pos] = 1
 void mk_check_items(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, uint32_t K,
-                    unsigned long long* viol, hipStream_t st);
+                    unsigned long long* viol, uint8_t* amb, hipStream_t st);
 void mk_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t E,
                   uint32_t* itemsSA, uint32_t* headsSA, hipStream_t st);
 void mk_dbl_keys(const uint32_t* act, const uint32_t* sa, const uint32_t* grp, uint32_t h, uint32_t U,
@@ -111,10 +113,28 @@ void mk_win_cross(const ItemsSoA& it, uint32_t K, const uint32_t* winIncl, uint3
                   hipStream_t st);
 void mk_win_cross_off(const uint32_t* keyW, uint32_t ncross, uint32_t nw, uint32_t* crossOff, hipStream_t st);
 void mk_item_sk(const ItemsSoA& it, uint32_t K, hipStream_t st);
+// Queries of the checked counter (hr != nullptr) whose target t has mask[t]
+// are not answered on the device: (source slot, t) pairs go to list (cnt
+// counts them, the first cap are stored) for the host's std::map replay; a
+// query at an unmasked target that could land differently in a std::map
+// (match.h:27-33 not a strict weak order there) sets amb[t] and counts in
+// stats[3].
+struct HostRoute {
+  const uint8_t* mask = nullptr;
+  uint8_t* amb = nullptr;
+  uint32_t* list = nullptr;
+  unsigned long long* cnt = nullptr;
+  unsigned long long cap = 0;
+};
 void mk_counter_win(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
                     const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
-                    unsigned long long* counter, unsigned long long* stats, uint32_t n, uint32_t slotCap, bool check,
-                    hipStream_t st);
+                    unsigned long long* counter, unsigned long long* stats, uint32_t n, uint32_t slotCap,
+                    const HostRoute* hr, hipStream_t st);
+// counter[slot[i]] += add[i]
+void mk_counter_adds(const uint32_t* slot, const unsigned long long* add, uint32_t m, unsigned long long* counter,
+                     hipStream_t st);
+// mask[i] |= other[i]
+void mk_or_mask(uint8_t* mask, const uint8_t* other, uint32_t n, hipStream_t st);
 // target-major counter: windows of <= 256 targets (winStart), register accumulators
 void mk_counter_tgt(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
                     const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,

@@ -26,7 +26,7 @@ extern "C" {
 #define CMSBWT_EINPUT 3     /* input on which the reference is undefined            */
 #define CMSBWT_EDEVICE 4    /* HIP runtime error or HIP code object not loadable    */
 #define CMSBWT_ELIMIT 5     /* size limit (reference int32/uint32 limits)           */
-#define CMSBWT_EORDER 6     /* map comparator ambiguity (match.h:27-33) detected    */
+#define CMSBWT_EORDER 6     /* comparator ambiguity the sharded merge cannot replay */
 #define CMSBWT_EINTERNAL 7  /* unexpected host exception (thread creation, ...)     */
 
 /* utils.h:8-14 struct Args, plus engine knobs. */
@@ -54,7 +54,8 @@ typedef struct cmsbwt_stats {
   uint64_t counter_bad, counter_good, counter_nothing;
   uint64_t runs;          /* records in .rl_bwt (or runs of .bwt)               */
   uint64_t symbols;       /* sum of run lengths                                 */
-  uint64_t order_violations; /* comparator ambiguities seen (must be 0)         */
+  uint64_t order_violations; /* comparator ambiguities (match.h:27-33) found:   */
+                             /* resolved by the host std::map replay          */
   double t_index_s, t_upload_s, t_ms_walk_s, t_merge_s, t_write_s;
   double ms_walk_kernel_ms;  /* device time of the MS-walk kernel               */
   double counter_kernel_ms;  /* device time of the counterSmallerThanHead kernel */
@@ -71,6 +72,7 @@ typedef struct cmsbwt_stats {
   double t_ranks_ms;         /* ranks .. next-head ranks, FN:1429-1498          */
   double t_libsais_int_ms;   /* head-string suffix sort, FN:1455-1461           */
   double t_counter_ms;       /* counterSmallerThanHead, FN:1517-1611            */
+  uint64_t host_queries;     /* counter queries answered by the std::map replay */
 } cmsbwt_stats;
 
 typedef struct cmsbwt_ctx cmsbwt_ctx;

@@ -183,3 +183,49 @@ def py_read_docs(coll: bytes, prefix: int = UINT64_MAX, file_size: int = None):
             sn = read
         docs.append(content)
     return docs, sn
+
+
+# Text bytes of the ambiguity cases: >= 0x80 compare below DNA as signed chars
+# (FN:55) but sort above it in the suffix array; none is '\n', '\r', '>' or 0x02.
+AMBIG_BYTES = (0x81, 0x85, 0x8A, 0x9F, 0xC3, 0x10, 0x1F, 0x7E, 0x7F)
+
+
+def ambiguity_case(seed, ref_len, n_motifs=6, n_docs=80):
+    """A collection on which match.h's comparator is not a strict weak order.
+    The reference holds unique 24-mers U_k, each followed by a byte >= 0x90,
+    and every byte of AMBIG_BYTES followed by DNA.  Documents are pieces
+    U_k[s:e] + b + DNA: at (pos U_k + s, len e - s) the singleton mismatch test
+    (FN:54-55, signed chars) makes b >= 0x80 smaller=true and 0x7E/0x7F
+    smaller=false, while isaNext (the suffix starting with b, unsigned order)
+    puts the smaller=true keys above the smaller=false ones."""
+    rng = _rng(seed)
+    motifs = [rand_dna(rng, 24) for _ in range(n_motifs)]
+    ref = bytearray(rand_dna(rng, ref_len))
+    inserts = [m + bytes([int(rng.integers(0x90, 0x100))]) + rand_dna(rng, 40) for m in motifs]
+    inserts += [bytes([b]) + rand_dna(rng, 40) for b in AMBIG_BYTES for _ in range(2)]
+    step = ref_len // (len(inserts) + 1)
+    for i, s in enumerate(inserts):
+        o = (i + 1) * step
+        ref[o:o + len(s)] = s
+    docs = []
+    for _ in range(n_docs):
+        d = b""
+        for _ in range(int(rng.integers(1, 4))):
+            m = motifs[int(rng.integers(0, n_motifs))]
+            s = int(rng.integers(0, 7))
+            e = int(rng.integers(s + 14, 25))
+            b = AMBIG_BYTES[int(rng.integers(0, len(AMBIG_BYTES)))]
+            d += m[s:e] + bytes([b]) + rand_dna(rng, int(rng.integers(0, 60)))
+        docs.append(d)
+    return fasta([bytes(ref)]), fasta(docs)
+
+
+def ambiguity_cases():
+    """Comparator-ambiguity inputs on both reference paths
+    (_n < 1e6 writes the counter side file, FN:1795)."""
+    out = []
+    for name, seed, L, nd in (("amb_small_ref", 31, 200_000, 80), ("amb_small_ref_many", 32, 300_000, 400),
+                              ("amb_large_ref", 33, 1_100_000, 200)):
+        r, c = ambiguity_case(seed, L, n_docs=nd)
+        out.append((name, r, c, UINT64_MAX))
+    return out

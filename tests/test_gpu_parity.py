@@ -71,6 +71,27 @@ def test_small_cases_plain_bwt(engine, oracle, tmp_path, case):
     _compare(engine, oracle, tmp_path, case, rle=False)
 
 
+@pytest.mark.parametrize("rle", [True, False], ids=["rl_bwt", "bwt"])
+@pytest.mark.parametrize("case", cases.ambiguity_cases(), ids=lambda c: c[0])
+def test_comparator_ambiguity_replay(engine, oracle, tmp_path, case, rle):
+    """match.h:27-33 is not a strict weak order on these inputs (bytes >= 0x80,
+    signed compare at FN:55 vs unsigned suffix order): positions with
+    ambiguous items get their std::map layout replayed on the host, and
+    queries into them or ambiguous queries are answered there (map_replay.h);
+    every stage equals the oracle, which runs the reference's std::map."""
+    st = _compare(engine, oracle, tmp_path, case, rle=rle)
+    assert st.order_violations > 0 and st.host_queries > 0
+
+
+@pytest.mark.parametrize("case", cases.small_cases()[:6], ids=lambda c: c[0])
+def test_forced_map_replay(engine, oracle, tmp_path, case):
+    """CMSBWT_FORCE_REPLAY=1 rebuilds every position's items by the std::map
+    replay and answers every counter query on the host: the replay machinery
+    itself reproduces the oracle on consistent inputs."""
+    st = _compare(engine, oracle, tmp_path, case, env={"CMSBWT_FORCE_REPLAY": "1"})
+    assert st.host_queries > 0
+
+
 @pytest.mark.parametrize("chunk", [64, 257, 1000])
 @pytest.mark.parametrize("case", cases.small_cases()[:4], ids=lambda c: c[0])
 def test_chunk_restarts(engine, oracle, tmp_path, case, chunk):

@@ -94,6 +94,26 @@ def test_sharded_multi_rank_matches_oracle(oracle, tmp_path, case, world):
     _multi(oracle, tmp_path, case, world, rle=True)
 
 
+@pytest.mark.parametrize("world", [1, 2])
+@pytest.mark.parametrize("case", cases.ambiguity_cases()[:2], ids=lambda c: c[0])
+def test_sharded_comparator_ambiguity_falls_back(engine, oracle, tmp_path, case, world):
+    """Comparator ambiguity in the sharded merge: the step is
+    redone as a gather step whose one-GPU merge replays std::map (world 1 in
+    this process, world 2 over gloo); bytes equal the oracle's."""
+    if world == 1:
+        import cmsbwt.dist as cdist
+        d, rp, cp, prefix, ost, want = _oracle_files(oracle, tmp_path, case, True)
+        engine.initialize_reference(rp)
+        engine.load_collection_file(cp, prefix)
+        cdist.sharded_step(engine, "cuda:0", rle=True, xfer=cdist.Transport("cuda:0", 1, 0))
+        assert engine.runs_bytes() == want
+        st = engine.stats()
+        assert (st.heads, st.keys, st.rank) == (ost["heads"], ost["keys"], ost["rank"])
+        assert st.order_violations > 0
+    else:
+        _multi(oracle, tmp_path, case, world, rle=True)
+
+
 def test_sharded_four_ranks_plain_bwt_repeated(oracle, tmp_path):
     case = ("copies_40k",) + cases.copies_case(7, 40000, 9, 0.004) + (cases.UINT64_MAX,)
     _multi(oracle, tmp_path, case, 4, rle=False, steps=2)

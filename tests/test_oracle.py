@@ -91,3 +91,27 @@ def test_oracle_matches_committed_small_goldens(oracle, tmp_path, name):
     for rle, ext in ((True, ".rl_bwt"), (False, ".bwt")):
         assert oracle.run(os.path.join(d, "ref.fa"), os.path.join(d, "coll.fa"), out, rle=rle, prefix=prefix)[0] == 0
         assert open(out + ext, "rb").read() == open(os.path.join(d, "expected" + ext), "rb").read()
+
+
+@pytest.mark.parametrize("case", cases.ambiguity_cases(), ids=lambda c: c[0])
+def test_ambiguity_cases_break_the_map_order(oracle, tmp_path, case):
+    """The crafted inputs of the std::map replay tests really break
+    match.h:27-33's strict weak order: some position holds a smaller=true and
+    a smaller=false head of the same length whose isaNext values are in the
+    opposite order.  (The reference's output is then not the
+    multi-string BWT: parity means the oracle's std::map layout, not the
+    brute-force BWT.)"""
+    d, rp, cp, prefix = cases.materialise(tmp_path, case)
+    dump = os.path.join(d, "dump")
+    rc, st, _ = oracle.run(rp, cp, os.path.join(d, "o"), rle=False, prefix=prefix, dump_dir=dump)
+    assert rc == 0
+    pos, ln = oracle.load_dump(dump, "h_pos").astype(np.int64), oracle.load_dump(dump, "h_len").astype(np.int64)
+    sm, isa = oracle.load_dump(dump, "h_smaller"), oracle.load_dump(dump, "h_isa").astype(np.int64)
+    key = (pos << 32) | ln
+    tmax, fmin = {}, {}
+    for k, s, i in zip(key.tolist(), sm.tolist(), isa.tolist()):
+        if s:
+            tmax[k] = max(tmax.get(k, -1), i)
+        else:
+            fmin[k] = min(fmin.get(k, 1 << 40), i)
+    assert sum(1 for k in tmax if k in fmin and fmin[k] <= tmax[k]) > 0
