@@ -69,7 +69,7 @@ def cpu_baseline(ref_len, copies, p, seed, rle=True):
             "seconds": round(t_coll, 3)}
 
 
-PMC_FILE = "r02_pmc.json"  # tools/gpu_prof_r.sh + tools/pmc_summary.py (this round's kernels)
+PMC_FILE = "r03_pmc.json"  # tools/gpu_prof_r.sh + tools/pmc_summary.py (this round's kernels)
 
 # Algorithmic bytes of the MS walk (k_ms_walk2) -- what THIS algorithm must
 # move, each byte counted once (DESIGN.md §3.1 "Roofline"):

@@ -1223,7 +1223,14 @@ struct Engine {
     runsValid = false;
     if (env_u32("CMSBWT_RUN_BIN_SHIFT", 0) || env_u32("CMSBWT_RUN_BIN_GLOBAL", 0)) ensure_runs();
     uint32_t ef = read1(errf.p);
-    orderInvariant = (ef & 8u) == 0;
+    // The comparator is provably consistent when every isaNext suffix starts
+    // with its head's mismatch byte (k_finalize) and `smaller` follows the
+    // unsigned byte order the suffix array uses: FN:55 compares signed chars,
+    // so a reference byte >= 0x80 can make a singleton mismatch's `smaller`
+    // disagree with isaNext and forces the checked merge.
+    bool highBytes = false;
+    for (int c = 0x80; c < 256; c++) highBytes |= hix.present[c];
+    orderInvariant = (ef & 8u) == 0 && !highBytes;
     if (ef & 1) throw InputError{CMSBWT_EINPUT, "internal: match ends not monotone inside a document"};
     if (ef & 6) throw InputError{CMSBWT_EINPUT, "isaNext/run index outside the reference (reference UB)"};
     walked = true;

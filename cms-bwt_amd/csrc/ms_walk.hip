@@ -107,8 +107,10 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
   h.isa[i] = R.isa[q];
   // Order invariant: the isaNext suffix starts with the mismatching text byte
   // (or the head ends at the document separator and isaNext is the smallest
-  // suffix).  When it holds for every head, MatchInSet::operator< is a strict
-  // weak order on every position's keys and queries.
+  // suffix).  When it holds for every head and the reference has no byte >=
+  // 0x80 (FN:55's signed compare then agrees with the suffix order; checked
+  // on the host), MatchInSet::operator< is a strict weak order on every
+  // position's keys and queries.
   const uint8_t* dt = text + docOff[lo];
   {
     const uint8_t c = dt[ei];

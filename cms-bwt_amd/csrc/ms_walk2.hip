@@ -275,7 +275,7 @@ constexpr uint32_t kCoopMin = 4;  // (3: 14.58 ms, 5: 15.6, 6: 16.1, 8: 17.1: pe
 #ifndef CMSBWT_W2_WAVES
 #define CMSBWT_W2_WAVES 4
 #endif
-template <bool STATS>
+template <bool STATS, bool FAST>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CMSBWT_W2_WAVES, 8)))
 k_ms_walk2(Walk2Args A) {
   __shared__ unsigned long long sc[STATS ? 32 : 1];
@@ -294,6 +294,14 @@ k_ms_walk2(Walk2Args A) {
   }
   __syncthreads();
   const DevRef& R = A.R;
+  // table configuration; FAST instances (DNA alphabet, exact carried
+  // intervals, every walk table present: the benchmark's case) fold these to
+  // constants, so the code of the other configurations is not emitted
+  const bool hasPfx = FAST || R.pfx != nullptr;
+  const bool pfxDna = FAST || R.pfxDna != 0;
+  const bool pfxExact = FAST || R.pfxExact != 0;
+  const bool hasLd = FAST || R.ld != nullptr;
+  const bool hasIr = FAST || R.ir != nullptr;
   const Lv V{lvlL, lvlL + kMaxLevels, R.nlvl, (int32_t)R.n, R.lcp};
   const uint32_t n = R.n;
   const uintptr_t X = (uintptr_t)R.x;
@@ -349,7 +357,7 @@ k_ms_walk2(Walk2Args A) {
     tw = v;
     twAt = at;
     const uint32_t K = R.kmerK, Bb = R.kmerB;
-    if (R.pfxDna) {  // alphabet ACGT: 2-bit codes of 4 bytes at a time
+    if (pfxDna) {  // alphabet ACGT: 2-bit codes of 4 bytes at a time
       const uint32_t w4[4] = {v.x, v.y, v.z, v.w};
       uint32_t full = 0, bad = 16;
 #pragma unroll
@@ -395,7 +403,7 @@ k_ms_walk2(Walk2Args A) {
     u7 = (int32_t)m;
     ad0 = (uintptr_t)(R.pfx + pfxL[m] + 2 * code);
     use = U0E;
-    if (R.pfxExact) {
+    if (pfxExact) {
       if (i + 1 - t32At <= 16u) {
         use |= UREG;
       } else {
@@ -418,12 +426,12 @@ k_ms_walk2(Walk2Args A) {
   };
   // next character(s) over a large interval: prefix-rank tables below depth K
   auto begin_search = [&]() {
-    if (R.pfx && len < R.kmerK) begin_pfx();
+    if (hasPfx && len < R.kmerK) begin_pfx();
     else begin_bs();
   };
   auto isa1 = [&]() {
     phase = PH_ISA1;
-    if (R.ir) { ad0 = (uintptr_t)(R.ir + pos + 1); use = U0Q; }
+    if (hasIr) { ad0 = (uintptr_t)(R.ir + pos + 1); use = U0Q; }
     else { ad0 = (uintptr_t)(R.isa + pos + 1); use = U0D; }
   };
   // the carried interval after a skip or a mismatch is not needed when the
@@ -440,7 +448,7 @@ k_ms_walk2(Walk2Args A) {
     i += s;
     len -= s;
     pos += s;
-    if (R.pfxExact && len < R.kmerK) {  // the window at i + 1 decides
+    if (pfxExact && len < R.kmerK) {  // the window at i + 1 decides
       phase = PH_SKTXT;
       ad0 = T + i + 1;
       use = U0Q;
@@ -453,13 +461,15 @@ k_ms_walk2(Walk2Args A) {
   // (ADJ0/ADJ) when the answer is not inside them
   auto adj_records = [&](uint32_t lo, uint32_t hi, const uint4& rl, const uint4& rh) {
     if (len - 1u < 254u) {
-      const uint64_t pw = rl.y | ((uint64_t)rl.z << 32);          // bytes 0..5
-      const uint64_t nw = (rh.z >> 16) | ((uint64_t)rh.w << 16);  // bytes 0..5
+      // bytes 0..5 of the PSV side (rl.y, rl.z) and of the NSV side (rh.z
+      // from byte 2, rh.w), compared in 32-bit registers
       int jp = -1, jn = -1;
 #pragma unroll
       for (int j = 5; j >= 0; j--) {
-        if (((pw >> (8 * j)) & 0xff) < len) jp = j;
-        if (((nw >> (8 * j)) & 0xff) < len) jn = j;
+        const uint32_t pb = (j < 4 ? rl.y >> (8 * j) : rl.z >> (8 * (j - 4))) & 0xffu;
+        const uint32_t nb = (j < 2 ? rh.z >> (16 + 8 * j) : rh.w >> (8 * (j - 2))) & 0xffu;
+        if (pb < len) jp = j;
+        if (nb < len) jn = j;
       }
       if (jp >= 0 && jn >= 0) {
         lb = (int32_t)lo - jp;
@@ -550,7 +560,7 @@ k_ms_walk2(Walk2Args A) {
           smaller = false;
           twAt = 0xffffffffu;
           t32At = 0xfffffff0u;  // (another document's bytes)
-          if (R.pfx) {
+          if (hasPfx) {
             phase = PH_PFX_TEXT;
             ad0 = T + i;
             use = U0Q;
@@ -618,7 +628,7 @@ k_ms_walk2(Walk2Args A) {
         const uint64_t TT = (uint64_t)pos + 1 + len;
         ad0 = P + 4ull * (TT >= 16 ? TT - 16 : 0);
         use = U0Q | U1Q | U4Q | U5Q;
-        if (R.pfxExact && R.pfx) {  // and the 32 text bytes around the match end: the next window
+        if (pfxExact && hasPfx) {  // and the 32 text bytes around the match end: the next window
           ad2 = T + skip_text_base();
           use |= U2Q | U3Q;
         }
@@ -649,9 +659,9 @@ k_ms_walk2(Walk2Args A) {
         phase = PH_LCE_SA;
         ad0 = SA + 4ull * (uint32_t)lb;
         use = U0D;
-      } else if (R.pfxExact && len < R.kmerK) {  // (the only way on an unknown interval)
+      } else if (pfxExact && len < R.kmerK) {  // (the only way on an unknown interval)
         begin_pfx();
-      } else if (R.ld && rb - lb < 16 && len < 0xffffu) {
+      } else if (hasLd && rb - lb < 16 && len < 0xffffu) {
         phase = PH_EXT1;
         ad0 = (uintptr_t)(R.ld + lb);
         ad2 = T + i + len;
@@ -689,25 +699,31 @@ k_ms_walk2(Walk2Args A) {
     uint32_t skS = 0xffffffffu;
     if (phase == PH_SKIP1) {
       // entries Wb..Wb+15 below TT; PLCP[q] + q is non-decreasing, so the
-      // window decides when it starts at or below pos+1 or below the exit
-      const int64_t TT = (int64_t)pos + 1 + len, q0 = (int64_t)pos + 1;
-      const int64_t Wb = TT >= 16 ? TT - 16 : 0;
+      // window decides when it starts at or below pos+1 or below the exit.
+      // 32-bit arithmetic: positions and PLCP values are below n < 2^31, so
+      // no sum wraps (a negative tail entry wraps to a value below TT, as the
+      // signed sum would be)
+      // Entry k (q = Wb + k < TT) crosses when e[k] + k >= D = TT - Wb; the
+      // crossings are a suffix of the window (monotone), so the first one is
+      // the number c of entries that do not cross: one add, compare and
+      // carry-add per entry.  The exit is the first crossing at or above
+      // pos+1 (kmin = q0 - Wb when the window starts below it).
+      const uint32_t TT = pos + 1 + len, q0 = pos + 1;
+      const uint32_t Wb = TT >= 16 ? TT - 16 : 0, D = TT - Wb;
       const uint32_t e[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
                               v4.x, v4.y, v4.z, v4.w, v5.x, v5.y, v5.z, v5.w};
-      if (Wb <= q0 || (int64_t)(int32_t)e[0] + Wb < TT) {
-        int64_t qc = TT;  // first crossing (TT itself always crosses)
+      uint32_t c = 0;
 #pragma unroll
-        for (int k = 15; k >= 0; k--) {
-          const int64_t q = Wb + k;
-          if (q >= q0 && q < TT && (int64_t)(int32_t)e[k] + q >= TT) qc = q;
-        }
-        skS = (uint32_t)(qc - q0);
+      for (uint32_t k = 0; k < 16; k++) c += e[k] + k < D ? 1u : 0u;
+      if (Wb <= q0 || c > 0) {
+        const uint32_t kmin = Wb <= q0 ? q0 - Wb : 0u;
+        skS = Wb + (c > kmin ? c : kmin) - q0;
       }
     }
     // the text window this step loaded (one call site: the code is emitted once)
     {
       const bool wa = phase == PH_PFX_TEXT || phase == PH_SKTXT;
-      const bool sk = phase == PH_SKIP1 && R.pfxExact && R.pfx;  // the skip loaded 32 text bytes
+      const bool sk = phase == PH_SKIP1 && pfxExact && hasPfx;  // the skip loaded 32 text bytes
       const bool ws = sk && skS != 0xffffffffu && len - skS < R.kmerK;
       const bool wr = (use & UREG) != 0;
       if (sk) {
@@ -715,7 +731,7 @@ k_ms_walk2(Walk2Args A) {
         t32b = v3;
         t32At = skip_text_base();
       }
-      if (wa || ws || (phase == PH_PFX_PROBE && R.pfxExact)) {
+      if (wa || ws || (phase == PH_PFX_PROBE && pfxExact)) {
         uint4 vv = make_uint4(wa ? v0.x : v2.x, wa ? v0.y : v2.y, wa ? v0.z : v2.z, wa ? v0.w : v2.w);
         uint32_t at = phase == PH_PFX_TEXT ? i : i + 1;
         if (ws || wr) {  // bytes o..o+15 of the 32 skip bytes, o = next position - their base
@@ -823,10 +839,10 @@ k_ms_walk2(Walk2Args A) {
         break;
       }
       case PH_SKIP1: {
-        const int64_t TT = (int64_t)pos + 1 + len, q0 = (int64_t)pos + 1;
-        const int64_t Wb = TT >= 16 ? TT - 16 : 0;
+        const uint32_t TT = pos + 1 + len, q0 = pos + 1;
+        const uint32_t Wb = TT >= 16 ? TT - 16 : 0;
         if (skS != 0xffffffffu) {  // exit inside the window (scanned above)
-          if (R.pfxExact && R.pfx && len - skS < R.kmerK) {  // the window of the next position is decoded
+          if (pfxExact && hasPfx && len - skS < R.kmerK) {  // the window of the next position is decoded
             i += skS;
             len -= skS;
             pos += skS;
@@ -874,7 +890,7 @@ k_ms_walk2(Walk2Args A) {
         break;
       }
       case PH_ISA1: {
-        if (R.ir) adj_records(v0.x, v0.x, v0, v0);
+        if (hasIr) adj_records(v0.x, v0.x, v0, v0);
         else { u0 = u5 = (int32_t)v0.x; phase = PC_ADJ0; use = 0; }
         break;
       }
@@ -967,7 +983,7 @@ k_ms_walk2(Walk2Args A) {
       }
       case PH_PFX_PROBE: {  // (wm/wcode already describe the window at i + 1)
         const uint32_t m = (uint32_t)u7, code = (uint32_t)u6, Bb = R.kmerB;
-        if (!R.pfxExact && len > 0 && (v2.x != (uint32_t)lb || v2.y != (uint32_t)(rb - lb) + 1)) {
+        if (!pfxExact && len > 0 && (v2.x != (uint32_t)lb || v2.y != (uint32_t)(rb - lb) + 1)) {
           begin_bs();
           break;
         }
@@ -999,7 +1015,7 @@ k_ms_walk2(Walk2Args A) {
         phase = PC_POST;
         if (v0.y & kPfxSingle) {
           lb = rb = 0;  // a one-suffix interval: the skip of FN:1175-1189 follows
-        } else if (R.pfxExact && wm == R.kmerK) {
+        } else if (pfxExact && wm == R.kmerK) {
           lb = -1;  // the next position resolves by its own probe
           rb = -2;
         } else if (len == 0) {
@@ -1130,8 +1146,14 @@ void launch_ms_walk2(const DevRef& R, const uint8_t* text, const uint64_t* docOf
   if (!nchunks) return;
   Walk2Args A{R, text, docOff, chunks, nchunks, order, bandStart, nbands, nextChunk, pool, chunkCount, stats};
   const uint32_t blocks = (std::min<uint32_t>(lanes, nchunks) + 255) / 256;
-  if (stats) hipLaunchKernelGGL(k_ms_walk2<true>, dim3(blocks), dim3(256), 0, st, A);
-  else hipLaunchKernelGGL(k_ms_walk2<false>, dim3(blocks), dim3(256), 0, st, A);
+  const bool fast = R.pfx && R.pfxDna && R.pfxExact && R.ld && R.ir;
+  if (stats) {
+    if (fast) hipLaunchKernelGGL((k_ms_walk2<true, true>), dim3(blocks), dim3(256), 0, st, A);
+    else hipLaunchKernelGGL((k_ms_walk2<true, false>), dim3(blocks), dim3(256), 0, st, A);
+  } else {
+    if (fast) hipLaunchKernelGGL((k_ms_walk2<false, true>), dim3(blocks), dim3(256), 0, st, A);
+    else hipLaunchKernelGGL((k_ms_walk2<false, false>), dim3(blocks), dim3(256), 0, st, A);
+  }
 }
 
 }  // namespace cmsbwt

@@ -89,7 +89,8 @@ def test_forced_map_replay(engine, oracle, tmp_path, case):
     replay and answers every counter query on the host: the replay machinery
     itself reproduces the oracle on consistent inputs."""
     st = _compare(engine, oracle, tmp_path, case, env={"CMSBWT_FORCE_REPLAY": "1"})
-    assert st.host_queries > 0
+    # every query into a position with heads went to the host
+    assert st.host_queries >= st.counter_bad + st.counter_good
 
 
 @pytest.mark.parametrize("chunk", [64, 257, 1000])
