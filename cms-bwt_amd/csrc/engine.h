@@ -78,6 +78,15 @@ struct AdjustedRuns {  // k_wr_adjust's rule, as a scan input
     return (unsigned long long)r - (((a >> 16) && (pv >> 16) && (a & 0xff) == ((pv >> 8) & 0xff)) ? 1u : 0u);
   }
 };
+// (adjusted runs << kPackSymBits) | symbols of a writer element: both
+// exclusive scans of the writer in one pass
+struct PackedRunsSym {
+  AdjustedRuns runs;
+  const unsigned long long* sym;
+  __host__ __device__ unsigned long long operator()(uint32_t u) const {
+    return (runs(u) << kPackSymBits) | sym[u];
+  }
+};
 struct PlusOneU64 {
   __host__ __device__ unsigned long long operator()(unsigned long long v) const { return v + 1; }
 };
@@ -1940,14 +1949,37 @@ struct Engine {
       exscan(whl.p, wprev.p, 0u, V, LastNonEmpty());
       // runs of each element, less one when its first segment continues the
       // previous non-empty element's run (k_wr_adjust, fused into the scan)
-      auto runs64 = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint32_t>(0u),
-                                                     AdjustedRuns{wruns.p, whl.p, wprev.p});
-      exscan(runs64, wrunOff.p, 0ull, V);
-      exscan(wsym.p, wsymOff.p, 0ull, V);
-      Rn = read1(wrunOff.p + (V - 1)) + AdjustedRuns{wruns.p, whl.p, wprev.p}.host(V - 1, this);
-      symbols = read1(wsymOff.p + (V - 1)) + read1(wsym.p + (V - 1));
+      // one packed scan when the totals fit (at most 3 runs per element; the
+      // symbol total, which the remainder quirk of FN:1761-1770 can lift above
+      // the collection length, from one reduce), else two
+      const AdjustedRuns adj{wruns.p, whl.p, wprev.p};
+      uint64_t symTotal = 0;
+      {
+        DBuf<unsigned long long> tot;
+        tot.alloc(1);
+        size_t b = 0;
+        HIPCHK(rocprim::reduce(nullptr, b, wsym.p, tot.p, 0ull, (size_t)V, rocprim::plus<unsigned long long>(), st));
+        HIPCHK(rocprim::reduce(scratch(b), b, wsym.p, tot.p, 0ull, (size_t)V, rocprim::plus<unsigned long long>(), st));
+        symTotal = read1(tot.p);
+      }
+      const bool packed = symTotal < (1ull << kPackSymBits) && 3ull * V < (1ull << (64 - kPackSymBits)) &&
+                          !env_u32("CMSBWT_WR_TWO_SCANS", 0);
+      if (packed) {
+        auto rs = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint32_t>(0u),
+                                                   PackedRunsSym{adj, wsym.p});
+        exscan(rs, wrunOff.p, 0ull, V);
+        const unsigned long long last = read1(wrunOff.p + (V - 1));
+        Rn = (last >> kPackSymBits) + adj.host(V - 1, this);
+        symbols = (last & ((1ull << kPackSymBits) - 1)) + read1(wsym.p + (V - 1));
+      } else {
+        auto runs64 = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint32_t>(0u), adj);
+        exscan(runs64, wrunOff.p, 0ull, V);
+        exscan(wsym.p, wsymOff.p, 0ull, V);
+        Rn = read1(wrunOff.p + (V - 1)) + adj.host(V - 1, this);
+        symbols = read1(wsymOff.p + (V - 1)) + read1(wsym.p + (V - 1));
+      }
       runStart.alloc(std::max<uint64_t>(Rn, 1)); runChar.alloc(std::max<uint64_t>(Rn, 1));
-      mk_el_wr_emit(ei, V, wrunOff.p, wsymOff.p, wprev.p, runStart.p, runChar.p, st);
+      mk_el_wr_emit(ei, V, wrunOff.p, packed ? nullptr : wsymOff.p, wprev.p, runStart.p, runChar.p, st);
       itemOfSlot.release();
     }
     runs.alloc(Rn * 9);

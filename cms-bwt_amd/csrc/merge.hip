@@ -1565,7 +1565,16 @@ __global__ void k_el_wr_emit(ElemArgs A, uint32_t V, const unsigned long long* _
   if (e >= V) return;
   const uint32_t pv = prevHL[e];
   int prev = (pv >> 16) ? (int)((pv >> 8) & 0xff) : -1;
-  unsigned long long j = runOff[e], pos = symOff[e];
+  // symOff == nullptr: one packed scan, run offset << kPackSymBits | symbol offset
+  unsigned long long j, pos;
+  if (symOff) {
+    j = runOff[e];
+    pos = symOff[e];
+  } else {
+    const unsigned long long v = runOff[e];
+    j = v >> kPackSymBits;
+    pos = v & ((1ull << kPackSymBits) - 1);
+  }
   d_elem_segments(A, e, [&](uint8_t c, unsigned long long cnt) {
     if ((int)c != prev) {
       runStart[j] = pos;

@@ -171,6 +171,9 @@ void mk_el_count(const uint32_t* headBase, uint32_t n, uint32_t E, uint32_t H, u
 void mk_el_rof(const uint32_t* elemBase, const uint32_t* m, uint32_t n, uint32_t* rOf, hipStream_t st);
 void mk_el_wr_count(const ElemIn& w, uint32_t V, uint32_t* runs, unsigned long long* sym, uint32_t* hl,
                     hipStream_t st);
+// run and symbol offsets packed into one 64-bit scan (symbol totals < 2^34,
+// run totals < 2^30): k_el_wr_emit takes the packed offsets with symOff == nullptr
+constexpr uint32_t kPackSymBits = 34;
 void mk_el_wr_emit(const ElemIn& w, uint32_t V, const unsigned long long* runOff, const unsigned long long* symOff,
                    const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st);
 // element writer of the position-sharded merge (elements of the owned SA

@@ -72,6 +72,14 @@ def test_small_cases_plain_bwt(engine, oracle, tmp_path, case):
 
 
 @pytest.mark.parametrize("rle", [True, False], ids=["rl_bwt", "bwt"])
+@pytest.mark.parametrize("case", cases.small_cases()[:5], ids=lambda c: c[0])
+def test_writer_two_scans(engine, oracle, tmp_path, case, rle):
+    """Writer offsets (FN:1631-1777) by two 64-bit scans, the path taken
+    when run and symbol totals do not fit one packed scan."""
+    _compare(engine, oracle, tmp_path, case, rle=rle, env={"CMSBWT_WR_TWO_SCANS": "1"})
+
+
+@pytest.mark.parametrize("rle", [True, False], ids=["rl_bwt", "bwt"])
 @pytest.mark.parametrize("case", cases.ambiguity_cases(), ids=lambda c: c[0])
 def test_comparator_ambiguity_replay(engine, oracle, tmp_path, case, rle):
     """match.h:27-33 is not a strict weak order on these inputs (bytes >= 0x80,
