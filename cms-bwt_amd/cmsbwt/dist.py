@@ -251,7 +251,7 @@ def sharded_merge(eng, x: Transport, rle: bool = True):
         U = eng.dm_dbl_apply(back.data_ptr())
         h *= 2
     # 4. head ranks / next-head ranks to the position owners
-    ranks = x.empty((H, 2), i32)
+    ranks = x.empty((H, 3), i32)  # head rank, next-head rank, BWT character
     eng.dm_pack_ranks(ranks.data_ptr())
     rr = x.a2a(ranks, hc, rc)
     eng.dm_load_ranks(rr.data_ptr())

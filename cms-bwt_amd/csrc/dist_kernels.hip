@@ -247,9 +247,12 @@ __global__ void k_dm_dbl_apply(const uint32_t* __restrict__ aPerm, const uint32_
 }
 
 // head rank and next-head rank (FN:1468-1494) of every head, heads send order
+// doc side: (head rank, next-head rank, BWT character) per head in send
+// order; the character travels here so that the position side places it with
+// the ranks it reads anyway (one gather per slot, not two)
 __global__ void k_dm_pack_ranks(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ grp,
-                                const uint16_t* __restrict__ nexthead, uint64_t n, uint32_t H,
-                                int32_t* __restrict__ out, uint32_t* __restrict__ err) {
+                                const uint16_t* __restrict__ nexthead, const uint8_t* __restrict__ lchar,
+                                uint64_t n, uint32_t H, int32_t* __restrict__ out, uint32_t* __restrict__ err) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const uint32_t i = perm[j];
@@ -257,8 +260,9 @@ __global__ void k_dm_pack_ranks(const uint32_t* __restrict__ perm, const uint32_
   uint32_t nv = 0;
   if (nx < H) nv = grp[nx] - 1;
   else atomicOr(err, 2u);
-  out[2 * j] = (int32_t)(grp[i] - 1);
-  out[2 * j + 1] = (int32_t)nv;
+  out[3 * j] = (int32_t)(grp[i] - 1);
+  out[3 * j + 1] = (int32_t)nv;
+  out[3 * j + 2] = (int32_t)lchar[i];
 }
 
 // position side: the head characters by slot (the member with head rank hr
@@ -268,16 +272,16 @@ __global__ void k_dm_pack_ranks(const uint32_t* __restrict__ perm, const uint32_
 // rank pair per slot
 __global__ void k_dm_load_ranks(const int32_t* __restrict__ in, const uint32_t* __restrict__ Pm,
                                 const uint32_t* __restrict__ itemOfSlot, const ItemsSoA it,
-                                const uint32_t* __restrict__ gItem, const uint8_t* __restrict__ lchar, uint32_t H,
-                                uint32_t* __restrict__ nbiS, uint8_t* __restrict__ bwtSlot,
-                                uint32_t* __restrict__ err) {
+                                const uint32_t* __restrict__ gItem, uint32_t H, uint32_t* __restrict__ nbiS,
+                                uint8_t* __restrict__ bwtSlot, uint32_t* __restrict__ err) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= H) return;
   const uint32_t r = Pm[s], q = itemOfSlot[s];
-  const uint2 w = *(const uint2*)(in + 2ull * r);
-  nbiS[s] = w.y;
-  const uint32_t k = w.x - (gItem[q] - 1);
-  if (k < it.count[q]) bwtSlot[it.slot[q] + k] = lchar[r];
+  const int32_t* w = in + 3ull * r;  // (rank, next-head rank, character), one 12-B record
+  const uint32_t hr = (uint32_t)w[0], nb = (uint32_t)w[1], ch = (uint32_t)w[2];
+  nbiS[s] = nb;
+  const uint32_t k = hr - (gItem[q] - 1);
+  if (k < it.count[q]) bwtSlot[it.slot[q] + k] = (uint8_t)ch;
   else atomicOr(err, 4u);
 }
 
@@ -454,16 +458,14 @@ void mk_dm_dbl_apply(const uint32_t* aPerm, const uint32_t* act, const unsigned 
                      uint32_t* keep, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_dm_dbl_apply, g1d(n), dim3(256), 0, st, aPerm, act, back, n, grp, keep);
 }
-void mk_dm_pack_ranks(const uint32_t* perm, const uint32_t* grp, const uint16_t* nexthead, uint64_t n, uint32_t H,
-                      int32_t* out, uint32_t* err, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_dm_pack_ranks, g1d(n), dim3(256), 0, st, perm, grp, nexthead, n, H, out, err);
+void mk_dm_pack_ranks(const uint32_t* perm, const uint32_t* grp, const uint16_t* nexthead, const uint8_t* lchar,
+                      uint64_t n, uint32_t H, int32_t* out, uint32_t* err, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_dm_pack_ranks, g1d(n), dim3(256), 0, st, perm, grp, nexthead, lchar, n, H, out, err);
 }
 void mk_dm_load_ranks(const int32_t* in, const uint32_t* Pm, const uint32_t* itemOfSlot, const ItemsSoA& it,
-                      const uint32_t* gItem, const uint8_t* lchar, uint32_t H, uint32_t* nbi, uint8_t* bwtSlot,
-                      uint32_t* err, hipStream_t st) {
+                      const uint32_t* gItem, uint32_t H, uint32_t* nbi, uint8_t* bwtSlot, uint32_t* err, hipStream_t st) {
   if (!H) return;
-  hipLaunchKernelGGL(k_dm_load_ranks, g1d(H), dim3(256), 0, st, in, Pm, itemOfSlot, it, gItem, lchar, H, nbi, bwtSlot,
-                     err);
+  hipLaunchKernelGGL(k_dm_load_ranks, g1d(H), dim3(256), 0, st, in, Pm, itemOfSlot, it, gItem, H, nbi, bwtSlot, err);
 }
 void mk_dm_halo_count(const ItemsSoA& it, uint32_t K, const uint32_t* split, uint32_t world, uint32_t rank,
                       uint32_t n, uint32_t* c, hipStream_t st) {

@@ -261,7 +261,7 @@ uint64_t Engine::dm_dbl_apply(const unsigned long long* back) {
 
 // ---- 4. head ranks and next-head ranks to the position owners
 void Engine::dm_pack_ranks(int32_t* out) {
-  mk_dm_pack_ranks(dm.hPerm.p, dm.grp.p, hNext.p, H, H, out, dm.err.p, st);
+  mk_dm_pack_ranks(dm.hPerm.p, dm.grp.p, hNext.p, hChar.p, H, H, out, dm.err.p, st);
   HIPCHK(hipGetLastError());
   sync();
   dm_check_err("next-head ranks");
@@ -277,7 +277,7 @@ void Engine::dm_load_ranks(const int32_t* recv) {
     // inside small items through Pm, large items by one sort)
     DBuf<uint32_t> nbi;
     nbi.alloc(std::max<uint32_t>(Hp, 1));
-    mk_dm_load_ranks(recv, dm.Pm.p, dm.itemOfSlot.p, S, dm.gItem.p, dm.rCh.p, Hp, nbi.p, dm.bwtSlot.p, dm.err.p, st);
+    mk_dm_load_ranks(recv, dm.Pm.p, dm.itemOfSlot.p, S, dm.gItem.p, Hp, nbi.p, dm.bwtSlot.p, dm.err.p, st);
     if (Hp) {
       mk_nhr_rank(nullptr, nbi.p, dm.itemOfSlot.p, Hp, dm.nhr.p, st);  // nbi in slot order
       sort_nhr_items(S, dm.IS.K, dm.itemOfSlot.p, dm.nhr.p, Hp, true);
@@ -332,6 +332,23 @@ void Engine::dm_counter(const int32_t* hdr, uint64_t nh, const int32_t* words, u
   const uint32_t n = R.n, K = dm.IS.K, Hp = dm.Hp;
   if (nh + K >= 0xffffffffull || nw + Hp >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "halo too large"};
   const uint32_t Kh = (uint32_t)nh, Kc = Kh + K, Hc = (uint32_t)nw + Hp;
+  const ItemsSoA S = dm.IS.soa();
+  if (Kh == 0 && nw == 0) {  // no halo (rank 0, or one rank): the own items as they are
+    DBuf<unsigned long long> cst;
+    cst.alloc(8);
+    cst.zero(st);
+    dm.counter.alloc((uint64_t)Hp + 1);
+    dm.counter.zero(st);
+    counter_phase(S, K, dm.IS.posBegin.p, dm.IS.posF.p, dm.nhr.p, dm.counter.p, cst.p, n, dm.P0, dm.P1, dm.check);
+    unsigned long long cs[8];
+    HIPCHK(hipMemcpyAsync(cs, cst.p, sizeof(cs), hipMemcpyDeviceToHost, st));
+    sync();
+    for (int k = 0; k < 5; k++) out6[k] = cs[k];
+    out6[3] += dm.viol;
+    out6[5] = K;
+    stats.counter_kernel_ms = counter_kernel_ms;
+    return;
+  }
   // combined items: halo (positions before P0, ascending) then the own items
   DBuf<uint32_t> cPos, cLen, cIsa, cUntil, cCount, cSlot, cNhr, pb, pf;
   DBuf<uint8_t> cSmall;
@@ -340,7 +357,6 @@ void Engine::dm_counter(const int32_t* hdr, uint64_t nh, const int32_t* words, u
   cSk.alloc(Kc); cSlot.alloc((uint64_t)Kc + 1); cNhr.alloc(std::max<uint32_t>(Hc, 1));
   ItemsSoA C{cPos.p, cLen.p, cIsa.p, cSmall.p, cUntil.p, cCount.p, nullptr, cSlot.p, nullptr, cSk.p};
   mk_dm_halo_unpack(hdr, Kh, C, st);
-  const ItemsSoA S = dm.IS.soa();
   auto cp = [&](void* d, const void* s, uint64_t b) {
     if (b) HIPCHK(hipMemcpyAsync(d, s, b, hipMemcpyDeviceToDevice, st));
   };
@@ -419,14 +435,34 @@ void Engine::dm_units(int64_t* out) {
   runs.alloc(std::max<uint32_t>(V, 1)); adj.alloc(std::max<uint32_t>(V, 1)); sym.alloc(std::max<uint32_t>(V, 1));
   dm.ehl.alloc(std::max<uint32_t>(V, 1));
   dm.runIn.alloc(std::max<uint32_t>(V, 1));
-  dm.symIn.alloc(std::max<uint32_t>(V, 1));
+  dm.symPacked = false;
   if (V) {
     mk_el_wr_count(ei, V, runs.p, sym.p, dm.ehl.p, st);
     mk_dm_el_adj(dm.rOf.p, dm.ehl.p, runs.p, V, adj.p, st);
-    inscan(rocprim::make_transform_iterator(adj.p, WidenU64()), dm.runIn.p, V, rocprim::plus<unsigned long long>());
-    inscan(sym.p, dm.symIn.p, V, rocprim::plus<unsigned long long>());
+    // runs and symbols in one packed inclusive scan when the totals fit (as
+    // the one-GPU writer), else two
+    uint64_t symTotal = 0;
+    {
+      DBuf<unsigned long long> tot;
+      tot.alloc(1);
+      size_t b = 0;
+      HIPCHK(rocprim::reduce(nullptr, b, sym.p, tot.p, 0ull, (size_t)V, rocprim::plus<unsigned long long>(), st));
+      HIPCHK(rocprim::reduce(scratch(b), b, sym.p, tot.p, 0ull, (size_t)V, rocprim::plus<unsigned long long>(), st));
+      symTotal = read1(tot.p);
+    }
+    dm.symPacked = symTotal < (1ull << kPackSymBits) && 3ull * V < (1ull << (64 - kPackSymBits)) &&
+                   !env_u32("CMSBWT_WR_TWO_SCANS", 0);
+    if (dm.symPacked) {
+      inscan(rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint32_t>(0u),
+                                              PackAdjSym{adj.p, sym.p}),
+             dm.runIn.p, V, rocprim::plus<unsigned long long>());
+    } else {
+      dm.symIn.alloc(V);
+      inscan(rocprim::make_transform_iterator(adj.p, WidenU64()), dm.runIn.p, V, rocprim::plus<unsigned long long>());
+      inscan(sym.p, dm.symIn.p, V, rocprim::plus<unsigned long long>());
+    }
   }
-  mk_dm_el_units(dm.eBase.p, m.p, dm.runIn.p, dm.symIn.p, dm.ehl.p, n, dm.E, Uw, out, st);
+  mk_dm_el_units(dm.eBase.p, m.p, dm.runIn.p, dm.symPacked ? nullptr : dm.symIn.p, dm.ehl.p, n, dm.E, Uw, out, st);
   HIPCHK(hipGetLastError());
   sync();
 }
@@ -459,7 +495,7 @@ uint64_t Engine::dm_emit(const int64_t* unitsAll) {
     // rank 0 holds the output: its own runs go straight to their global indices
     dm.gStart.alloc(std::max<uint64_t>(dm.Rn, 1));
     dm.gChar.alloc(std::max<uint64_t>(dm.Rn, 1));
-    mk_dm_el_emit(ei, dm.V, dm.runIn.p, dm.symIn.p, dm.runOff.p, dm.symOff.p, dm.uprev.p, dm.uhl.p, dm.ehl.p,
+    mk_dm_el_emit(ei, dm.V, dm.runIn.p, dm.symPacked ? nullptr : dm.symIn.p, dm.runOff.p, dm.symOff.p, dm.uprev.p, dm.uhl.p, dm.ehl.p,
                   dm.gStart.p, dm.gChar.p, st);
     dm.Rloc = 0;
   } else {
@@ -471,7 +507,7 @@ uint64_t Engine::dm_emit(const int64_t* unitsAll) {
     dm.Rloc = read1(srcOff.p + (Uw - 1)) + read1(own.p + (Uw - 1));
     dm.locStart.alloc(std::max<uint64_t>(dm.Rloc, 1));
     dm.locChar.alloc(std::max<uint64_t>(dm.Rloc, 1));
-    mk_dm_el_emit(ei, dm.V, dm.runIn.p, dm.symIn.p, srcOff.p, dm.symOff.p, dm.uprev.p, dm.uhl.p, dm.ehl.p,
+    mk_dm_el_emit(ei, dm.V, dm.runIn.p, dm.symPacked ? nullptr : dm.symIn.p, srcOff.p, dm.symOff.p, dm.uprev.p, dm.uhl.p, dm.ehl.p,
                   dm.locStart.p, dm.locChar.p, st);
   }
   HIPCHK(hipGetLastError());

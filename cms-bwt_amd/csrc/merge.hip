@@ -1650,6 +1650,16 @@ __global__ void k_dm_el_adj(const uint32_t* __restrict__ rOf, const uint32_t* __
 // the end phrases (one element each), unit E + r - 1 the elements of SA rank
 // r; zero for units of other ranks.  runIn / symIn: inclusive scans over the
 // elements of adj and sym.
+// inclusive run / symbol scans of the elements: two arrays, or one packed
+// array (runs << kPackSymBits | symbols) when sym == nullptr
+struct ElemScan {
+  const unsigned long long* run;
+  const unsigned long long* sym;
+  __device__ unsigned long long r(uint32_t i) const { return sym ? run[i] : run[i] >> kPackSymBits; }
+  __device__ unsigned long long s(uint32_t i) const {
+    return sym ? sym[i] : run[i] & ((1ull << kPackSymBits) - 1);
+  }
+};
 __global__ void k_dm_el_units(const uint32_t* __restrict__ elemBase, const uint32_t* __restrict__ m,
                               const unsigned long long* __restrict__ runIn, const unsigned long long* __restrict__ symIn,
                               const uint32_t* __restrict__ hl, uint32_t n, uint32_t E, uint32_t U,
@@ -1667,9 +1677,10 @@ __global__ void k_dm_el_units(const uint32_t* __restrict__ elemBase, const uint3
     e0 = elemBase[r];
     e1 = e0 + m[r];
   }
-  const unsigned long long rb = e0 ? runIn[e0 - 1] : 0ull, sb = e0 ? symIn[e0 - 1] : 0ull;
-  const uint32_t nr = (uint32_t)(runIn[e1 - 1] - rb);
-  const unsigned long long ns = symIn[e1 - 1] - sb;
+  const ElemScan es{runIn, symIn};
+  const unsigned long long rb = e0 ? es.r(e0 - 1) : 0ull, sb = e0 ? es.s(e0 - 1) : 0ull;
+  const uint32_t nr = (uint32_t)(es.r(e1 - 1) - rb);
+  const unsigned long long ns = es.s(e1 - 1) - sb;
   const uint32_t hf = hl[e0], hlast = hl[e1 - 1];
   const uint32_t h = (hf >> 16) ? ((1u << 16) | (hlast & 0xff00u) | (hf & 0xffu)) : 0u;
   out[u] = (int64_t)(((uint64_t)h << 32) | nr);
@@ -1693,6 +1704,7 @@ __global__ void k_dm_el_emit(ElemArgs A, uint32_t V, const uint32_t* __restrict_
   const uint32_t u = r ? A.E + r - 1 : e - elemBase[0];
   const uint32_t e0 = r ? elemBase[r] : e;
   const uint32_t pu = prevHL[u], hu = unitHL[u];
+  const ElemScan es{runIn, symIn};
   int prev;
   unsigned long long j = unitRunOff[u];
   if (e == e0) {
@@ -1700,9 +1712,9 @@ __global__ void k_dm_el_emit(ElemArgs A, uint32_t V, const uint32_t* __restrict_
   } else {
     prev = (int)((hl[e - 1] >> 8) & 0xff);
     const bool joined = (hu >> 16) && (pu >> 16) && (hu & 0xff) == ((pu >> 8) & 0xff);
-    j += runIn[e - 1] - (e0 ? runIn[e0 - 1] : 0ull) - (joined ? 1u : 0u);
+    j += es.r(e - 1) - (e0 ? es.r(e0 - 1) : 0ull) - (joined ? 1u : 0u);
   }
-  unsigned long long pos = unitSymOff[u] + (e ? symIn[e - 1] : 0ull) - (e0 ? symIn[e0 - 1] : 0ull);
+  unsigned long long pos = unitSymOff[u] + (e ? es.s(e - 1) : 0ull) - (e0 ? es.s(e0 - 1) : 0ull);
   d_elem_segments(A, e, [&](uint8_t c, unsigned long long cnt) {
     if ((int)c != prev) {
       runStart[j] = pos;

@@ -219,12 +219,13 @@ void mk_dm_dbl_result(const unsigned long long* key, const uint32_t* val, const 
                       const uint32_t* ksMax, uint64_t n, unsigned long long* res, hipStream_t st);
 void mk_dm_dbl_apply(const uint32_t* aPerm, const uint32_t* act, const unsigned long long* back, uint64_t n, uint32_t* grp,
                      uint32_t* keep, hipStream_t st);
-void mk_dm_pack_ranks(const uint32_t* perm, const uint32_t* grp, const uint16_t* nexthead, uint64_t n, uint32_t H,
-                      int32_t* out, uint32_t* err, hipStream_t st);
+// (head rank, next-head rank, BWT character): 3 words per head in send order
+void mk_dm_pack_ranks(const uint32_t* perm, const uint32_t* grp, const uint16_t* nexthead, const uint8_t* lchar,
+                      uint64_t n, uint32_t H, int32_t* out, uint32_t* err, hipStream_t st);
 // head characters by slot (bwtSlot) and the next-head ranks in slot order (nbiS)
 void mk_dm_load_ranks(const int32_t* in, const uint32_t* Pm, const uint32_t* itemOfSlot, const ItemsSoA& it,
-                      const uint32_t* gItem, const uint8_t* lchar, uint32_t H, uint32_t* nbiS, uint8_t* bwtSlot,
-                      uint32_t* err, hipStream_t st);
+                      const uint32_t* gItem, uint32_t H, uint32_t* nbiS, uint8_t* bwtSlot, uint32_t* err,
+                      hipStream_t st);
 void mk_dm_halo_count(const ItemsSoA& it, uint32_t K, const uint32_t* split, uint32_t world, uint32_t rank,
                       uint32_t n, uint32_t* c, hipStream_t st);
 void mk_dm_halo_fill(const uint32_t* c, const uint32_t* off, uint32_t K, uint32_t rank, uint32_t* dest,

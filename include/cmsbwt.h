@@ -160,7 +160,8 @@ int cmsbwt_walk_import(cmsbwt_ctx* ctx, uint64_t heads, uint64_t ndocs, uint64_t
  *     dm_dbl_pack -> 2 words/element; all-to-all; dm_dbl_sort -> result
  *     (label | unresolved << 32);
  *     reverse all-to-all -> dm_dbl_apply; h *= 2
- *   dm_pack_ranks -> 2 words/head; all-to-all (head counts) -> dm_load_ranks
+ *   dm_pack_ranks -> 3 words/head (rank, next-head rank, BWT character);
+ *     all-to-all (head counts) -> dm_load_ranks
  *   dm_route_halo -> counts; dm_pack_halo -> 6 words/item + nhr words;
  *     all-to-all -> dm_counter -> {bad, good, nothing, violations, errors, items}
  *   dm_units -> int64[2*(E+n-1)]; all-reduce(sum) -> dm_emit -> nlocal

@@ -44,7 +44,7 @@ def test_sharded_world1_matches_oracle(engine, oracle, tmp_path, case, rle):
     assert (st.counter_bad, st.counter_good, st.counter_nothing) == (ost["bad"], ost["good"], ost["nothing"])
 
 
-@pytest.mark.parametrize("env", ["CMSBWT_GROUP3", "CMSBWT_GROUP64"])
+@pytest.mark.parametrize("env", ["CMSBWT_GROUP3", "CMSBWT_GROUP64", "CMSBWT_WR_TWO_SCANS"])
 @pytest.mark.parametrize("case", [c for c in cases.small_cases() if c[0] in ("copies_5k_1pct", "tiny_docs",
                                                                          "copies_20k_multiline")],
                          ids=lambda c: c[0])

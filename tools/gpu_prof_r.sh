@@ -7,6 +7,7 @@ OUT=gpurun_out/prof; rm -rf $OUT; mkdir -p $OUT
 B="python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $B > $OUT/kt.log 2>&1
 python3 tools/kstats.py $OUT/kt/kt_kernel_stats.csv > $OUT/kt_summary.txt
+python3 tools/launches.py $OUT/kt/kt_kernel_trace.csv > $OUT/launches.txt
 B1="python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum" \
