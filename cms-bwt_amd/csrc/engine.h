@@ -28,6 +28,7 @@
 #include <deque>
 #include <functional>
 #include <mutex>
+#include <exception>
 #include <thread>
 #include <fstream>
 #include <map>
@@ -85,6 +86,14 @@ struct PackedRunsSym {
   const unsigned long long* sym;
   __host__ __device__ unsigned long long operator()(uint32_t u) const {
     return (runs(u) << kPackSymBits) | sym[u];
+  }
+};
+// (adjusted runs << kPackSymBits) | symbols of a sharded-writer element
+struct PackAdjSym {
+  const uint32_t* adj;
+  const unsigned long long* sym;
+  __host__ __device__ unsigned long long operator()(uint32_t u) const {
+    return ((unsigned long long)adj[u] << kPackSymBits) | sym[u];
   }
 };
 struct PlusOneU64 {
@@ -279,6 +288,10 @@ struct Engine {
   }
   ~Engine() {
     g_alloc = &alloc;
+    if (pend.on) {  // a collection upload still streaming into HBM
+      pend.th.join();
+      pend.on = false;
+    }
     for (void* b : pinned) (void)hipHostFree(b);
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
@@ -886,6 +899,7 @@ struct Engine {
   void upload_collection(const Collection& c) {
     if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
     auto t0 = std::chrono::steady_clock::now();
+    upload_file_end(false);
     reset_collection();
     for (uint64_t d = 0; d < c.ndocs(); d++) {
       uint64_t len = c.off[d + 1] - c.off[d] - 1;
@@ -965,6 +979,60 @@ struct Engine {
     if (err) throw HipError{"HIP error while streaming the collection file"};
   }
 
+  // Whole-file upload started ahead of the reference index (cmsbwt_run): the
+  // raw bytes stream into HBM on the reader threads' own streams while the
+  // index kernels run on the engine stream; load_collection_file_gpu of the
+  // same path then only waits for it.  Buffers are allocated here, on the
+  // calling thread (the caching allocator is not shared with the readers).
+  struct PendingUpload {
+    bool on = false;
+    std::string path;
+    uint64_t fsz = 0;
+    DBuf<uint8_t> raw;
+    std::thread th;
+    std::exception_ptr err;
+  } pend;
+  void upload_file_begin(const std::string& path) {
+    upload_file_end(false);
+    int fd = open(path.c_str(), O_RDONLY);
+    if (fd < 0) return;  // the load reports the error, after the reference's
+    struct stat sbuf;
+    if (fstat(fd, &sbuf) != 0) { close(fd); return; }
+    const uint64_t fsz = (uint64_t)sbuf.st_size, ntiles = (fsz + kRdTile - 1) / kRdTile;
+    pend.raw.alloc(ntiles * kRdTile + kRdTile);
+    ensure_pinned(std::max(1u, std::min(64u, env_u32("CMSBWT_READ_THREADS", 8))),
+                  (uint64_t)std::max(1u, env_u32("CMSBWT_READ_CHUNK_MB", 32)) << 20);
+    pend.on = true;
+    pend.path = path;
+    pend.fsz = fsz;
+    pend.err = nullptr;
+    uint8_t* dst = pend.raw.p;
+    pend.th = std::thread([this, fd, fsz, dst] {
+      try {
+        stream_file(fd, 0, fsz, dst);
+      } catch (...) {
+        pend.err = std::current_exception();
+      }
+      close(fd);
+    });
+  }
+  // Wait for a pending upload; with take, hand its buffer over (else drop it).
+  bool upload_file_end(bool take, const std::string& path = "", DBuf<uint8_t>* raw = nullptr, uint64_t* fsz = nullptr) {
+    if (!pend.on) return false;
+    pend.th.join();
+    pend.on = false;
+    const bool match = take && path == pend.path;
+    std::exception_ptr e = pend.err;
+    pend.err = nullptr;
+    if (match) {
+      if (e) std::rethrow_exception(e);
+      raw->swap_in(pend.raw);
+      *fsz = pend.fsz;
+    }
+    pend.raw.release();
+    return match;
+  }
+
   // Same Collection as read_collection(path, UINT64_MAX) + upload_collection
   // (tests/test_gpu_parity.py::test_gpu_reader_*), produced in HBM.  With a
   // byte range: the documents of bytes [off, off + len) of the file, which
@@ -973,22 +1041,27 @@ struct Engine {
     if (!refLoaded) throw InputError{CMSBWT_EARG, "load the reference first"};
     auto t0 = std::chrono::steady_clock::now();
     reset_collection();
-    int fd = open(path.c_str(), O_RDONLY);
-    if (fd < 0) throw InputError{CMSBWT_EIO, "Error opening file of sequence (" + path + ")"};
-    struct stat sbuf;
-    if (fstat(fd, &sbuf) != 0) { close(fd); throw InputError{CMSBWT_EIO, "cannot stat " + path}; }
-    fileOff = std::min<uint64_t>(fileOff, (uint64_t)sbuf.st_size);
-    const uint64_t fsz = std::min<uint64_t>(sliceLen, (uint64_t)sbuf.st_size - fileOff);  // bytes of this slice
-    const uint64_t ntiles = (fsz + kRdTile - 1) / kRdTile;
     DBuf<uint8_t> raw;
-    raw.alloc(ntiles * kRdTile + kRdTile);  // tiles read whole; '\n'/'>' lookups one past len
-    try {
-      stream_file(fd, fileOff, fsz, raw.p);
-    } catch (...) {
+    uint64_t fsz = 0;
+    const bool whole = fileOff == 0 && sliceLen == ~0ull;
+    if (!(whole && upload_file_end(true, path, &raw, &fsz))) {
+      int fd = open(path.c_str(), O_RDONLY);
+      if (fd < 0) throw InputError{CMSBWT_EIO, "Error opening file of sequence (" + path + ")"};
+      struct stat sbuf;
+      if (fstat(fd, &sbuf) != 0) { close(fd); throw InputError{CMSBWT_EIO, "cannot stat " + path}; }
+      fileOff = std::min<uint64_t>(fileOff, (uint64_t)sbuf.st_size);
+      fsz = std::min<uint64_t>(sliceLen, (uint64_t)sbuf.st_size - fileOff);  // bytes of this slice
+      const uint64_t ntiles0 = (fsz + kRdTile - 1) / kRdTile;
+      raw.alloc(ntiles0 * kRdTile + kRdTile);  // tiles read whole; '\n'/'>' lookups one past len
+      try {
+        stream_file(fd, fileOff, fsz, raw.p);
+      } catch (...) {
+        close(fd);
+        throw;
+      }
       close(fd);
-      throw;
     }
-    close(fd);
+    const uint64_t ntiles = (fsz + kRdTile - 1) / kRdTile;
     DBuf<uint64_t> lastNl, carry;
     lastNl.alloc(ntiles + 1);
     carry.alloc(ntiles + 1);
@@ -2340,7 +2413,8 @@ struct Engine {
     DBuf<int64_t> bucket;
     DBuf<uint32_t> eBase, rOf, ehl;
     DBuf<uint4> info1;
-    DBuf<unsigned long long> info2, cum, runIn, symIn;
+    DBuf<unsigned long long> info2, cum, runIn, symIn;  // symPacked: runIn holds both (symIn unused)
+    bool symPacked = false;
     DBuf<uint32_t> uruns, uhl, uprev;
     DBuf<unsigned long long> runOff, symOff, locStart, gStart;
     DBuf<uint8_t> locChar, gChar;

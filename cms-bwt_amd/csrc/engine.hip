@@ -317,8 +317,23 @@ int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path
     }
     fclose(f);
   }
-  rc = cmsbwt_load_reference_file(ctx, ref_path);
   Engine& e = *ctx->e;
+  {
+    // the collection streams into HBM (reader threads, their own streams)
+    // while the reference index is built on the engine stream; the device
+    // reader then starts from the uploaded bytes.  Only for the device reader
+    // path (no -p); errors are reported at the load, after the reference's.
+    const char* hr = getenv("CMSBWT_HOST_READER");
+    const char* ov = getenv("CMSBWT_OVERLAP_UPLOAD");
+    if (a->prefix == UINT64_MAX && !(hr && *hr && *hr != '0') && !(ov && *ov == '0')) {
+      try {
+        e.upload_file_begin(coll_path);
+      } catch (...) {
+        // no overlap (e.g. out of pinned memory): the load reads the file itself
+      }
+    }
+  }
+  rc = cmsbwt_load_reference_file(ctx, ref_path);
   if (rc) {
     if (e.hix.file_bytes) log << "n = " << e.hix.file_bytes << '\n';
     return fail(rc);
