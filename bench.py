@@ -194,10 +194,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    # Rehearsal of the N>1 path on a one-GPU box (never set by the driver):
+    # CMSBWT_BENCH_SAME_GPU=1 puts every rank on device 0 and uses gloo (host
+    # staging) instead of RCCL, which allows one rank per device.
+    same_gpu = os.environ.get("CMSBWT_BENCH_SAME_GPU", "0") == "1"
+    if same_gpu:
+        local = 0
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", init_method="env://")
+        dist.init_process_group("gloo" if same_gpu else "nccl", init_method="env://")
 
     import cmsbwt
     import cmsbwt.dist as cdist
@@ -236,7 +242,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if dist:
-        t = torch.tensor([dt], device=f"cuda:{local}", dtype=torch.float64)
+        t = torch.tensor([dt], device="cpu" if same_gpu else f"cuda:{local}", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     st = eng.stats()

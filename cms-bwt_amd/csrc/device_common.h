@@ -23,6 +23,10 @@ struct DevRef {
   const uint32_t* isa;
   const int32_t* lcp;     // n+1 entries
   const int32_t* plcp;    // max-neighbour PLCP (FN:272-274)
+  // min(PLCP, 255) as bytes (n + 32): the PLCP skip's first window (16 entries
+  // below the match end) only asks PLCP[q] >= T - q <= 16, so one 16-B load
+  // decides it, from a 1/4-size array that stays in the XCDs' L2
+  const uint8_t* plcp8;
   const uint8_t* bwt;
   const int32_t* lvl[kMaxLevels];  // lvl[0][b] = min lcp[64b..64b+63], lvl[k] = min of 64 lvl[k-1]
   uint32_t lvlLen[kMaxLevels];

@@ -297,7 +297,7 @@ void Engine::dm_route_halo(uint64_t* itemCounts, uint64_t* wordCounts) {
   off.alloc(K);
   mk_dm_halo_count(S, K, dm.dPsplit.p, world, dm.rank, R.n, c.p, st);
   exscan(c.p, off.p, 0u, K);
-  const uint32_t np = K ? read1(off.p + (K - 1)) + read1(c.p + (K - 1)) : 0;
+  const uint32_t np = K ? (uint32_t)sum2(off.p + (K - 1), c.p + (K - 1)) : 0;
   dm.npairs = np;
   DBuf<uint32_t> dest, item, perm, w;
   dest.alloc(np);
@@ -416,7 +416,7 @@ void Engine::dm_units(int64_t* out) {
   dm.eBase.alloc(n);
   mk_dm_el_count(dsa.p, IS.posBegin.p, IS.slot.p, n, dm.E, dm.P0, dm.P1, m.p, st);
   exscan(m.p, dm.eBase.p, 0u, n);
-  const uint64_t V64 = (uint64_t)read1(dm.eBase.p + (n - 1)) + read1(m.p + (n - 1));
+  const uint64_t V64 = sum2(dm.eBase.p + (n - 1), m.p + (n - 1));
   if (V64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer elements"};
   const uint32_t V = dm.V = (uint32_t)V64;
   dm.rOf.alloc(std::max<uint32_t>(V, 1));
@@ -488,8 +488,8 @@ uint64_t Engine::dm_emit(const int64_t* unitsAll) {
   auto runs64 = rocprim::make_transform_iterator(dm.uruns.p, WidenU64());
   exscan(runs64, dm.runOff.p, 0ull, Uw);
   exscan(sym.p, dm.symOff.p, 0ull, Uw);
-  dm.Rn = read1(dm.runOff.p + (Uw - 1)) + read1(dm.uruns.p + (Uw - 1));
-  dm.symbols = read1(dm.symOff.p + (Uw - 1)) + read1(sym.p + (Uw - 1));
+  dm.Rn = sum2(dm.runOff.p + (Uw - 1), dm.uruns.p + (Uw - 1));
+  dm.symbols = sum2(dm.symOff.p + (Uw - 1), sym.p + (Uw - 1));
   const ElemIn ei = dm_elem_in();
   if (dm.rank == 0) {
     // rank 0 holds the output: its own runs go straight to their global indices
@@ -504,7 +504,7 @@ uint64_t Engine::dm_emit(const int64_t* unitsAll) {
     srcOff.alloc(Uw);
     mk_dm_own_runs(dm.uruns.p, Uw, dsa.p, dm.E, n, dm.P0, dm.P1, own.p, st);
     exscan(own.p, srcOff.p, 0ull, Uw);
-    dm.Rloc = read1(srcOff.p + (Uw - 1)) + read1(own.p + (Uw - 1));
+    dm.Rloc = sum2(srcOff.p + (Uw - 1), own.p + (Uw - 1));
     dm.locStart.alloc(std::max<uint64_t>(dm.Rloc, 1));
     dm.locChar.alloc(std::max<uint64_t>(dm.Rloc, 1));
     mk_dm_el_emit(ei, dm.V, dm.runIn.p, dm.symPacked ? nullptr : dm.symIn.p, srcOff.p, dm.symOff.p, dm.uprev.p, dm.uhl.p, dm.ehl.p,
@@ -537,7 +537,7 @@ void Engine::dm_finish(const unsigned long long* const* starts, const uint8_t* c
     if (k == dm.rank) continue;
     mk_dm_own_runs(dm.uruns.p, Uw, dsa.p, dm.E, n, dm.Psplit[k], dm.Psplit[k + 1], own.p, st);
     exscan(own.p, srcOff.p, 0ull, Uw);
-    const uint64_t rk = read1(srcOff.p + (Uw - 1)) + read1(own.p + (Uw - 1));
+    const uint64_t rk = sum2(srcOff.p + (Uw - 1), own.p + (Uw - 1));
     if (rk != counts[k]) throw InputError{CMSBWT_EINPUT, "internal: rank " + std::to_string(k) + " sent " +
                                                              std::to_string(counts[k]) + " runs, expected " +
                                                              std::to_string(rk)};

@@ -235,6 +235,7 @@ struct Engine {
   HostIndex hix;
   DBuf<uint8_t> dx, dbwt;
   DBuf<int32_t> dsa, dlcp, dplcp;
+  DBuf<uint8_t> dplcp8;  // min(PLCP, 255), the walk's first skip window
   DBuf<uint32_t> disa;
   DBuf<uint32_t> dpfx;
   DBuf<uint32_t> dld;
@@ -311,6 +312,17 @@ struct Engine {
     HIPCHK(hipMemcpyAsync(&v, d, sizeof(T_), hipMemcpyDeviceToHost, st));
     sync();
     return v;
+  }
+  // *a + *b read back with one synchronisation (the sizes after a scan: last
+  // exclusive offset + last count)
+  template <class A_, class B_>
+  uint64_t sum2(const A_* a, const B_* b) {
+    A_ va;
+    B_ vb;
+    HIPCHK(hipMemcpyAsync(&va, a, sizeof(A_), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipMemcpyAsync(&vb, b, sizeof(B_), hipMemcpyDeviceToHost, st));
+    sync();
+    return (uint64_t)va + (uint64_t)vb;
   }
 
   // ---- rocPRIM helpers
@@ -403,7 +415,7 @@ struct Engine {
       mk_sel_count(flags, n, tc.p, st);
       exscan(tc.p, to.p, 0u, nt);
       mk_sel_write(in, flags, n, to.p, out, st);
-      return read1(to.p + (nt - 1)) + read1(tc.p + (nt - 1));
+      return (uint32_t)sum2(to.p + (nt - 1), tc.p + (nt - 1));
     }
     DBuf<uint32_t> cnt;
     cnt.alloc(1);
@@ -528,6 +540,7 @@ struct Engine {
     R.isa = disa.p;
     R.lcp = dlcp.p;
     R.plcp = dplcp.p;
+    stage_plcp8(n);
     R.bwt = dbwt.p;
     R.n = n;
     if (read1(err.p)) throw InputError{CMSBWT_EINPUT, "internal: PLCP monotonicity violated"};
@@ -560,6 +573,13 @@ struct Engine {
     mark("adjacency");
     hix.t_sa = std::chrono::duration<double>(t1 - t0).count();
     hix.t_lcp = std::chrono::duration<double>(now() - t1).count();
+  }
+
+  void stage_plcp8(uint32_t n) {
+    dplcp8.alloc((uint64_t)n + 32);
+    HIPCHK(hipMemsetAsync(dplcp8.p + n, 0, 32, st));
+    launch_ix_plcp8(dplcp.p, n, dplcp8.p, st);
+    R.plcp8 = dplcp8.p;
   }
 
   // =====================================================================
@@ -650,6 +670,7 @@ struct Engine {
     R.isa = disa.p;
     R.lcp = dlcp.p;
     R.plcp = dplcp.p;
+    stage_plcp8(n);
     R.bwt = dbwt.p;
     R.n = n;
     build_prefix_tables(false);
@@ -1274,7 +1295,7 @@ struct Engine {
     launch_chunk_with_end(plan.dch.p, chunkCount.p, nch, withEnd.p, st);
     exscan(withEnd.p, chunkBase.p, 0ull, nch);
     {
-      const unsigned long long tot = read1(chunkBase.p + (nch - 1)) + read1(withEnd.p + (nch - 1));
+      const unsigned long long tot = sum2(chunkBase.p + (nch - 1), withEnd.p + (nch - 1));
       // uint32 head indices and labels (1 .. H + 1): the reference's int32
       // limit (FN:1436-1437, 1456) is lifted to 2^32 - 2 heads
       if (tot >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "more than 2^32-2 heads (uint32 head indices)"};
@@ -1480,7 +1501,7 @@ struct Engine {
           sort_keys(bigList.p + 1, bpos.p, nb, bN);
           mk_grp_big_sizes(bpos.p, nb, hb.p, sz.p, st);
           exscan(sz.p, off.p, 0u, nb);
-          const uint32_t B = read1(off.p + (nb - 1)) + read1(sz.p + (nb - 1));
+          const uint32_t B = (uint32_t)sum2(off.p + (nb - 1), sz.p + (nb - 1));
           DBuf<uint32_t> bidx, pB, pB2;
           DBuf<unsigned long long> kB, kB2;
           bidx.alloc(B); pB.alloc(B); pB2.alloc(B); kB.alloc(B); kB2.alloc(B);
@@ -1573,7 +1594,7 @@ struct Engine {
     sort_keys(bigList.p + 1, items.p, nb, bits_for(K));
     mk_item_counts_of(items.p, nb, S.count, cnt.p, st);
     exscan(cnt.p, off.p, 0u, nb);
-    const uint32_t B = read1(off.p + (nb - 1)) + read1(cnt.p + (nb - 1));
+    const uint32_t B = (uint32_t)sum2(off.p + (nb - 1), cnt.p + (nb - 1));
     DBuf<unsigned long long> bk, bk2;
     DBuf<uint32_t> bslots;
     bk.alloc(B); bk2.alloc(B); bslots.alloc(B);
@@ -1623,7 +1644,7 @@ struct Engine {
     itemOff.alloc(K);
     mk_win_cross(S, K, wincl.p, n, crossCnt.p, nullptr, nullptr, nullptr, cstatsP + 4, 0, st);
     exscan(crossCnt.p, itemOff.p, 0u, K);
-    const uint32_t ncross = K ? read1(itemOff.p + (K - 1)) + read1(crossCnt.p + (K - 1)) : 0;
+    const uint32_t ncross = K ? (uint32_t)sum2(itemOff.p + (K - 1), crossCnt.p + (K - 1)) : 0;
     keyW.alloc(std::max<uint32_t>(ncross, 1));
     keyW2.alloc(std::max<uint32_t>(ncross, 1));
     valQ.alloc(std::max<uint32_t>(ncross, 1));
@@ -1866,7 +1887,7 @@ struct Engine {
         cntR.zero(st);
         mk_act_count(posBegin.p, sCount.p, disa.p, n, cntR.p, st);
         exscan(cntR.p, offR.p, 0u, n);
-        U = read1(offR.p + (n - 1)) + read1(cntR.p + (n - 1));
+        U = (uint32_t)sum2(offR.p + (n - 1), cntR.p + (n - 1));
         act.alloc(std::max<uint32_t>(U, 1)); act2.alloc(std::max<uint32_t>(U, 1));
         mk_act_fill(posBegin.p, sSlot.p, sCount.p, disa.p, headBase.p, offR.p, n, act.p, st);
       }
@@ -1946,21 +1967,22 @@ struct Engine {
     counter.alloc((uint64_t)H + 1);
     counter.zero(st);
     uint64_t W = 0;
+    // work volume (statistics only): sum of untilNext, read back with the
+    // counter statistics
+    DBuf<uint64_t> wsum;
+    wsum.alloc(1);
     {
-      // work volume (statistics only): sum of untilNext
-      DBuf<uint64_t> wsum;
-      wsum.alloc(1);
       auto u64in = rocprim::make_transform_iterator(sUntil.p, WidenU64());
       size_t b = 0;
       HIPCHK(rocprim::reduce(nullptr, b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
       HIPCHK(rocprim::reduce(scratch(b), b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
-      W = read1(wsum.p);
       HIPCHK(hipEventRecord(evm[4], st));
       if (!check) counter_phase(S, K, posBegin.p, posF.p, nhr.p, counter.p, cstats.p, n, 0, n, false);
       HIPCHK(hipEventRecord(evm[5], st));
     }
     unsigned long long cs[8];
     uint64_t queryViol = 0;
+    HIPCHK(hipMemcpyAsync(&W, wsum.p, 8, hipMemcpyDeviceToHost, st));
     if (check) {
       queryViol = counter_checked(IS, h, nhr, hostMask, cstats, n, cs);
     } else {
@@ -1999,7 +2021,7 @@ struct Engine {
       m.alloc(n); eBase.alloc(n);
       mk_el_count(headBase.p, n, E, H, m.p, st);
       exscan(m.p, eBase.p, 0u, n);
-      const uint64_t V64 = (uint64_t)read1(eBase.p + (n - 1)) + read1(m.p + (n - 1));
+      const uint64_t V64 = sum2(eBase.p + (n - 1), m.p + (n - 1));
       if (V64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer elements"};
       const uint32_t V = (uint32_t)V64;
       DBuf<uint32_t> rOf;
@@ -2049,7 +2071,7 @@ struct Engine {
         exscan(runs64, wrunOff.p, 0ull, V);
         exscan(wsym.p, wsymOff.p, 0ull, V);
         Rn = read1(wrunOff.p + (V - 1)) + adj.host(V - 1, this);
-        symbols = read1(wsymOff.p + (V - 1)) + read1(wsym.p + (V - 1));
+        symbols = sum2(wsymOff.p + (V - 1), wsym.p + (V - 1));
       }
       runStart.alloc(std::max<uint64_t>(Rn, 1)); runChar.alloc(std::max<uint64_t>(Rn, 1));
       mk_el_wr_emit(ei, V, wrunOff.p, packed ? nullptr : wsymOff.p, wprev.p, runStart.p, runChar.p, st);

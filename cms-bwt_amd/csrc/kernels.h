@@ -103,6 +103,8 @@ void launch_ix_lcp(const uint8_t* x, const int32_t* sa, uint32_t n, const uint32
                    int32_t* plcpRaw, int32_t* lcp, int32_t* plcp, hipStream_t st);
 void launch_ix_bwt(const uint8_t* x, const int32_t* sa, uint32_t n, uint8_t* bwt, hipStream_t st);
 void launch_ix_plcp_check(const int32_t* plcp, uint32_t n, uint32_t* err, hipStream_t st);
+// min(PLCP, 255) bytes for the walk's first skip window (DevRef::plcp8)
+void launch_ix_plcp8(const int32_t* plcp, uint32_t n, uint8_t* out, hipStream_t st);
 void launch_ix_level(const int32_t* prev, uint32_t prevLen, int32_t* cur, uint32_t curLen, hipStream_t st);
 void launch_ix_child(const uint8_t* x, const int32_t* sa, const int32_t* lcp, uint32_t n, uint32_t* ld,
                      hipStream_t st);

@@ -19,7 +19,7 @@
 //   LCE         16 B of x and of the text      POST / LCE_COOP
 //   LCE_COOP    (none) the whole wave compares 1 KiB per step of one lane's
 //               long extension with coalesced loads, lane by lane -> POST
-//   SKIP1       PLCP[T-16..T-1]                ISA1 / SKIP0 (FN:1176-1185)
+//   SKIP1       min(PLCP, 255)[T-16..T-1], bytes  ISA1 / SKIP0 (FN:1176-1185)
 //   SKIP0       PLCP[pos+1]                    ISA1 / GALLOP
 //   GALLOP/SKIPBS  one PLCP probe              ISA1
 //   ISA1        record of ISA[pos+1]           ADV / ADJ0    (FN:1187, FN:11-25)
@@ -307,6 +307,7 @@ k_ms_walk2(Walk2Args A) {
   const uintptr_t X = (uintptr_t)R.x;
   const uintptr_t SA = (uintptr_t)R.sa;
   const uintptr_t P = (uintptr_t)R.plcp;
+  const uintptr_t P8 = (uintptr_t)R.plcp8;
   const uint32_t lane = threadIdx.x & 63;
 
   // chunk
@@ -626,8 +627,8 @@ k_ms_walk2(Walk2Args A) {
         // probe the 16 entries below T first
         phase = PH_SKIP1;
         const uint64_t TT = (uint64_t)pos + 1 + len;
-        ad0 = P + 4ull * (TT >= 16 ? TT - 16 : 0);
-        use = U0Q | U1Q | U4Q | U5Q;
+        ad0 = P8 + (TT >= 16 ? TT - 16 : 0);  // min(PLCP, 255) bytes: one 16-B load
+        use = U0Q;
         if (pfxExact && hasPfx) {  // and the 32 text bytes around the match end: the next window
           ad2 = T + skip_text_base();
           use |= U2Q | U3Q;
@@ -710,11 +711,11 @@ k_ms_walk2(Walk2Args A) {
       // pos+1 (kmin = q0 - Wb when the window starts below it).
       const uint32_t TT = pos + 1 + len, q0 = pos + 1;
       const uint32_t Wb = TT >= 16 ? TT - 16 : 0, D = TT - Wb;
-      const uint32_t e[16] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w,
-                              v4.x, v4.y, v4.z, v4.w, v5.x, v5.y, v5.z, v5.w};
+      // entries as bytes min(PLCP, 255): exact for the test e + k >= D <= 16
+      const uint32_t w4[4] = {v0.x, v0.y, v0.z, v0.w};
       uint32_t c = 0;
 #pragma unroll
-      for (uint32_t k = 0; k < 16; k++) c += e[k] + k < D ? 1u : 0u;
+      for (uint32_t k = 0; k < 16; k++) c += ((w4[k >> 2] >> (8 * (k & 3))) & 0xffu) + k < D ? 1u : 0u;
       if (Wb <= q0 || c > 0) {
         const uint32_t kmin = Wb <= q0 ? q0 - Wb : 0u;
         skS = Wb + (c > kmin ? c : kmin) - q0;

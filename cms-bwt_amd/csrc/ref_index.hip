@@ -328,6 +328,13 @@ __global__ void k_ix_pfx_one(uint32_t* __restrict__ tab, uint64_t E, const int32
 
 static inline dim3 gix(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
+__global__ void k_ix_plcp8(const int32_t* __restrict__ plcp, uint32_t n, uint8_t* __restrict__ out) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < n) out[q] = (uint8_t)min(max(plcp[q], 0), 255);
+}
+void launch_ix_plcp8(const int32_t* plcp, uint32_t n, uint8_t* out, hipStream_t st) {
+  hipLaunchKernelGGL(k_ix_plcp8, dim3((n + 255) / 256), dim3(256), 0, st, plcp, n, out);
+}
 void launch_ix_plcp_check(const int32_t* plcp, uint32_t n, uint32_t* err, hipStream_t st) {
   if (n > 1) hipLaunchKernelGGL(k_ix_plcp_check, gix(n), dim3(256), 0, st, plcp, n, err);
 }
