@@ -147,14 +147,18 @@ void Engine::dm_group(const int32_t* recv, uint64_t nrecv, uint32_t* saCounts) {
   }
   // slot-major members: item of each slot, received index of each slot
   dm.itemOfSlot.alloc(Hp);
-  dm.Pm.alloc(Hp);
   if (Hp) {
     DBuf<uint32_t> mark;
     mark.alloc(Hp);
     mark.zero(st);
     mk_slot_mark(S.slot, K, mark.p, st);
     inscan(mark.p, dm.itemOfSlot.p, Hp, rocprim::plus<uint32_t>());
-    mk_slot_members(S, dm.itemOfSlot.p, dm.IS.P.p, Hp, dm.Pm.p, st);
+  }
+  if (dm.IS.slotIsFirst) {
+    dm.Pm.swap_in(dm.IS.P);  // members already in slot order
+  } else {
+    dm.Pm.alloc(Hp);
+    if (Hp) mk_slot_members(S, dm.itemOfSlot.p, dm.IS.P.p, Hp, dm.Pm.p, st);
   }
   const bool ownsEnd = dm.P0 <= n - 1 && n - 1 < dm.P1;
   mk_dm_sa_counts(dsa.p, dm.IS.posBegin.p, S.slot, n, ownsEnd ? dm.E : 0, saCounts, st);

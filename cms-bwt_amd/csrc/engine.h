@@ -1442,6 +1442,7 @@ struct Engine {
   // slots (prefixSumForPositions, FN:1504-1515), per-position item ranges.
   struct ItemSet {
     uint32_t K = 0;
+    bool slotIsFirst = false;  // slot[q] == first[q]: P is already slot-major
     DBuf<uint32_t> P;  // member (head index) of each sorted head
     DBuf<uint32_t> pos, len, isa, until, count, first, slot;  // map order; slot has K+1 entries
     DBuf<uint8_t> small;
@@ -1510,6 +1511,11 @@ struct Engine {
           sort_pairs(kB.p, kB2.p, pB.p, pB2.p, B, 2 * bN + bL);  // stable: idx order kept per key
           mk_scatter_kp(bidx.p, B, kB2.p, pB2.p, gk2.p, perm2.p, st);
           mk_grp_big_fields(bidx.p, B, perm2.p, h, tsS.p, smS.p, st);
+          // their members in map order too (k_grp_seg ranks the others so)
+          DBuf<uint8_t> tS;
+          tS.alloc(B);
+          mk_grp_big_maporder(bpos.p, nb, hb.p, off.p, gk2.p, perm2.p, tsS.p, smS.p, kB.p, pB.p, pB2.p, tS.p, bidx.p,
+                              bN, st);
         }
       }
     } else if (packed) {  // one sort on the composite key
@@ -1548,17 +1554,27 @@ struct Engine {
     mk_item_count(aFirst.p, aCount.p, K, H, st);
     key.release();
     key2.release();
-    // map order inside each position (match.h:27-33): one thread per
-    // position reorders its items, already sorted by (len, isaNext)
+    // map order inside each position (match.h:27-33): the position-first
+    // grouping ranked the members in map order already; the composite-key
+    // sorts give (len, isaNext) order and one thread per position reorders
+    // its items
     DBuf<uint32_t> pbA, order;
     pbA.alloc((uint64_t)n + 1);
-    order.alloc(K);
     mk_pos_begin(aPos.p, K, n, pbA.p, st);
-    mk_map_order(pbA.p, aLen.p, aSmall.p, n, order.p, st);
-    S.pos.alloc(K); S.len.alloc(K); S.isa.alloc(K); S.until.alloc(K); S.count.alloc(K); S.first.alloc(K);
-    S.slot.alloc((uint64_t)K + 1); S.small.alloc(K); S.sk.alloc(K);
+    S.slotIsFirst = posFirst;  // items and their members share one order
+    if (posFirst) {
+      S.pos.swap_in(aPos); S.len.swap_in(aLen); S.isa.swap_in(aIsa); S.until.swap_in(aUntil);
+      S.count.swap_in(aCount); S.first.swap_in(aFirst); S.small.swap_in(aSmall);
+      S.slot.alloc((uint64_t)K + 1); S.sk.alloc(K);
+    } else {
+      order.alloc(K);
+      mk_map_order(pbA.p, aLen.p, aSmall.p, n, order.p, st);
+      S.pos.alloc(K); S.len.alloc(K); S.isa.alloc(K); S.until.alloc(K); S.count.alloc(K); S.first.alloc(K);
+      S.slot.alloc((uint64_t)K + 1); S.small.alloc(K); S.sk.alloc(K);
+      ItemsSoA SS0 = S.soa();
+      mk_item_permute(A0, order.p, SS0, K, st);
+    }
     ItemsSoA SS = S.soa();
-    mk_item_permute(A0, order.p, SS, K, st);
     mk_item_sk(SS, K, st);
     order.release();
     aPos.release(); aLen.release(); aIsa.release(); aUntil.release(); aCount.release(); aFirst.release();
@@ -1704,6 +1720,7 @@ struct Engine {
     up(IS.pos, I.pos); up(IS.len, I.len); up(IS.isa, I.isa); up(IS.until, I.until);
     up(IS.count, I.count); up(IS.first, I.first); up(IS.small, I.small); up(IS.P, I.P);
     IS.K = k;
+    IS.slotIsFirst = false;
     IS.slot.alloc((uint64_t)k + 1);
     IS.sk.alloc(k);
     ItemsSoA SS = IS.soa();
@@ -1849,7 +1866,6 @@ struct Engine {
     // slot-major members: item of each slot and member idx of each slot
     DBuf<uint32_t> itemOfSlot, Pm;
     itemOfSlot.alloc(H);
-    Pm.alloc(H);
     {
       DBuf<uint32_t> mark;
       mark.alloc(H);
@@ -1857,14 +1873,20 @@ struct Engine {
       mk_slot_mark(sSlot.p, K, mark.p, st);
       inscan(mark.p, itemOfSlot.p, H, rocprim::plus<uint32_t>());
     }
-    mk_slot_members(S, itemOfSlot.p, P.p, H, Pm.p, st);
+    // members in slot order: P itself when the grouping emitted items and
+    // members in one order (P stays: the host replay reads it)
+    if (!IS.slotIsFirst) {
+      Pm.alloc(H);
+      mk_slot_members(S, itemOfSlot.p, P.p, H, Pm.p, st);
+    }
+    const uint32_t* const PmP = IS.slotIsFirst ? P.p : Pm.p;
     {
       DBuf<uint32_t> rankBase, gBase;
       rankBase.alloc(n);
       gBase.alloc(n);
       mk_pos_rank_base(posBegin.p, sSlot.p, disa.p, itemRankBase.p, headBase.p, n, E, keepT ? rankBase.p : nullptr,
                        gBase.p, st);
-      mk_ranks_slot(S, itemOfSlot.p, Pm.p, H, rankBase.p, gBase.p, n, keepT ? T.p : nullptr, saT.p, grp.p, nullptr,
+      mk_ranks_slot(S, itemOfSlot.p, PmP, H, rankBase.p, gBase.p, n, keepT ? T.p : nullptr, saT.p, grp.p, nullptr,
                     st);
     }
     itemRankBase.release();
@@ -1952,9 +1974,9 @@ struct Engine {
         nbi.alloc(H);
         if (fused) {  // gather + rank inside the item in one pass
           mk_nhr_idx(grp.p, 1u, hNext.p, H, nbi.p, st);
-          mk_nhr_rank(Pm.p, nbi.p, itemOfSlot.p, H, nhr.p, st);
+          mk_nhr_rank(PmP, nbi.p, itemOfSlot.p, H, nhr.p, st);
         } else {
-          mk_nhr_slot(Pm.p, grp.p, 1u, hNext.p, H, nbi.p, nhr.p, st);
+          mk_nhr_slot(PmP, grp.p, 1u, hNext.p, H, nbi.p, nhr.p, st);
         }
       }
       sort_nhr_items(S, K, itemOfSlot.p, nhr.p, H, fused);

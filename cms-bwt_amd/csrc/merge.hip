@@ -56,21 +56,50 @@ __global__ void __launch_bounds__(256) k_grp_seg(const uint32_t* __restrict__ po
                                                  uint32_t* __restrict__ tsOut, uint8_t* __restrict__ smOut,
                                                  uint32_t* __restrict__ bigList, uint32_t maxSmall,
                                                  int32_t* __restrict__ diffEnds, uint32_t n) {
-  // one thread per sorted head: its rank inside its position's segment by
-  // counting over the segment, staged in LDS with a halo either side
-  __shared__ unsigned long long lk[kGrpBlock + 2 * kGrpHalo];
+  // one thread per sorted head: its rank inside its position's segment in
+  // MAP order (match.h:27-33 on consistent data: smaller=true items by (len,
+  // isaNext), then smaller=false items by (len descending, isaNext); members
+  // of an item by idx), by counting over the segment staged in LDS with a
+  // halo either side.  An item's class is the `smaller` of its first-inserted
+  // (lowest idx) member, as the first std::map insertion keeps it.
+  constexpr uint32_t W = kGrpBlock + 2 * kGrpHalo;
+  __shared__ unsigned long long lk[W], mk[W];
+  __shared__ uint32_t lp[W];
+  __shared__ uint8_t ls[W];
   __shared__ int32_t endL[kGrpEnds];
   const uint32_t k0 = blockIdx.x * kGrpBlock;
   const int64_t base = (int64_t)k0 - kGrpHalo;
-  for (uint32_t i = threadIdx.x; i < kGrpBlock + 2 * kGrpHalo; i += blockDim.x) {
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) {
     const int64_t j = base + i;
     if (j >= 0 && j < (int64_t)H) {
       const HeadKV w = kv[j];
       lk[i] = ((unsigned long long)(w.len & 0x7fffffffu) << bN) | w.isa;
+      lp[i] = posS[j];
+      ls[i] = (uint8_t)(w.len >> 31);
+    } else {
+      lp[i] = 0xffffffffu;
     }
   }
   if (diffEnds)
     for (uint32_t i = threadIdx.x; i < kGrpEnds; i += blockDim.x) endL[i] = 0;
+  __syncthreads();
+  // map key of every staged head: its item's first member is the leftmost
+  // entry of its position with the same (len, isaNext) (kv is idx-ascending
+  // per position).  Only heads of segments ranked here (<= the halo, inside
+  // the window) need it; the scan has fixed bounds (segment start from hb),
+  // so its LDS reads pipeline
+  const uint32_t lim = min(maxSmall, kGrpHalo);
+  for (uint32_t i = threadIdx.x; i < W; i += blockDim.x) {
+    const uint32_t pi = lp[i];
+    if (pi == 0xffffffffu) continue;
+    const int64_t sb = (int64_t)hb[pi] - base, se = (int64_t)hb[pi + 1] - base;
+    if (se - sb > lim || sb < 0 || se > (int64_t)W) continue;
+    const unsigned long long me = lk[i];
+    uint32_t f = i;
+    for (int64_t j = (int64_t)i - 1; j >= sb; j--) f = lk[j] == me ? (uint32_t)j : f;
+    const unsigned long long L = me >> bN, I = me & ((1ull << bN) - 1);
+    mk[i] = ls[f] ? ((L << bN) | I) : ((1ull << 63) | ((~L & ((1ull << bL) - 1)) << bN) | I);
+  }
   __syncthreads();
   const uint32_t k = k0 + threadIdx.x;
   if (diffEnds) {
@@ -101,16 +130,82 @@ __global__ void __launch_bounds__(256) k_grp_seg(const uint32_t* __restrict__ po
     if (k == b) bigList[1 + atomicAdd(bigList, 1u)] = p;
     return;
   }
-  // (len, isa) order; equal keys keep idx order (kv is idx-ascending per position)
+  // map order; members of an item keep idx order (kv is idx-ascending per position)
+  const unsigned long long mme = mk[threadIdx.x + kGrpHalo];
   uint32_t r = 0;
   for (uint32_t j = b; j < e; j++) {
-    const unsigned long long lj = lk[j - base];
-    r += (lj < me || (lj == me && j < k)) ? 1u : 0u;
+    const unsigned long long mj = mk[j - base];
+    r += (mj < mme || (mj == mme && j < k)) ? 1u : 0u;
   }
   key[b + r] = hp | me;
   perm[b + r] = v.idx;
   tsOut[b + r] = v.tonext;
   smOut[b + r] = (uint8_t)(v.len >> 31);
+}
+// Big segments come out of their radix sort in (len, isaNext, idx) order: one
+// block per big position puts its members in map order (smaller=true items as
+// sorted, then smaller=false items by len descending, isaNext ascending; an
+// item's class from its first, lowest-idx member) through tmp at the
+// segment's offset in the big list.  Destinations from one prefix count of the
+// smaller=false members: an S member at t goes to t - F(t); an F member of
+// the len group [gs, ge) to nS + (nF - F(ge)) + (F(t) - F(gs)).
+__global__ void __launch_bounds__(256) k_grp_big_maporder(
+    const uint32_t* __restrict__ bpos, uint32_t nb, const uint32_t* __restrict__ hb, const uint32_t* __restrict__ off,
+    unsigned long long* __restrict__ key, uint32_t* __restrict__ perm, uint32_t* __restrict__ ts,
+    uint8_t* __restrict__ sm, unsigned long long* __restrict__ tKey, uint32_t* __restrict__ tPerm,
+    uint32_t* __restrict__ tTs, uint8_t* __restrict__ tSm, uint32_t* __restrict__ tF, int bN) {
+  __shared__ uint32_t wsum[4];
+  const uint32_t b = hb[bpos[blockIdx.x]], m = hb[bpos[blockIdx.x] + 1] - b, o = off[blockIdx.x];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  uint32_t carry = 0;
+  for (uint32_t c = 0; c < m; c += 256) {
+    const uint32_t t = c + threadIdx.x;
+    bool f = false;
+    if (t < m) {
+      const unsigned long long kt = key[b + t];
+      tKey[o + t] = kt; tPerm[o + t] = perm[b + t]; tTs[o + t] = ts[b + t]; tSm[o + t] = sm[b + t];
+      uint32_t lo = 0, hi = t;  // first member of the item: first entry with key kt
+      while (lo < hi) {
+        const uint32_t md = (lo + hi) >> 1;
+        if (key[b + md] < kt) lo = md + 1; else hi = md;
+      }
+      f = sm[b + lo] == 0;
+    }
+    const uint64_t bal = __ballot(f);
+    if (lane == 0) wsum[wv] = (uint32_t)__popcll(bal);
+    __syncthreads();
+    uint32_t pre = carry;
+    for (uint32_t x = 0; x < wv; x++) pre += wsum[x];
+    if (t < m) tF[o + t] = pre + (uint32_t)__popcll(bal & ((1ull << lane) - 1));
+    carry += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    __syncthreads();
+  }
+  const uint32_t nF = carry, nS = m - nF;
+  auto F = [&](uint32_t t) { return t < m ? tF[o + t] : nF; };
+  for (uint32_t t = threadIdx.x; t < m; t += 256) {
+    const unsigned long long kt = tKey[o + t];
+    const bool isF = F(t + 1) != F(t);
+    uint32_t dst;
+    if (!isF) {
+      dst = t - F(t);
+    } else {
+      const unsigned long long g = kt >> bN;  // pos | len
+      uint32_t lo = 0, hi = t;
+      while (lo < hi) {
+        const uint32_t md = (lo + hi) >> 1;
+        if ((tKey[o + md] >> bN) < g) lo = md + 1; else hi = md;
+      }
+      const uint32_t gs = lo;
+      lo = t + 1; hi = m;
+      while (lo < hi) {
+        const uint32_t md = (lo + hi) >> 1;
+        if ((tKey[o + md] >> bN) <= g) lo = md + 1; else hi = md;
+      }
+      const uint32_t ge = lo;
+      dst = nS + (nF - F(ge)) + (F(t) - F(gs));
+    }
+    key[b + dst] = kt; perm[b + dst] = tPerm[o + t]; ts[b + dst] = tTs[o + t]; sm[b + dst] = tSm[o + t];
+  }
 }
 __global__ void k_grp_big_fields(const uint32_t* __restrict__ idx, uint32_t B, const uint32_t* __restrict__ perm,
                                  HeadsSoA h, uint32_t* __restrict__ tsOut, uint8_t* __restrict__ smOut) {
@@ -2137,6 +2232,12 @@ void mk_dm_el_emit(const ElemIn& w, uint32_t V, const unsigned long long* runIn,
                    hipStream_t st) {
   if (V) hipLaunchKernelGGL(k_dm_el_emit, g1(V), dim3(256), 0, st, elem_args(w), V, w.elemBase, runIn, symIn,
                             unitRunOff, unitSymOff, prevHL, unitHL, hl, runStart, runChar);
+}
+void mk_grp_big_maporder(const uint32_t* bpos, uint32_t nb, const uint32_t* hb, const uint32_t* off,
+                         unsigned long long* key, uint32_t* perm, uint32_t* ts, uint8_t* sm, unsigned long long* tKey,
+                         uint32_t* tPerm, uint32_t* tTs, uint8_t* tSm, uint32_t* tF, int bN, hipStream_t st) {
+  if (nb) hipLaunchKernelGGL(k_grp_big_maporder, dim3(nb), dim3(256), 0, st, bpos, nb, hb, off, key, perm, ts, sm, tKey,
+                             tPerm, tTs, tSm, tF, bN);
 }
 void mk_grp_seg(const uint32_t* posS, const uint32_t* hb, const HeadKV* kv, uint32_t H, int bN, int bL,
                 unsigned long long* key, uint32_t* perm, uint32_t* tsOut, uint8_t* smOut, uint32_t* bigList,

@@ -12,6 +12,11 @@ void mk_gather(const uint32_t* src, const uint32_t* perm, uint32_t* dst, uint64_
 void mk_item_flags(const uint32_t* perm, const HeadsSoA& h, uint32_t* flag, uint64_t H, hipStream_t st);
 void mk_group_key(const HeadsSoA& h, uint64_t H, int bN, int bL, unsigned long long* key, hipStream_t st);
 // grouping, position first (radix by pos, then per-position segments)
+// members of the big segments (bpos, offsets off in the big list) reordered
+// into map order; t* are temporaries of the big list's size
+void mk_grp_big_maporder(const uint32_t* bpos, uint32_t nb, const uint32_t* hb, const uint32_t* off,
+                         unsigned long long* key, uint32_t* perm, uint32_t* ts, uint8_t* sm, unsigned long long* tKey,
+                         uint32_t* tPerm, uint32_t* tTs, uint8_t* tSm, uint32_t* tF, int bN, hipStream_t st);
 void mk_grp_seg(const uint32_t* posS, const uint32_t* hb, const HeadKV* kv, uint32_t H, int bN, int bL,
                 unsigned long long* key, uint32_t* perm, uint32_t* tsOut, uint8_t* smOut, uint32_t* bigList,
                 uint32_t maxSmall, int32_t* diffEnds, uint32_t n, hipStream_t st);
