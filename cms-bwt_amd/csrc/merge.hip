@@ -94,6 +94,7 @@ __global__ void __launch_bounds__(256) k_grp_seg(const uint32_t* __restrict__ po
     if (pi == 0xffffffffu) continue;
     const int64_t sb = (int64_t)hb[pi] - base, se = (int64_t)hb[pi + 1] - base;
     if (se - sb > lim || sb < 0 || se > (int64_t)W) continue;
+    if (se <= (int64_t)kGrpHalo || sb >= (int64_t)(kGrpHalo + kGrpBlock)) continue;  // no owner in this block
     const unsigned long long me = lk[i];
     uint32_t f = i;
     for (int64_t j = (int64_t)i - 1; j >= sb; j--) f = lk[j] == me ? (uint32_t)j : f;

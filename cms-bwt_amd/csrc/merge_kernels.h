@@ -94,7 +94,8 @@ uint32_t sel_tiles(uint32_t n);
 void mk_sel_count(const uint32_t* flags, uint32_t n, uint32_t* tileCnt, hipStream_t st);
 void mk_sel_write(const uint32_t* in, const uint32_t* flags, uint32_t n, const uint32_t* tileOff, uint32_t* out,
                   hipStream_t st);
-// map order of each position's items (one thread per position)
+// map order of each position's items, one thread per position (the composite-key
+// grouping paths; the position-first grouping emits map order itself)
 void mk_map_order(const uint32_t* posBegin, const uint32_t* len, const uint8_t* sm, uint32_t n, uint32_t* order,
                   hipStream_t st);
 // per-group doubling round (small groups sorted by one thread each)
