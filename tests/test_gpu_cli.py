@@ -43,8 +43,9 @@ KEYS_SMALL.insert(KEYS_SMALL.index("ndoc: "), "uniqueHeadNumber: ")
 KEYS_SMALL.insert(KEYS_SMALL.index("counterBad: "), "capOfBufferSuffixes = ")
 
 
-def run_cli(args, cwd=None):
-    return subprocess.run([CLI] + args, capture_output=True, text=True, cwd=cwd, timeout=300)
+def run_cli(args, cwd=None, env=None):
+    e = dict(os.environ, **env) if env else None
+    return subprocess.run([CLI] + args, capture_output=True, text=True, cwd=cwd, timeout=300, env=e)
 
 
 def parse_log(path, keys):
@@ -125,6 +126,23 @@ def test_cli_config1_both_formats_and_log(built, oracle, tmp_path):
     assert os.path.getsize(pre + ".list.bwt") == g["bwt_bytes"]
     assert sha(pre + ".list.bwt") == g["bwt_sha256"]
     assert os.path.exists(pre + ".list.log")
+
+
+@pytest.mark.parametrize("env", [{"CMSBWT_OVERLAP_UPLOAD": "0"}, {"CMSBWT_HOST_READER": "1"}],
+                         ids=["upload_after_index", "host_reader"])
+def test_cli_ingest_paths_golden(built, tmp_path, env):
+    """`cmsbwt_run` streams the collection into HBM while the reference index
+    is built (default); the upload after the index (CMSBWT_OVERLAP_UPLOAD=0)
+    and the host getline reader (FN:1138-1147) give the same golden .rl_bwt
+    and headNumber on config 1."""
+    g = json.load(open(os.path.join(GOLD, "golden.json")))["c1"]
+    pre = str(tmp_path / "c1")
+    _gen_np().gen(1_000_000, 10, 0.001, 11, pre)
+    r = run_cli(["-r", "-o", pre + "_r", pre + ".list"], env=env)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert sha(pre + "_r.rl_bwt") == g["rl_bwt_sha256"]
+    v = parse_log(pre + "_r.log", KEYS_LARGE)
+    assert num(v["headNumber: "]) == g["headNumber"]
 
 
 def test_cli_config2_golden(built, tmp_path):
