@@ -51,9 +51,12 @@ def synth_reference(L: int, seed: int) -> bytes:
     return np.frombuffer(b"ACGT", dtype=np.uint8)[(h >> np.uint64(62)).astype(np.int64)].tobytes()
 
 
-def cpu_baseline(ref_len, copies, p, seed, rle=True):
+def cpu_baseline(ref_len, copies, p, seed, rle=True, full_copies=None):
     """Oracle (single-threaded CPU restatement) on a bounded sample of the same
-    workload, collection stage only (parse .. .rl_bwt closed)."""
+    workload, collection stage only (parse .. .rl_bwt closed).  The counter
+    phase grows with the copy count, so a short sample overstates the CPU's
+    rate: the oracle's own full-size run of this workload (timed once in the
+    build container, tests/golden/golden.json) is reported beside it."""
     import oracle_lib
     gen = oracle_lib.GEN
     with tempfile.TemporaryDirectory() as td:
@@ -63,10 +66,17 @@ def cpu_baseline(ref_len, copies, p, seed, rle=True):
         if rc:
             raise RuntimeError(f"oracle rc={rc}")
     chars = ref_len * copies
-    return {"value": round(chars / 1e6 / t_coll, 3), "unit": "MB/s", "cores": 1, "kind": "port",
-            "sample": f"{ref_len // 10**6} MB ref + {copies} copies @{p * 100:g}% ({chars / 1e6:.0f} MB collection), "
-                      f"oracle collection stage {t_coll:.2f} s, index {t_idx:.2f} s excluded",
-            "seconds": round(t_coll, 3)}
+    out = {"value": round(chars / 1e6 / t_coll, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+           "sample": f"{ref_len // 10**6} MB ref + {copies} copies @{p * 100:g}% ({chars / 1e6:.0f} MB collection), "
+                     f"oracle collection stage {t_coll:.2f} s, index {t_idx:.2f} s excluded",
+           "seconds": round(t_coll, 3)}
+    full = golden_entry(ref_len, full_copies, p, seed) if full_copies else None
+    if full and full.get("oracle_collection_seconds"):
+        fs = full["oracle_collection_seconds"]
+        out["full_size"] = {"value": round(ref_len * full_copies / 1e6 / fs, 3), "unit": "MB/s", "seconds": fs,
+                            "cores": 1, "sample": f"the whole workload ({full_copies} copies), oracle collection "
+                                                  "stage, timed once in the build container (tests/golden/golden.json)"}
+    return out
 
 
 PMC_FILE = "r03_pmc.json"  # tools/gpu_prof_r.sh + tools/pmc_summary.py (this round's kernels)
@@ -108,17 +118,47 @@ def pmc_traffic(args, kernel="k_ms_walk2"):
         return None, None
 
 
-def golden_for(args, rle):
-    """The oracle's sha256 for this exact workload, when committed."""
+def golden_entry(ref_len, copies, p, seed):
+    """The oracle's committed results for this exact synth.h workload, if any."""
     try:
         g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))
     except (OSError, ValueError):
         return None
     for k, v in g.items():
-        if isinstance(v, dict) and v.get("generator") == "synth.h" and \
-                v.get("args") == [args.ref_len, args.copies, args.p, args.seed]:
-            return v.get("rl_bwt_sha256" if rle else "bwt_sha256")
+        if isinstance(v, dict) and v.get("generator") == "synth.h" and v.get("args") == [ref_len, copies, p, seed]:
+            return v
     return None
+
+
+def golden_for(args, rle):
+    """The oracle's sha256 for this exact workload, when committed."""
+    v = golden_entry(args.ref_len, args.copies, args.p, args.seed)
+    return v.get("rl_bwt_sha256" if rle else "bwt_sha256") if v else None
+
+
+def parity_check(eng, args, rle):
+    """sha256 of the runs of the last timed step (rank 0 holds them) and the
+    global statistics, against the oracle's golden for this workload."""
+    import hashlib
+    st = eng.stats()
+    out = {"heads": st.heads, "keys": st.keys, "rank": st.rank, "runs": st.runs,
+           "counter_bad": st.counter_bad, "counter_good": st.counter_good, "counter_nothing": st.counter_nothing}
+    if not rle:
+        out["verdict"] = "not checked (plain runs; the golden holds the expanded .bwt)"
+        return out
+    sha = hashlib.sha256(eng.runs_bytes()).hexdigest()
+    out["rl_bwt_sha256"] = sha[:16]
+    g = golden_entry(args.ref_len, args.copies, args.p, args.seed)
+    if not g:
+        out["verdict"] = "no golden for this workload"
+        return out
+    want = {"heads": g["headNumber"], "keys": g["keys"], "rank": g["Rank"], "runs": g["rl_runs"],
+            "counter_bad": g["counterBad"], "counter_good": g["counterGood"], "counter_nothing": g["counterDoNothing"]}
+    bad = [k for k, v in want.items() if out[k] != v]
+    if sha != g["rl_bwt_sha256"]:
+        bad.append("rl_bwt_sha256")
+    out["verdict"] = "bit-exact vs oracle golden" if not bad else "MISMATCH vs oracle golden: " + ",".join(bad)
+    return out
 
 
 def _sha256_file(path):
@@ -184,6 +224,7 @@ def main():
     ap.add_argument("--cpu-copies", type=int, default=30)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-e2e", action="store_true", help="skip the end-to-end CLI leg (Metric 1)")
+    ap.add_argument("--no-check", action="store_true", help="skip the sha256 check of the last step's runs")
     ap.add_argument("--e2e-reps", type=int, default=3)
     ap.add_argument("--plain", action="store_true",
                     help="plain .bwt instead of .rl_bwt (BASELINE config 5 runs without -r)")
@@ -219,14 +260,27 @@ def main():
     xfer = cdist.Transport(device) if (world > 1 or mode == "sharded1") else None
 
     rle = not args.plain
+    # per-step stage wall times of this rank (N > 1: walk, then the sharded
+    # or gathered merge) and the walk statistics of this rank's shard
+    stage = {"walk": 0.0, "merge": 0.0, "n": 0}
+    walk_local = {}
 
     def step():
         if world == 1 and mode != "sharded1":
             eng.step(rle=rle)
-        elif gather:  # all heads to rank 0, single-GPU merge there
-            cdist.gather_step(eng, device, rle=rle)
+            return
+        t0 = time.perf_counter()
+        eng.ms_walk()  # synchronous: ends with the engine stream drained
+        t1 = time.perf_counter()
+        w = eng.stats()
+        walk_local.update(heads=w.heads, chars=w.chars, kernel_ms=w.ms_walk_kernel_ms)
+        if gather:    # all heads to rank 0, single-GPU merge there
+            cdist.gather_merge(eng, device, rle=rle)
         else:         # merge sharded by reference position (dist_merge.hip)
-            cdist.sharded_step(eng, device, rle=rle, xfer=xfer)
+            cdist.sharded_merge(eng, xfer, rle)
+        stage["walk"] += t1 - t0
+        stage["merge"] += time.perf_counter() - t1
+        stage["n"] += 1
 
     def barrier():
         torch.cuda.synchronize(local)
@@ -236,32 +290,45 @@ def main():
     for _ in range(args.warmup):
         step()
     barrier()
+    stage.update(walk=0.0, merge=0.0, n=0)
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
     barrier()
     dt = time.perf_counter() - t0
-    if dist:
-        t = torch.tensor([dt], device="cpu" if same_gpu else f"cuda:{local}", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = float(t.item())
     st = eng.stats()
-    if world > 1:  # walk statistics of rank 0's shard; merge statistics are global on rank 0
-        st_walk_chars = args.ref_len * (c1 - c0)
+    if world == 1 and mode != "sharded1":
+        walk_local.update(heads=st.heads, chars=st.chars, kernel_ms=st.ms_walk_kernel_ms)
+        stage.update(walk=st.t_ms_walk_s * args.steps, merge=st.t_merge_s * args.steps, n=args.steps)
+    ns = max(1, stage["n"])
+    # per rank: [step time, walk stage, merge stage, walk kernel] -> max over
+    # ranks; the walk roofline below is that of the slowest rank's kernel
+    # (algorithmic bytes of the rank whose kernel was slowest)
+    mine = [dt, stage["walk"] / ns, stage["merge"] / ns, walk_local["kernel_ms"],
+            float(walk_local["heads"]), float(walk_local["chars"]), float(st.device_peak_bytes)]
+    if dist:
+        t = torch.tensor(mine, device="cpu" if same_gpu else f"cuda:{local}", dtype=torch.float64)
+        allt = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(allt, t)
+        rows = [[float(v) for v in x.cpu().tolist()] for x in allt]
     else:
-        st_walk_chars = st.chars
+        rows = [mine]
+    dt = max(r[0] for r in rows)
+    slow = max(rows, key=lambda r: r[3])
     chars_total = args.ref_len * args.copies
     ms_step = dt / args.steps * 1e3
     value = chars_total / 1e6 / (dt / args.steps)
 
     # Roofline of the dominant kernel, the MS walk: algorithmic bytes of this
     # algorithm (WALK_B_PER_*) over its HIP-event duration (last step, on the
-    # engine's stream, where the kernel is launched)
-    n_local = st_walk_chars
-    heads_local = st.heads if world == 1 else int(st.heads * (c1 - c0) / max(1, args.copies))
+    # engine's stream, where the kernel is launched); N > 1: the slowest rank
+    n_local, heads_local = int(slow[5]), int(slow[4])
     b_alg = WALK_B_PER_CHAR * n_local + WALK_B_PER_HEAD * heads_local
     b_survey = SURVEY_B_PER_CHAR * n_local + SURVEY_B_PER_HEAD * heads_local
-    t_ms = st.ms_walk_kernel_ms / 1e3
+    # compulsory HBM bytes if the 10 MB reference and every table stayed in
+    # the caches: each text byte read once + each 16-B head record written
+    b_floor = n_local + 16 * heads_local
+    t_ms = slow[3] / 1e3
     achieved = b_alg / t_ms / 1e9 if t_ms > 0 else 0.0
     traffic, traffic_src = pmc_traffic(args) if world == 1 else (None, None)
     ctraffic, _ = pmc_traffic(args, "k_counter_tgt") if world == 1 else (None, None)
@@ -291,6 +358,10 @@ def main():
                                     "DESIGN.md §3.1",
                      "traffic_over_algorithmic": round(traffic / b_alg, 2) if traffic else None,
                      "traffic_GBps": round(traffic / t_ms / 1e9, 1) if traffic and t_ms > 0 else None,
+                     "hbm_floor_bytes": b_floor,
+                     "frac_hbm_floor": round(b_floor / t_ms / 1e9 / HBM_PEAK_GBS, 4) if t_ms > 0 else None,
+                     "hbm_floor_model": "1 B/char (text read once) + 16 B/head (record written): reference "
+                                        "and tables assumed cache-resident",
                      "frac_survey_model": round(b_survey / t_ms / 1e9 / HBM_PEAK_GBS, 4) if t_ms > 0 else None,
                      "survey_model": "22 B/char + 24 B/head (SURVEY.md §8d: the reference's per-character "
                                      "streams; exceeds 1 because this walk does not perform them)"},
@@ -300,10 +371,23 @@ def main():
                            "queries": int(st.counter_good + st.counter_bad + st.counter_nothing),
                            "traffic": ctraffic,
                            "traffic_GBps": round(ctraffic / (c_ms / 1e3) / 1e9, 1) if ctraffic and c_ms > 0 else None},
-        "stages_ms": {"ms_walk": round(st.t_ms_walk_s * 1e3, 2), "merge": round(st.t_merge_s * 1e3, 2),
-                      "ms_walk_kernel": round(st.ms_walk_kernel_ms, 2),
-                      "counter_kernel": round(st.counter_kernel_ms, 2)},
+        "stages_ms": {"ms_walk": round(max(r[1] for r in rows) * 1e3, 2),
+                      "merge": round(max(r[2] for r in rows) * 1e3, 2),
+                      "ms_walk_kernel": round(max(r[3] for r in rows), 2),
+                      "counter_kernel": round(st.counter_kernel_ms, 2),
+                      "note": "per step; N > 1: max over ranks of each rank's stage wall time"},
+        "hbm_peak_gib": round(max(r[6] for r in rows) / 2**30, 2),
     }
+    if world > 1:
+        out["per_rank"] = [{"step_ms": round(r[0] / args.steps * 1e3, 2), "walk_ms": round(r[1] * 1e3, 2),
+                            "merge_ms": round(r[2] * 1e3, 2), "walk_kernel_ms": round(r[3], 2),
+                            "heads": int(r[4]), "chars": int(r[5]), "hbm_peak_gib": round(r[6] / 2**30, 2)}
+                           for r in rows]
+    if rank == 0 and not args.no_check:
+        try:
+            out["parity"] = parity_check(eng, args, rle)
+        except Exception as e:  # reported, never fatal for the GPU number
+            out["parity"] = {"error": str(e)[-400:]}
     eng.close()
     if rank == 0 and world == 1 and not args.no_e2e:
         try:
@@ -312,7 +396,8 @@ def main():
             out["e2e"] = {"error": str(e)[-400:]}
     if rank == 0 and not args.no_cpu:
         try:
-            out["cpu_baseline"] = cpu_baseline(args.ref_len, args.cpu_copies, args.p, args.seed, rle=rle)
+            out["cpu_baseline"] = cpu_baseline(args.ref_len, args.cpu_copies, args.p, args.seed, rle=rle,
+                                               full_copies=args.copies)
         except Exception as e:  # reported, never fatal for the GPU number
             out["cpu_baseline"] = {"error": str(e)}
     if rank == 0:

@@ -33,6 +33,8 @@ CMSBWT_EDEVICE = 4
 CMSBWT_ELIMIT = 5
 CMSBWT_EORDER = 6
 CMSBWT_EINTERNAL = 7
+CMSBWT_BACKEND_PEER = 0
+CMSBWT_BACKEND_RCCL = 1
 UINT64_MAX = (1 << 64) - 1
 
 ARRAYS = {  # name -> numpy dtype, as dumped by the oracle
@@ -56,7 +58,8 @@ class CmsBwtError(RuntimeError):
 
 class _Args(ctypes.Structure):
     _fields_ = [("prefix", ctypes.c_uint64), ("buffer_gb", ctypes.c_uint32), ("rle", ctypes.c_int32),
-                ("outname", ctypes.c_char_p), ("device", ctypes.c_int32), ("verbose", ctypes.c_int32)]
+                ("outname", ctypes.c_char_p), ("device", ctypes.c_int32), ("verbose", ctypes.c_int32),
+                ("n_gpus", ctypes.c_int32), ("backend", ctypes.c_int32)]
 
 
 class Stats(ctypes.Structure):
@@ -70,7 +73,7 @@ class Stats(ctypes.Structure):
         [(k, ctypes.c_int64) for k in ("first_rank_to_head", "last_rank_to_head")] + \
         [(k, ctypes.c_double) for k in ("t_augment_ms", "t_sa_ms", "t_isa_ms", "t_lcp_ms", "t_rmq_ms", "t_bwt_ms",
                                         "t_ranks_ms", "t_libsais_int_ms", "t_counter_ms")] + \
-        [("host_queries", ctypes.c_uint64)]
+        [("host_queries", ctypes.c_uint64), ("device_peak_bytes", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -178,6 +181,8 @@ class Args:
     prefixLength: int = UINT64_MAX  # -p
     device: int = 0
     verbose: bool = False
+    n_gpus: int = 1               # ranks in this process (include/cmsbwt.h cmsbwt_args)
+    backend: str = "peer"         # multi-GPU transport: "peer" | "rccl"
 
 
 def computeBWT(arg: Args, refFileName: str, collFileName: str) -> Stats:
@@ -187,7 +192,8 @@ def computeBWT(arg: Args, refFileName: str, collFileName: str) -> Stats:
     lib = load_library()
     out = arg.outname or arg.filename
     a = _Args(arg.prefixLength, arg.buffer, 1 if arg.format else 0, out.encode(), arg.device,
-              1 if arg.verbose else 0)
+              1 if arg.verbose else 0, arg.n_gpus,
+              CMSBWT_BACKEND_RCCL if arg.backend == "rccl" else CMSBWT_BACKEND_PEER)
     st = Stats()
     rc = lib.cmsbwt_run(ctypes.byref(a), refFileName.encode(), collFileName.encode(), ctypes.byref(st))
     if rc != CMSBWT_OK:

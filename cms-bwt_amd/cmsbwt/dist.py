@@ -105,6 +105,11 @@ def import_walk(eng, combined: dict, totals):
 def gather_step(eng, device, rle: bool = True, root: int = 0):
     """One distributed step: local walk, gather, merge on root."""
     eng.ms_walk()
+    return gather_merge(eng, device, rle, root)
+
+
+def gather_merge(eng, device, rle: bool = True, root: int = 0):
+    """The merge of gather_step after this rank's walk: gather, merge on root."""
     st = eng.stats()
     local = export_walk(eng, device)
     combined, totals = gather_walk(local, (st.heads, st.ndocs, st.chars, st.order_invariant), device, root)

@@ -2,7 +2,10 @@
 // main.cpp:14-132: same getopt surface ("p:b:o:rh"), same two-line list file,
 // same outputs (<base>.rl_bwt | <base>.bwt, <base>.log, and
 // <base>.counterSmallerThanHead_true for references below 1e6 symbols).
-// Extra flags: -g <device> selects the HIP device, -v prints stage times.
+// Extra flags: -g <device> selects the HIP device (rank 0's with -n),
+// -n <gpus> runs on that many GPUs in this process (SURVEY.md §8(b) n_gpus;
+// ranks wrap over the devices, so -n 4 on one GPU runs four ranks on it),
+// -t peer|rccl picks the multi-GPU transport, -v prints stage times.
 #include <getopt.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -26,6 +29,8 @@ static void print_help(char** argv) {  // main.cpp:14-24
             << "\t-r \toutputs the run-length encoded BWT, def. false " << std::endl
             << "\t-o \tbasename for the output files, def. <input filename>" << std::endl
             << "\t-g \tHIP device ordinal, def. 0" << std::endl
+            << "\t-n \tnumber of GPUs (ranks in this process), def. 1" << std::endl
+            << "\t-t \tmulti-GPU transport: peer (HBM pulls over xGMI) or rccl, def. peer" << std::endl
             << "\t-v \tprint stage timings" << std::endl
             << "\t-h \tprints this help" << std::endl;
   exit(-1);
@@ -35,12 +40,12 @@ int main(int argc, char** argv) {
   std::string filename, outname;
   unsigned long long prefix = UINT64_MAX;
   unsigned buffer = 2;
-  int rle = 0, device = 0, verbose = 0;
+  int rle = 0, device = 0, verbose = 0, ngpus = 1, backend = CMSBWT_BACKEND_PEER;
   puts("==== Command line:");
   for (int i = 0; i < argc; i++) printf(" %s", argv[i]);
   puts("");
   int c;
-  while ((c = getopt(argc, argv, "p:b:o:rhg:v")) != -1) {
+  while ((c = getopt(argc, argv, "p:b:o:rhg:vn:t:")) != -1) {
     switch (c) {
       case 'p': prefix = strtoull(optarg, nullptr, 10); break;
       case 'b': buffer = (unsigned)atoi(optarg); break;
@@ -48,6 +53,12 @@ int main(int argc, char** argv) {
       case 'o': outname = optarg; break;
       case 'g': device = atoi(optarg); break;
       case 'v': verbose = 1; break;
+      case 'n': ngpus = atoi(optarg); break;
+      case 't':
+        if (std::string(optarg) == "rccl") backend = CMSBWT_BACKEND_RCCL;
+        else if (std::string(optarg) == "peer") backend = CMSBWT_BACKEND_PEER;
+        else { std::cout << "Unknown transport " << optarg << ". Use -h for help." << std::endl; exit(-1); }
+        break;
       case 'h': print_help(argv); break;
       default: std::cout << "Unknown option. Use -h for help." << std::endl; exit(-1);
     }
@@ -55,6 +66,7 @@ int main(int argc, char** argv) {
   if (argc == optind + 1) filename = argv[optind];
   else { std::cout << "Invalid number of arguments" << std::endl; print_help(argv); }
   if (outname.empty()) outname = filename;
+  if (ngpus < 1 || ngpus > 64) { std::cout << "Invalid number of GPUs " << ngpus << std::endl; exit(-1); }
   std::cout << "==== Parameters:" << std::endl;
   std::cout << "Input file: " << filename << std::endl;
   std::cout << "Output basename: " << outname << std::endl;
@@ -80,7 +92,7 @@ int main(int argc, char** argv) {
   std::cout << "==== For more information about the execution, please check the log file: " << outname + ".log"
             << std::endl;
   std::cout << "==== Processing reference sequence" << std::endl;
-  cmsbwt_args a{prefix, buffer, rle, outname.c_str(), device, verbose};
+  cmsbwt_args a{prefix, buffer, rle, outname.c_str(), device, verbose, ngpus, backend};
   cmsbwt_stats s{};
   int rc = cmsbwt_run(&a, ref.c_str(), coll.c_str(), &s);
   if (rc != CMSBWT_OK) {

@@ -250,6 +250,7 @@ struct Engine {
   std::vector<uint64_t> hdoc;  // doc offsets (ndocs+1), doc k = [hdoc[k], hdoc[k+1]-1)
   uint64_t ndocs = 0, chars = 0, sn = 0;
   uint64_t collChars = 0;  // chars of the loaded collection (ms_walk input)
+  bool collTail = false;   // the device reader closed a tail document (FN:1269-1275)
 
   // ---- walk outputs
   bool walked = false;
@@ -289,7 +290,8 @@ struct Engine {
   }
   ~Engine() {
     g_alloc = &alloc;
-    if (pend.on) {  // a collection upload still streaming into HBM
+    if (pend.on) {  // a collection upload still streaming into HBM: stop it
+      pend.cancel = true;
       pend.th.join();
       pend.on = false;
     }
@@ -957,8 +959,9 @@ struct Engine {
 
   // pread of the file into pinned buffers by `nt` threads, each DMAing its
   // chunks to dst on its own stream (double-buffered: reading chunk c+2T
-  // overlaps the copy of chunk c).
-  void stream_file(int fd, uint64_t base, uint64_t fsz, uint8_t* dst) {
+  // overlaps the copy of chunk c).  `cancel` (optional) stops the readers
+  // between chunks; the call then returns with dst partly written.
+  void stream_file(int fd, uint64_t base, uint64_t fsz, uint8_t* dst, const std::atomic<bool>* cancel = nullptr) {
     const uint32_t nt = std::max(1u, std::min(64u, env_u32("CMSBWT_READ_THREADS", 8)));
     ensure_pinned(nt, (uint64_t)std::max(1u, env_u32("CMSBWT_READ_CHUNK_MB", 32)) << 20);
     const uint64_t CH = pinnedBytes;
@@ -975,7 +978,7 @@ struct Engine {
             ok(hipEventCreateWithFlags(&ev[0], hipEventDisableTiming)) &&
             ok(hipEventCreateWithFlags(&ev[1], hipEventDisableTiming))) {
           uint32_t it = 0;
-          for (uint64_t c = k; c < nch && !err; c += nt, it++) {
+          for (uint64_t c = k; c < nch && !err && !(cancel && cancel->load()); c += nt, it++) {
             const int j = it & 1;
             uint8_t* buf = (uint8_t*)pinned[2 * k + j];
             if (used[j] && !ok(hipEventSynchronize(ev[j]))) break;
@@ -1012,6 +1015,7 @@ struct Engine {
     DBuf<uint8_t> raw;
     std::thread th;
     std::exception_ptr err;
+    std::atomic<bool> cancel{false};
   } pend;
   void upload_file_begin(const std::string& path) {
     upload_file_end(false);
@@ -1027,19 +1031,22 @@ struct Engine {
     pend.path = path;
     pend.fsz = fsz;
     pend.err = nullptr;
+    pend.cancel = false;
     uint8_t* dst = pend.raw.p;
     pend.th = std::thread([this, fd, fsz, dst] {
       try {
-        stream_file(fd, 0, fsz, dst);
+        stream_file(fd, 0, fsz, dst, &pend.cancel);
       } catch (...) {
         pend.err = std::current_exception();
       }
       close(fd);
     });
   }
-  // Wait for a pending upload; with take, hand its buffer over (else drop it).
+  // Wait for a pending upload; with take, hand its buffer over (else stop the
+  // readers between chunks and drop it).
   bool upload_file_end(bool take, const std::string& path = "", DBuf<uint8_t>* raw = nullptr, uint64_t* fsz = nullptr) {
     if (!pend.on) return false;
+    if (!take || path != pend.path) pend.cancel = true;
     pend.th.join();
     pend.on = false;
     const bool match = take && path == pend.path;
@@ -1065,6 +1072,9 @@ struct Engine {
     DBuf<uint8_t> raw;
     uint64_t fsz = 0;
     const bool whole = fileOff == 0 && sliceLen == ~0ull;
+    // a pending whole-file upload of another path (or a byte range of this
+    // one) must stop before this call's readers use the same pinned buffers
+    if (!whole) upload_file_end(false);
     if (!(whole && upload_file_end(true, path, &raw, &fsz))) {
       int fd = open(path.c_str(), O_RDONLY);
       if (fd < 0) throw InputError{CMSBWT_EIO, "Error opening file of sequence (" + path + ")"};
@@ -1120,7 +1130,8 @@ struct Engine {
     HIPCHK(hipMemcpyAsync(off.data(), ddoc.p, (nsep + 1) * 8, hipMemcpyDeviceToHost, st));
     const unsigned long long badv = read1(bad.p);
     uint64_t size = total, sn = fsz;
-    if (total > off[nsep]) {  // tail document (FN:1269-1275)
+    collTail = total > off[nsep];
+    if (collTail) {  // tail document (FN:1269-1275)
       const uint64_t e = total + 1;
       HIPCHK(hipMemsetAsync(dtext.p + total, kSep, 1, st));
       off.push_back(e);
@@ -2005,8 +2016,11 @@ struct Engine {
     unsigned long long cs[8];
     uint64_t queryViol = 0;
     HIPCHK(hipMemcpyAsync(&W, wsum.p, 8, hipMemcpyDeviceToHost, st));
+    double tCheckedMs = -1;  // checked path: device passes + host replay queries, wall time
     if (check) {
+      const auto tc = std::chrono::steady_clock::now();
       queryViol = counter_checked(IS, h, nhr, hostMask, cstats, n, cs);
+      tCheckedMs = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - tc).count();
     } else {
       HIPCHK(hipMemcpyAsync(cs, cstats.p, sizeof(cs), hipMemcpyDeviceToHost, st));
       sync();
@@ -2122,7 +2136,7 @@ struct Engine {
       HIPCHK(hipEventElapsedTime(&c, evm[4], evm[5]));
       stats.t_ranks_ms = a;
       stats.t_libsais_int_ms = b;
-      stats.t_counter_ms = c;
+      stats.t_counter_ms = tCheckedMs >= 0 ? tCheckedMs : c;
     }
     stats.t_merge_s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
   }
@@ -2490,3 +2504,9 @@ struct Engine {
 };
 
 }  // namespace cmsbwt
+
+// The C ABI's context (engine.hip): one engine and its last error message.
+struct cmsbwt_ctx {
+  cmsbwt::Engine* e = nullptr;
+  std::string err;
+};

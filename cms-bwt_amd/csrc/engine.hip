@@ -1,15 +1,67 @@
 // engine.hip — the C ABI of include/cmsbwt.h over cmsbwt::Engine (engine.h).
 #include "engine.h"
+#include "run_log.h"
+#include "ctx_view.h"
+
+// ---- ctx_view.h: the multi-GPU driver's view of a rank's engine
+namespace cmsbwt {
+CtxView ctx_view(const cmsbwt_ctx* c) {
+  const Engine& e = *c->e;
+  CtxView v;
+  v.device = e.device;
+  v.st = e.st;
+  v.n = e.R.n;
+  v.H = e.H;
+  v.ndocs = e.ndocs;
+  v.chars = e.chars;
+  v.sn = e.sn;
+  v.collTail = e.collTail;
+  v.orderInvariant = e.orderInvariant;
+  const void* h[8] = {e.hStart.p, e.hPos.p, e.hLen.p, e.hSmall.p, e.hChar.p, e.hIsa.p, e.hTonext.p, e.hNext.p};
+  for (int k = 0; k < 8; k++) v.heads[k] = h[k];
+  v.diff = e.diff.p;
+  v.hasHead = e.hasHead.p;
+  v.dmItems = e.dm.IS.K;
+  v.dmItemPos = e.dm.IS.pos.p;
+  v.dmGrp = e.dm.grp.p;
+  v.dmU = e.dm.U;
+  v.stats = e.stats;
+  v.devicePeak = e.alloc.peak;
+  return v;
+}
+void* ctx_alloc(cmsbwt_ctx* c, uint64_t bytes) {
+  g_alloc = &c->e->alloc;
+  (void)hipSetDevice(c->e->device);
+  try {
+    return c->e->alloc.get(std::max<uint64_t>(bytes, 1));
+  } catch (const HipError& he) {
+    throw CtxError{CMSBWT_EDEVICE, he.msg};
+  }
+}
+void ctx_free(cmsbwt_ctx* c, void* p) {
+  if (p) c->e->alloc.put(p);
+}
+uint64_t ctx_count_distinct(cmsbwt_ctx* c, const uint32_t* v, uint32_t k) {
+  if (!k) return 0;
+  Engine& e = *c->e;
+  g_alloc = &e.alloc;
+  try {
+    DBuf<unsigned long long> r;
+    r.alloc(1);
+    r.zero(e.st);
+    mk_count_distinct(v, k, r.p, e.st);
+    return e.read1(r.p);
+  } catch (const HipError& he) {
+    throw CtxError{CMSBWT_EDEVICE, he.msg};
+  }
+}
+}  // namespace cmsbwt
 
 // =========================================================================
 // C ABI
 using cmsbwt::Engine;
 using cmsbwt::HipError;
 
-struct cmsbwt_ctx {
-  Engine* e = nullptr;
-  std::string err;
-};
 
 template <class F>
 static int guard(cmsbwt_ctx* c, F&& f) {
@@ -175,6 +227,7 @@ int cmsbwt_walk_import(cmsbwt_ctx* ctx, uint64_t heads, uint64_t ndocs, uint64_t
 int cmsbwt_get_stats(const cmsbwt_ctx* ctx, cmsbwt_stats* out) {
   if (!ctx || !out) return CMSBWT_EARG;
   *out = ctx->e->stats;
+  out->device_peak_bytes = ctx->e->alloc.peak;
   return CMSBWT_OK;
 }
 
@@ -286,6 +339,7 @@ int cmsbwt_host_suffix_array(const uint8_t* s, uint64_t n, int32_t* sa_out) {
 // small-reference collection pass (FN:1093-1628 / FN:312-936) and a writer.
 int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path, cmsbwt_stats* stats_out) {
   if (!a || !ref_path || !coll_path || !a->outname) return CMSBWT_EARG;
+  if (a->n_gpus > 1) return cmsbwt::run_multi(a, ref_path, coll_path, stats_out);  // multi.hip
   std::string out = a->outname;
   std::ofstream log(out + ".log");
   cmsbwt_ctx* ctx = nullptr;
@@ -334,6 +388,15 @@ int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path
     }
   }
   rc = cmsbwt_load_reference_file(ctx, ref_path);
+  if (rc == CMSBWT_EDEVICE && e.pend.on) {
+    // the index did not fit beside the collection's raw bytes: stop the
+    // overlapped upload, free its buffer and build the index alone (the
+    // collection is then read after it, as without the overlap)
+    e.upload_file_end(false);
+    cmsbwt::g_alloc = &e.alloc;
+    e.alloc.trim();
+    rc = cmsbwt_load_reference_file(ctx, ref_path);
+  }
   if (rc) {
     if (e.hix.file_bytes) log << "n = " << e.hix.file_bytes << '\n';
     return fail(rc);
@@ -343,64 +406,21 @@ int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path
     struct stat sb;
     return stat(coll_path, &sb) == 0 ? (uint64_t)sb.st_size : ~0ull;
   }();
-  log << "n = " << s.ref_file_bytes << '\n';
-  log << "Reference (size = " << s.ref_read_size << "):\n\t";
-  if (sn0 == ~0ull) {
-    log << "Error opening file of sequence (" << coll_path << ")\n";
+  if (cmsbwt::log_reference(log, s, sn0, a->prefix, coll_path, ms(t0, now()))) {
     cmsbwt_ctx_destroy(ctx);
     return CMSBWT_EIO;
   }
-  log << "ftello(infile): " << sn0 << '\n';
-  log << "sn: " << std::min<uint64_t>(sn0, a->prefix) << '\n';
-  log << "Augmenting reference done in " << (long long)s.t_augment_ms << " ms\n";
-  log << "Computing SA done in " << (long long)s.t_sa_ms << " ms\n";
-  log << "\tComputing ISA..." << '\n';
-  log << "Computing ISA done in " << (long long)s.t_isa_ms << " ms\n";
-  log << "Computing LCP and PLCP done in " << (long long)s.t_lcp_ms << " ms\n";
-  log << "Computing RMQ...\n";
-  log << "Computing RMQ done in " << (long long)s.t_rmq_ms << " ms\n";
-  log << "Computing BWT...\n";
-  log << "Computing BWT done in " << (long long)s.t_bwt_ms << " ms\n";
-  log << "Finished pre-processing\n";
-  log << "Preprocessing done in " << ms(t0, now()) << " ms\n";
   auto t1 = now();
   rc = cmsbwt_load_collection_file(ctx, coll_path, a->prefix);
   if (rc) return fail(rc);
   const bool small = e.R.n < 1000000;  // FN:1792: small-reference path below 1e6
-  log << "File is in memory\n";
-  log << "_x.len: " << e.R.n << '\n';
-  log << "_sx.len: " << s.sn_initial << '\n';
-  log << "About to start main parsing loop...\n";
+  cmsbwt::log_collection_start(log, s, e.R.n);
   rc = cmsbwt_ms_walk(ctx);
   if (rc) return fail(rc);
   log << "Finished parsing file of length: " << e.sn << "\n";
   rc = cmsbwt_merge(ctx, a->rle ? 1 : 0);
   if (rc) return fail(rc);
-  if (!small) log << "phrasesSet.size(): " << s.positions << "\n";
-  log << "headNumber: " << s.heads << "\n";
-  if (small) log << "uniqueHeadNumber: " << s.keys << "\n";
-  log << "ndoc: " << s.ndocs + 1 << "\n";
-  log << "docBoundaries.size(): " << s.ndocs + 1 << "\n";
-  log << "Time to compute matching statistics: " << (long long)(s.t_ms_walk_s * 1000) << " milliseconds\n";
-  log << "Going to compute ranks for positions\n";
-  if (!small) log << "Rank: " << s.rank << "\n";
-  log << "libsais_int ran in " << (long long)s.t_libsais_int_ms << " milliseconds\n";
-  log << "First rankToHead: " << s.first_rank_to_head << "\n";
-  log << "Last rankToHead: " << s.last_rank_to_head << "\n";
-  log << "Done computing ranks for positions in " << (long long)s.t_ranks_ms << " milliseconds\n";
-  log << "currentSum: " << s.current_sum << "\n";
-  log << "Going to compute counterSmallerThanHead for positions\n";
-  if (small) {  // FN:713-727: the -b buffer of the small path (unsigned int GB * 2^30, wrapping)
-    const uint32_t cap32 = a->buffer_gb * 1073741824u;
-    const double ram = e.sn < (uint64_t)cap32 ? (double)e.sn : (double)cap32;
-    log << "capOfBufferSuffixes = " << (uint64_t)(ram / 20.0 + 1) << "\n";
-  }
-  log << "counterBad: " << s.counter_bad << "\n";
-  log << "counterGood: " << s.counter_good << "\n";
-  log << "counterDoNothing: " << s.counter_nothing << "\n";
-  log << "Done computing counterSmallerThanHead for positions in " << (long long)s.t_counter_ms
-      << " milliseconds\n";
-  log << "Inverted data in bucketsForExpandedBWT\n";
+  cmsbwt::log_collection_end(log, s, small, e.sn, a->buffer_gb);
   rc = cmsbwt_write_output(ctx, out.c_str(), a->rle ? 1 : 0);
   if (rc) return fail(rc);
   log << "MS-walk kernel: " << s.ms_walk_kernel_ms << " ms; collection pass: " << ms(t1, now()) << " ms\n";

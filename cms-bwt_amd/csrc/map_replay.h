@@ -122,18 +122,20 @@ inline HostQueryOut host_queries(const HostItems& I, const std::vector<uint32_t>
   HostQueryOut o;
   *layoutMismatch = false;
   std::sort(q.begin(), q.end(), [](const auto& a, const auto& b) { return a.second < b.second; });
-  std::map<RefKey, uint32_t> m;  // key -> rank within the map (FN:1448)
+  std::map<RefKey, std::pair<uint32_t, uint32_t>> m;  // key -> (rank within the map (FN:1448), members)
   uint32_t cur = UINT32_MAX;
   for (const auto& pr : q) {
     const uint32_t sq = pr.first, t = pr.second;
     if (t != cur) {  // replay the map of t: heads in index order, as FN:1401-1414
       cur = t;
       m.clear();
-      for (const ReplayHead& h : heads_at(I, t, hsmall, nullptr)) m.insert({h.key, 0u});
+      for (const ReplayHead& h : heads_at(I, t, hsmall, nullptr)) m.insert({h.key, {0u, 0u}}).first->second.second++;
       uint32_t r = 0, k = I.posBegin[t];
       for (auto& kv : m) {  // the device items of t must be the map's entries in order
-        if (k >= I.posBegin[t + 1] || I.len[k] != kv.first.len || I.isa[k] != kv.first.isaNext) *layoutMismatch = true;
-        kv.second = r++;
+        if (k >= I.posBegin[t + 1] || I.len[k] != kv.first.len || I.isa[k] != kv.first.isaNext ||
+            (I.small[k] != 0) != kv.first.smaller || I.count[k] != kv.second.second)
+          *layoutMismatch = true;
+        kv.second.first = r++;
         k++;
       }
       if (k != I.posBegin[t + 1]) *layoutMismatch = true;
@@ -144,7 +146,7 @@ inline HostQueryOut host_queries(const HostItems& I, const std::vector<uint32_t>
     const RefKey toFind{I.len[qi] - 1 - (t - I.pos[qi] - 1), I.small[qi] != 0, I.isa[qi]};  // uint32 wrap, FN:1532
     auto ptr = m.lower_bound(toFind);
     if (ptr == m.end()) continue;  // FN:1535-1536
-    const uint32_t tq = I.posBegin[t] + ptr->second;
+    const uint32_t tq = I.posBegin[t] + ptr->second.first;
     const uint32_t so = slot[tq], co = I.count[tq];
     const bool hasNext = std::next(ptr) != m.end();
     const uint32_t* me = nhr.data() + sq;

@@ -270,6 +270,12 @@ constexpr uint32_t kCoopJ = 4;  // 16-B pieces per thread per cooperative round
 // pending long extensions served together (r03 A/B, walk kernel: 1 -> 15.12 ms,
 // 4 -> 14.74 ms: a round trip of the wave serves four slots instead of ~2)
 constexpr uint32_t kCoopMin = 4;  // (3: 14.58 ms, 5: 15.6, 6: 16.1, 8: 17.1: pending lanes idle longer)
+// four slots whose ended extensions are replaced by pending lanes within the
+// round loop (CMSBWT_COOP_REFILL=0 builds the fixed groups of four for A/B)
+#ifndef CMSBWT_COOP_REFILL
+#define CMSBWT_COOP_REFILL 1
+#endif
+constexpr bool kCoopRefill = CMSBWT_COOP_REFILL != 0;
 // waves per SIMD of the walk (Makefile W2WAVES; measured 3 -> 16.50 ms,
 // 4 -> 16.44-16.68, 5 -> 16.9, 6 -> 31.3 with register spills)
 #ifndef CMSBWT_W2_WAVES
@@ -1058,6 +1064,83 @@ k_ms_walk2(Walk2Args A) {
     // wave's round trips, unless no other lane of the wave is still walking.
     uint64_t coop = __ballot(phase == PH_LCE_COOP);
     const bool drain = coop == __ballot(phase != PH_DONE);
+    if (kCoopRefill && (uint32_t)__popcll(coop) >= 4 && (drain || (uint32_t)__popcll(coop) >= kCoopMin)) {
+      // Four slots of 16 threads, each with its own offset: a slot whose
+      // extension ends takes the next pending lane in the same round trip, so
+      // the wave's rounds follow the total length of the extensions instead
+      // of the longest of each group of four (r04).
+      uint32_t Ls[4];
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        Ls[q] = (uint32_t)__builtin_ctzll(coop);
+        coop &= coop - 1;
+      }
+      const uint32_t g = lane >> 4, k = lane & 15;
+      uint32_t myL = g == 0 ? Ls[0] : g == 1 ? Ls[1] : g == 2 ? Ls[2] : Ls[3];
+      uintptr_t xa = ((uintptr_t)__shfl((uint32_t)(ad0 >> 32), (int)myL) << 32) | __shfl((uint32_t)ad0, (int)myL);
+      uintptr_t ta = ((uintptr_t)__shfl((uint32_t)(ad2 >> 32), (int)myL) << 32) | __shfl((uint32_t)ad2, (int)myL);
+      uint32_t runT = 0, open = 15u;
+      while (open) {
+        uint32_t mine = 16, mj = 0, cc = 0;
+        if ((open >> g) & 1) {
+          uint4 xv[kCoopJ], tv[kCoopJ];
+#pragma unroll
+          for (uint32_t j = 0; j < kCoopJ; j++) {
+            const uint32_t o = runT + 16 * (k + (j << 4));
+            xv[j] = ldu16(xa + o);
+            tv[j] = ldu16_nt(ta + o);
+          }
+#pragma unroll
+          for (int j = (int)kCoopJ - 1; j >= 0; j--) {
+            uint8_t xc = 0, tc = 0;
+            const uint32_t m = diff16(xv[j], tv[j], xc, tc);
+            if (m < 16) { mine = m; mj = (uint32_t)j; cc = (uint32_t)xc | ((uint32_t)tc << 8); }
+          }
+        }
+        if (STATS && lane == 0) atomicAdd(&sc[31], 1ull);
+        uint64_t mask[kCoopJ];
+#pragma unroll
+        for (uint32_t j = 0; j < kCoopJ; j++) mask[j] = __ballot(mine < 16 && mj == j);
+        uint32_t fresh = 0;  // slots given a new lane this round
+#pragma unroll
+        for (uint32_t q = 0; q < 4; q++) {
+          if (!((open >> q) & 1)) continue;
+          const uint64_t sm = 0xffffull << (q << 4);
+#pragma unroll
+          for (uint32_t j = 0; j < kCoopJ; j++) {
+            const uint64_t hit = mask[j] & sm;
+            if (hit) {  // first mismatching byte of slot q: piece j, thread f
+              const uint32_t f = (uint32_t)__builtin_ctzll(hit);
+              const uint32_t mm = (uint32_t)__shfl((int)mine, (int)f);
+              const uint32_t c2 = (uint32_t)__shfl((int)cc, (int)f);
+              const uint32_t rq = (uint32_t)__shfl((int)runT, (int)f);
+              if (lane == Ls[q]) {
+                len += rq + 16 * ((f - (q << 4)) + (j << 4)) + mm;
+                smaller = (int8_t)(uint8_t)c2 > (int8_t)(uint8_t)(c2 >> 8);  // FN:55
+                phase = PC_POST;
+              }
+              if (coop) {
+                Ls[q] = (uint32_t)__builtin_ctzll(coop);
+                coop &= coop - 1;
+                fresh |= 1u << q;
+              } else {
+                open &= ~(1u << q);
+              }
+              break;
+            }
+          }
+        }
+        runT = ((fresh >> g) & 1) ? 0u : runT + 16u * 16u * kCoopJ;
+        if (fresh) {
+          myL = g == 0 ? Ls[0] : g == 1 ? Ls[1] : g == 2 ? Ls[2] : Ls[3];
+          const uintptr_t nx = ((uintptr_t)__shfl((uint32_t)(ad0 >> 32), (int)myL) << 32) |
+                               __shfl((uint32_t)ad0, (int)myL);
+          const uintptr_t nt = ((uintptr_t)__shfl((uint32_t)(ad2 >> 32), (int)myL) << 32) |
+                               __shfl((uint32_t)ad2, (int)myL);
+          if ((fresh >> g) & 1) { xa = nx; ta = nt; }
+        }
+      }
+    }
     while (coop && (drain || (uint32_t)__popcll(coop) >= kCoopMin)) {
       const uint32_t P = (uint32_t)__popcll(coop);
       const uint32_t S = P >= 4 ? 4u : P >= 2 ? 2u : 1u;

@@ -26,7 +26,11 @@ extern "C" {
 #define CMSBWT_EINPUT 3     /* input on which the reference is undefined            */
 #define CMSBWT_EDEVICE 4    /* HIP runtime error or HIP code object not loadable    */
 #define CMSBWT_ELIMIT 5     /* size limit (reference int32/uint32 limits)           */
-#define CMSBWT_EORDER 6     /* comparator ambiguity the sharded merge cannot replay */
+#define CMSBWT_EORDER 6     /* reserved, no longer returned: a sharded step that    */
+                            /* meets comparator ambiguity is redone as a gather    */
+                            /* step (every head to rank 0, one-GPU merge with the  */
+                            /* std::map replay there; rank 0 then needs the memory */
+                            /* of a one-GPU merge of all heads, ~135 B per head)   */
 #define CMSBWT_EINTERNAL 7  /* unexpected host exception (thread creation, ...)     */
 
 /* utils.h:8-14 struct Args, plus engine knobs. */
@@ -35,9 +39,23 @@ typedef struct cmsbwt_args {
   uint32_t buffer_gb;   /* -b  (small path memory knob only; no output effect)  */
   int32_t rle;          /* -r  1 = <out>.rl_bwt, 0 = <out>.bwt                  */
   const char* outname;  /* -o  basename (NULL = list file name)                 */
-  int32_t device;       /* HIP device ordinal                                   */
+  int32_t device;       /* HIP device ordinal (rank 0's device with n_gpus > 1)  */
   int32_t verbose;      /* 1 = stage times on stderr                            */
+  int32_t n_gpus;       /* ranks in this process (0/1 = one GPU); rank k runs on */
+                        /* device (device + k) % device count, so ranks may     */
+                        /* share a GPU (tests)                                  */
+  int32_t backend;      /* n_gpus > 1: CMSBWT_BACKEND_PEER or _RCCL              */
 } cmsbwt_args;
+
+/* Transports of the in-process multi-GPU run (cmsbwt_run with n_gpus > 1).
+ * PEER: all-to-alls, reductions and the run gather as pulls between the
+ *   ranks' HBM buffers (hipMemcpyPeerAsync over xGMI; device-local copies
+ *   when ranks share a GPU).
+ * RCCL: the same exchanges as RCCL send/recv groups and all-reduces on a
+ *   communicator made by ncclCommInitAll (needs one distinct GPU per rank;
+ *   librccl is opened at run time). */
+#define CMSBWT_BACKEND_PEER 0
+#define CMSBWT_BACKEND_RCCL 1
 
 /* Statistics mirrored from the reference .log (FN:1417-1422, 1452, 1515,
  * 1606-1608) plus engine timings. */
@@ -73,6 +91,7 @@ typedef struct cmsbwt_stats {
   double t_libsais_int_ms;   /* head-string suffix sort, FN:1455-1461           */
   double t_counter_ms;       /* counterSmallerThanHead, FN:1517-1611            */
   uint64_t host_queries;     /* counter queries answered by the std::map replay */
+  uint64_t device_peak_bytes; /* high-water mark of this context's HBM buffers  */
 } cmsbwt_stats;
 
 typedef struct cmsbwt_ctx cmsbwt_ctx;

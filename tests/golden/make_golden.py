@@ -1,7 +1,9 @@
 """Regenerate tests/golden/ (run in the build container; needs the oracle).
 
-* golden.json "survey": outputs of the REAL reference recorded in SURVEY.md
-  (App. B runs, numpy generator of gen_np.py) -- the oracle must reproduce them.
+* golden.json "survey": counts recorded in SURVEY.md (App. B runs, numpy
+  generator of gen_np.py) from a survey-container build of the reference
+  linked against a stand-in libsais -- the oracle reproduces them, but they do
+  not pin parity (parity unpinned).
 * golden.json "c1"/"t2": oracle outputs on those inputs (sha256 of .rl_bwt,
   run/symbol counts), used by the GPU tests as golden vectors.
 * small/<case>/: tiny inputs with expected .rl_bwt / .bwt bytes.  These are

@@ -1,0 +1,63 @@
+"""GPU: BASELINE config 4 -- the headline workload (10 MB reference + 1000
+copies @0.1 % SNP, 10 GB, -r) sharded over N ranks -- run through bench.py's
+own N > 1 path.
+
+The driver launches `bench.py --gpus N` under torchrun with one rank per GPU
+over RCCL.  Here the ranks share the test GPU (CMSBWT_BENCH_SAME_GPU=1: every
+rank on device 0, gloo with host staging instead of RCCL, which allows one rank
+per device); the sharding, the sharded merge (dist_merge.hip) and every
+collective are the ones the N-GPU run issues.  Rank 0's runs of the timed step
+must equal the oracle's golden for this exact workload (golden synth_c3:
+sha256 of the .rl_bwt, headNumber, keys, Rank, runs and the three counter
+totals), FN:1138-1352 (document loop, sharded) and FN:1387-1777 (merge)."""
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def run_bench(world, extra=(), env_extra=None, timeout=900):
+    env = dict(os.environ, CMSBWT_BENCH_SAME_GPU="1", PYTHONUNBUFFERED="1")
+    env.update(env_extra or {})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), "--steps", "1", "--warmup", "0", "--no-cpu", "--no-e2e", *extra]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_config4_sharded_bench_golden(world):
+    out = run_bench(world)
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["synth_c3"]
+    par = out["parity"]
+    assert par["verdict"] == "bit-exact vs oracle golden", par
+    assert par["heads"] == g["headNumber"] == 100572666
+    assert par["rank"] == g["Rank"] == 54555418
+    assert (par["counter_bad"], par["counter_good"], par["counter_nothing"]) == \
+        (g["counterBad"], g["counterGood"], g["counterDoNothing"])
+    assert out["n_gpus"] == world and len(out["per_rank"]) == world
+    # every rank walked its share of the documents; the merge stage is timed
+    assert sum(r["chars"] for r in out["per_rank"]) == 10**10
+    assert sum(r["heads"] for r in out["per_rank"]) == g["headNumber"]
+    assert out["stages_ms"]["merge"] > 0 and out["stages_ms"]["ms_walk"] > 0
+    print(json.dumps({"world": world, "ms_per_step": out["ms_per_step"], "stages_ms": out["stages_ms"],
+                      "per_rank": out["per_rank"], "hbm_peak_gib": out["hbm_peak_gib"]}))
