@@ -29,6 +29,7 @@ struct CtxView {
   const uint32_t* dmItemPos = nullptr;
   const uint32_t* dmGrp = nullptr;   // group label (1 + head rank) per head
   uint64_t dmU = 0;                  // unresolved members after dm_dbl_init
+  uint32_t dmLabelBias = 0;          // added to every label in dmGrp
   cmsbwt_stats stats{};
   uint64_t devicePeak = 0;
 };

@@ -101,10 +101,13 @@ __global__ void k_dm_sa_counts(const int32_t* __restrict__ sa, const uint32_t* _
 // gBase[p] + slot[q] (gBase from k_pos_rank_base: 1 + headBase[ISA[p]] minus
 // the slot of p's first item; slots ascend with p, so it is read in order).
 // Bit 32: unresolved (item with >= 2 members; labels use all 32 bits).
-// Written in received order for the return trip.
+// Written in received order for the return trip.  Labels carry `bias`
+// (0 in production; tests set it so that labels cross 2^31 on small inputs,
+// CMSBWT_DM_LABEL_BIAS); gItem keeps the unbiased label.
 __global__ void k_dm_group_labels(const ItemsSoA it, const uint32_t* __restrict__ itemOfSlot,
                                   const uint32_t* __restrict__ Pm, uint32_t H, const uint32_t* __restrict__ gBase,
-                                  uint32_t n, unsigned long long* __restrict__ back, uint32_t* __restrict__ gItem) {
+                                  uint32_t n, uint32_t bias, unsigned long long* __restrict__ back,
+                                  uint32_t* __restrict__ gItem) {
   const uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= H) return;
   const uint32_t q = itemOfSlot[s], sq = it.slot[q], m = s - sq, p = it.pos[q];
@@ -118,7 +121,7 @@ __global__ void k_dm_group_labels(const ItemsSoA it, const uint32_t* __restrict_
     if (m == 0) gItem[q] = g;
     act = it.count[q] >= 2 ? 1u : 0u;
   }
-  back[Pm[s]] = (unsigned long long)g | ((unsigned long long)act << 32);
+  back[Pm[s]] = (unsigned long long)(g + bias) | ((unsigned long long)act << 32);
 }
 
 // doc side: labels arrive in send order; flags stay in send order
@@ -252,15 +255,16 @@ __global__ void k_dm_dbl_apply(const uint32_t* __restrict__ aPerm, const uint32_
 // the ranks it reads anyway (one gather per slot, not two)
 __global__ void k_dm_pack_ranks(const uint32_t* __restrict__ perm, const uint32_t* __restrict__ grp,
                                 const uint16_t* __restrict__ nexthead, const uint8_t* __restrict__ lchar,
-                                uint64_t n, uint32_t H, int32_t* __restrict__ out, uint32_t* __restrict__ err) {
+                                uint64_t n, uint32_t H, uint32_t bias, int32_t* __restrict__ out,
+                                uint32_t* __restrict__ err) {
   const uint64_t j = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (j >= n) return;
   const uint32_t i = perm[j];
   const uint32_t nx = i + nexthead[i];
   uint32_t nv = 0;
-  if (nx < H) nv = grp[nx] - 1;
+  if (nx < H) nv = grp[nx] - 1 - bias;
   else atomicOr(err, 2u);
-  out[3 * j] = (int32_t)(grp[i] - 1);
+  out[3 * j] = (int32_t)(grp[i] - 1 - bias);
   out[3 * j + 1] = (int32_t)nv;
   out[3 * j + 2] = (int32_t)lchar[i];
 }
@@ -423,8 +427,10 @@ void mk_dm_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t
   hipLaunchKernelGGL(k_dm_sa_counts, g1d(n), dim3(256), 0, st, sa, posBegin, slot, n, Eown, out);
 }
 void mk_dm_group_labels(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
-                        const uint32_t* gBase, uint32_t n, unsigned long long* back, uint32_t* gItem, hipStream_t st) {
-  if (H) hipLaunchKernelGGL(k_dm_group_labels, g1d(H), dim3(256), 0, st, it, itemOfSlot, Pm, H, gBase, n, back, gItem);
+                        const uint32_t* gBase, uint32_t n, uint32_t bias, unsigned long long* back, uint32_t* gItem,
+                        hipStream_t st) {
+  if (H)
+    hipLaunchKernelGGL(k_dm_group_labels, g1d(H), dim3(256), 0, st, it, itemOfSlot, Pm, H, gBase, n, bias, back, gItem);
 }
 void mk_dm_grp_init(const uint32_t* perm, const unsigned long long* in, uint64_t n, uint32_t* grp, uint32_t* actFlag,
                     hipStream_t st) {
@@ -459,8 +465,8 @@ void mk_dm_dbl_apply(const uint32_t* aPerm, const uint32_t* act, const unsigned 
   if (n) hipLaunchKernelGGL(k_dm_dbl_apply, g1d(n), dim3(256), 0, st, aPerm, act, back, n, grp, keep);
 }
 void mk_dm_pack_ranks(const uint32_t* perm, const uint32_t* grp, const uint16_t* nexthead, const uint8_t* lchar,
-                      uint64_t n, uint32_t H, int32_t* out, uint32_t* err, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_dm_pack_ranks, g1d(n), dim3(256), 0, st, perm, grp, nexthead, lchar, n, H, out, err);
+                      uint64_t n, uint32_t H, uint32_t bias, int32_t* out, uint32_t* err, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_dm_pack_ranks, g1d(n), dim3(256), 0, st, perm, grp, nexthead, lchar, n, H, bias, out, err);
 }
 void mk_dm_load_ranks(const int32_t* in, const uint32_t* Pm, const uint32_t* itemOfSlot, const ItemsSoA& it,
                       const uint32_t* gItem, uint32_t H, uint32_t* nbi, uint8_t* bwtSlot, uint32_t* err, hipStream_t st) {

@@ -78,13 +78,22 @@ void Engine::dm_begin(uint32_t world, uint32_t rank, uint64_t heads_total, uint6
   dm.E = (uint32_t)docs_total;
   dm.rle = rle;
   dm.check = !(flags & 1u) || env_u32("CMSBWT_FORCE_CHECK", 0) != 0;
+  // group labels are 1 .. Htot (+ bias: tests push them across 2^31 with
+  // small inputs; the labels, the label-range owners and the doubling keys
+  // carry it, the head ranks drop it)
+  {
+    const char* b = getenv("CMSBWT_DM_LABEL_BIAS");
+    const uint64_t bias = b ? strtoull(b, nullptr, 10) : 0;
+    if (bias + heads_total >= 0xffffffffull) throw InputError{CMSBWT_EARG, "label bias too large"};
+    dm.labelBias = (uint32_t)bias;
+  }
   dm.Psplit.assign(world + 1, 0);
   dm.Gsplit.assign(world + 1, 0);
   for (uint32_t k = 0; k <= world; k++) {
     dm.Psplit[k] = (uint32_t)((uint64_t)k * n / world);
-    dm.Gsplit[k] = 1 + (uint32_t)((uint64_t)k * dm.Htot / world);
+    dm.Gsplit[k] = dm.labelBias + 1 + (uint32_t)((uint64_t)k * dm.Htot / world);
   }
-  dm.Gsplit[world] = dm.Htot + 1;
+  dm.Gsplit[world] = dm.labelBias + dm.Htot + 1;
   dm.P0 = dm.Psplit[rank];
   dm.P1 = dm.Psplit[rank + 1];
   dm.dPsplit.alloc(world + 1);
@@ -178,7 +187,7 @@ void Engine::dm_labels(const uint32_t* saCounts, unsigned long long* back) {
     DBuf<uint32_t> gBase;
     gBase.alloc(n);
     mk_pos_rank_base(dm.IS.posBegin.p, dm.IS.slot.p, disa.p, nullptr, dm.headBase.p, n, 0, nullptr, gBase.p, st);
-    mk_dm_group_labels(dm.IS.soa(), dm.itemOfSlot.p, dm.Pm.p, dm.Hp, gBase.p, n, back, dm.gItem.p, st);
+    mk_dm_group_labels(dm.IS.soa(), dm.itemOfSlot.p, dm.Pm.p, dm.Hp, gBase.p, n, dm.labelBias, back, dm.gItem.p, st);
   }
   HIPCHK(hipGetLastError());
   sync();
@@ -241,7 +250,7 @@ void Engine::dm_dbl_sort(const int32_t* recv, uint64_t nrecv, unsigned long long
     DBuf<uint32_t> v, vb, gs, ks, gsM, ksM;
     k64.alloc(B); k64b.alloc(B); v.alloc(B); vb.alloc(B);
     mk_dm_dbl_bigkeys(big.p + 1, B, key2.p, val2.p, G0, k64.p, v.p, st);
-    sort_pairs(k64.p, k64b.p, v.p, vb.p, B, 32 + bits_for(dm.Htot));
+    sort_pairs(k64.p, k64b.p, v.p, vb.p, B, 32 + bits_for(G1 - 1));  // labels < G1
     gs.alloc(B); ks.alloc(B); gsM.alloc(B); ksM.alloc(B);
     mk_dm_dbl_marks(k64b.p, B, gs.p, ks.p, st);
     inscan(gs.p, gsM.p, B, rocprim::maximum<uint32_t>());
@@ -265,7 +274,7 @@ uint64_t Engine::dm_dbl_apply(const unsigned long long* back) {
 
 // ---- 4. head ranks and next-head ranks to the position owners
 void Engine::dm_pack_ranks(int32_t* out) {
-  mk_dm_pack_ranks(dm.hPerm.p, dm.grp.p, hNext.p, hChar.p, H, H, out, dm.err.p, st);
+  mk_dm_pack_ranks(dm.hPerm.p, dm.grp.p, hNext.p, hChar.p, H, H, dm.labelBias, out, dm.err.p, st);
   HIPCHK(hipGetLastError());
   sync();
   dm_check_err("next-head ranks");

@@ -2443,6 +2443,7 @@ struct Engine {
   struct DistMerge {
     bool on = false;  // the last merge was sharded (its runs live on rank 0)
     uint32_t world = 1, rank = 0, P0 = 0, P1 = 0, E = 0, Htot = 0;
+    uint32_t labelBias = 0;  // added to every group label (tests: CMSBWT_DM_LABEL_BIAS)
     int rle = 1;
     bool check = false;
     std::vector<uint32_t> Psplit, Gsplit;

@@ -25,6 +25,7 @@ CtxView ctx_view(const cmsbwt_ctx* c) {
   v.dmItemPos = e.dm.IS.pos.p;
   v.dmGrp = e.dm.grp.p;
   v.dmU = e.dm.U;
+  v.dmLabelBias = e.dm.labelBias;
   v.stats = e.stats;
   v.devicePeak = e.alloc.peak;
   return v;

@@ -208,7 +208,8 @@ void mk_dm_runs(const uint32_t* pos, const uint32_t* tonext, uint64_t H, uint32_
 void mk_dm_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t Eown,
                      uint32_t* out, hipStream_t st);
 void mk_dm_group_labels(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
-                        const uint32_t* gBase, uint32_t n, unsigned long long* back, uint32_t* gItem, hipStream_t st);
+                        const uint32_t* gBase, uint32_t n, uint32_t bias, unsigned long long* back, uint32_t* gItem,
+                        hipStream_t st);
 void mk_dm_grp_init(const uint32_t* perm, const unsigned long long* in, uint64_t n, uint32_t* grp, uint32_t* actFlag,
                     hipStream_t st);
 void mk_dm_dbl_pack(const uint32_t* aPerm, const uint32_t* act, const uint32_t* grp, uint32_t h, uint64_t n,
@@ -227,7 +228,7 @@ void mk_dm_dbl_apply(const uint32_t* aPerm, const uint32_t* act, const unsigned 
                      uint32_t* keep, hipStream_t st);
 // (head rank, next-head rank, BWT character): 3 words per head in send order
 void mk_dm_pack_ranks(const uint32_t* perm, const uint32_t* grp, const uint16_t* nexthead, const uint8_t* lchar,
-                      uint64_t n, uint32_t H, int32_t* out, uint32_t* err, hipStream_t st);
+                      uint64_t n, uint32_t H, uint32_t bias, int32_t* out, uint32_t* err, hipStream_t st);
 // head characters by slot (bwtSlot) and the next-head ranks in slot order (nbiS)
 void mk_dm_load_ranks(const int32_t* in, const uint32_t* Pm, const uint32_t* itemOfSlot, const ItemsSoA& it,
                       const uint32_t* gItem, uint32_t H, uint32_t* nbiS, uint8_t* bwtSlot, uint32_t* err,

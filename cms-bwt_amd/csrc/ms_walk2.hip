@@ -276,6 +276,12 @@ constexpr uint32_t kCoopMin = 4;  // (3: 14.58 ms, 5: 15.6, 6: 16.1, 8: 17.1: pe
 #define CMSBWT_COOP_REFILL 1
 #endif
 constexpr bool kCoopRefill = CMSBWT_COOP_REFILL != 0;
+// short unique matches go straight to the next position's probe instead of
+// the PLCP skip (CMSBWT_PROBE_NOSKIP=0 keeps the skip, for A/B)
+#ifndef CMSBWT_PROBE_NOSKIP
+#define CMSBWT_PROBE_NOSKIP 1
+#endif
+constexpr bool kProbeNoSkip = CMSBWT_PROBE_NOSKIP != 0;
 // waves per SIMD of the walk (Makefile W2WAVES; measured 3 -> 16.50 ms,
 // 4 -> 16.44-16.68, 5 -> 16.9, 6 -> 31.3 with register spills)
 #ifndef CMSBWT_W2_WAVES
@@ -627,7 +633,17 @@ k_ms_walk2(Walk2Args A) {
         count++;
       }
       len--;
-      if (lb == rb) {  // FN:1175-1189: skip, then adjustInterval(ISA[pos+1])
+      if (kProbeNoSkip && pfxExact && hasPfx && lb == rb && len < R.kmerK && twAt == i + 1 && wm == R.kmerK) {
+        // a short unique match (the mismatch region around a SNP): the
+        // next position's K symbols are decoded, and its probe gives its MS
+        // triple, which depends on the text alone -- a
+        // continuation shows as pos == prevPos + 1 (no head) -- so the skip
+        // (FN:1175-1189, one PLCP and one text load that usually skip
+        // nothing here) is not taken
+        virtual_interval();
+        phase = PC_ADV;
+        use = 0;
+      } else if (lb == rb) {  // FN:1175-1189: skip, then adjustInterval(ISA[pos+1])
         // the exit is the first q >= pos+1 with PLCP[q] + q >= T = pos+1+len;
         // PLCP of a random-like text is ~log4 n, so it lies ~12 below T:
         // probe the 16 entries below T first

@@ -443,7 +443,7 @@ bool sharded_merge(Xfer& x, cmsbwt_ctx* ctx, int rle, RankOut& ro) {
     MCHK(hipMemcpyAsync(&a, vd.dmGrp, 4, hipMemcpyDeviceToHost, vd.st));
     MCHK(hipMemcpyAsync(&b, vd.dmGrp + (H - 1), 4, hipMemcpyDeviceToHost, vd.st));
     x.sync();
-    fl = {a, b, 1};
+    fl = {a - vd.dmLabelBias, b - vd.dmLabelBias, 1};
   }
   // 4. head ranks / next-head ranks / BWT characters to the position owners
   auto tr2 = Clock::now();

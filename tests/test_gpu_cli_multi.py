@@ -151,3 +151,18 @@ def test_computeBWT_multi_python_mirror(built, oracle, tmp_path):
                                        prefixLength=prefix), rp, cp)
     assert open(os.path.join(d, "py.rl_bwt"), "rb").read() == open(os.path.join(d, "oracle.rl_bwt"), "rb").read()
     assert (st.heads, st.keys) == (ost["heads"], ost["keys"])
+
+
+def test_cli_multi_labels_past_2_31(built, tmp_path):
+    """Config 1 with -n 2 and the sharded merge's group labels biased to
+    straddle 2^31 (CMSBWT_DM_LABEL_BIAS; config 5's 2.12e9 heads sit at 0.986 x
+    2^31): golden bytes, and First/Last rankToHead without the bias."""
+    g = json.load(open(os.path.join(GOLD, "golden.json")))["c1"]
+    pre = str(tmp_path / "c1")
+    _gen_np().gen(1_000_000, 10, 0.001, 11, pre)
+    r1 = run_cli(["-r", "-o", pre + "_1", pre + ".list"])
+    r2 = run_cli(["-r", "-n", "2", "-o", pre + "_2", pre + ".list"],
+                 env={"CMSBWT_DM_LABEL_BIAS": str(2**31 - g["headNumber"] // 2)})
+    assert r1.returncode == 0 and r2.returncode == 0, r2.stdout + r2.stderr
+    assert sha(pre + "_2.rl_bwt") == g["rl_bwt_sha256"]
+    assert _values(pre + "_2.log", KEYS_LARGE) == _values(pre + "_1.log", KEYS_LARGE)

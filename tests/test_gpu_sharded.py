@@ -231,3 +231,31 @@ def test_sharded_four_ranks_config5_proxy_plain_golden(tmp_path):
         (g["counterBad"], g["counterGood"], g["counterDoNothing"])
     assert os.path.getsize(out + ".bwt") == g["bwt_bytes"]
     assert _sha_file(out + ".bwt") == g["bwt_sha256"]
+
+
+# Config 5 has 2,118,018,850 heads (tools/c5_size.py): 0.986 x
+# 2^31, so group labels of larger collections cross 2^31.  The sharded merge
+# carries a label bias (CMSBWT_DM_LABEL_BIAS) through every label it moves,
+# sorts and routes; biases just below 2^31 and near 2^32 make a small case's
+# labels cross bit 31 / use all 32 bits, with the oracle's bytes expected.
+LABEL_BIASES = [2**31 - 64, 2**32 - 2**20]
+
+
+@pytest.mark.parametrize("bias", LABEL_BIASES, ids=["straddle_2_31", "near_2_32"])
+@pytest.mark.parametrize("world", [1, 2])
+def test_sharded_labels_past_2_31(engine, oracle, tmp_path, world, bias, monkeypatch):
+    monkeypatch.setenv("CMSBWT_DM_LABEL_BIAS", str(bias))
+    case = [c for c in cases.small_cases() if c[0] == "copies_5k_1pct"][0]
+    if world == 1:
+        import cmsbwt.dist as cdist
+        d, rp, cp, prefix, ost, want = _oracle_files(oracle, tmp_path, case, True)
+        assert ost["heads"] > 64
+        engine.initialize_reference(rp)
+        engine.load_collection_file(cp, prefix)
+        cdist.sharded_step(engine, "cuda:0", rle=True, xfer=cdist.Transport("cuda:0", 1, 0))
+        assert engine.runs_bytes() == want
+        st = engine.stats()
+        assert (st.heads, st.keys, st.rank) == (ost["heads"], ost["keys"], ost["rank"])
+        assert (st.counter_bad, st.counter_good, st.counter_nothing) == (ost["bad"], ost["good"], ost["nothing"])
+    else:
+        _multi(oracle, tmp_path, case, world, rle=True)
