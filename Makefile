@@ -7,7 +7,9 @@ OUT ?= cms-bwt_amd/build
 HIPFLAGS := --offload-arch=$(ARCH) -O3 -std=c++17 -fPIC -Wall -Wno-unused-result -Wno-unused-function $(XFLAGS)
 HOSTFLAGS := -O3 -std=c++17 -fPIC -Wall
 
-OBJS := $(OUT)/engine.o $(OUT)/multi.o $(OUT)/dist_merge.o $(OUT)/dist_kernels.o $(OUT)/ms_walk.o $(OUT)/ms_walk2.o $(OUT)/merge.o $(OUT)/synth.o $(OUT)/coll_read.o $(OUT)/ref_index.o $(OUT)/host_index.o $(OUT)/host_reader.o
+# dist_merge.hip is compiled inside engine.hip (one translation unit: the
+# engine's rocPRIM instantiations are emitted once, not once per file)
+OBJS := $(OUT)/engine.o $(OUT)/multi.o $(OUT)/dist_kernels.o $(OUT)/ms_walk.o $(OUT)/ms_walk2.o $(OUT)/merge.o $(OUT)/synth.o $(OUT)/coll_read.o $(OUT)/ref_index.o $(OUT)/host_index.o $(OUT)/host_reader.o
 HDRS := $(wildcard $(SRC)/*.h) include/cmsbwt.h
 
 all: lib cli gen oracle
@@ -18,6 +20,8 @@ gen: $(OUT)/gen_synth
 
 $(OUT):
 	mkdir -p $(OUT)
+
+$(OUT)/engine.o: $(SRC)/dist_merge.hip
 
 $(OUT)/%.o: $(SRC)/%.hip $(HDRS) | $(OUT)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<

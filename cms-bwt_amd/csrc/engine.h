@@ -435,6 +435,14 @@ struct Engine {
     auto now = [] { return std::chrono::steady_clock::now(); };
     auto t0 = now();
     const uint32_t n = hix.n;
+    if (env_u32("CMSBWT_TIMING", 0)) {  // the first kernel of the process loads the code object
+      DBuf<uint32_t> one;
+      one.alloc(1);
+      mk_iota(one.p, 1, st);
+      sync();
+      fprintf(stderr, "[index] first launch %.3f s\n", std::chrono::duration<double>(now() - t0).count());
+      t0 = now();
+    }
     dx.alloc((uint64_t)n + kTextPad);
     HIPCHK(hipMemsetAsync(dx.p, 0, n + kTextPad, st));
     HIPCHK(hipMemcpyAsync(dx.p, hix.x.data(), n, hipMemcpyHostToDevice, st));

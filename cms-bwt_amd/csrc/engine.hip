@@ -522,3 +522,7 @@ int cmsbwt_dm_finish(cmsbwt_ctx* ctx, const uint64_t* const* starts, const uint8
 }
 
 }  // extern "C"
+
+// The position-sharded merge's Engine members, in this translation unit (see
+// the Makefile): engine.h's rocPRIM instantiations are emitted once.
+#include "dist_merge.hip"

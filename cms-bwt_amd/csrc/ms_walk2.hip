@@ -146,6 +146,26 @@ __device__ __forceinline__ uint32_t diff16(const uint4& x, const uint4& t, uint8
   return (d0 ? 0 : 8) + bit / 8;
 }
 
+// First and second differing bytes of two 16-byte strings (16 when none).
+__device__ __forceinline__ void diff16x2(const uint4& x, const uint4& t, uint32_t& m1, uint32_t& c1, uint32_t& m2,
+                                         uint32_t& c2) {
+  const uint64_t x0 = x.x | ((uint64_t)x.y << 32), x1 = x.z | ((uint64_t)x.w << 32);
+  const uint64_t t0 = t.x | ((uint64_t)t.y << 32), t1 = t.z | ((uint64_t)t.w << 32);
+  uint64_t d0 = x0 ^ t0, d1 = x1 ^ t1;
+  m1 = m2 = 16;
+  c1 = c2 = 0;
+#pragma unroll
+  for (int r = 0; r < 2; r++) {
+    if (!(d0 | d1)) break;
+    const bool lo = d0 != 0;
+    const uint32_t bit = (uint32_t)__builtin_ctzll(lo ? d0 : d1) & ~7u;
+    const uint32_t m = (lo ? 0u : 8u) + bit / 8;
+    const uint32_t c = (uint32_t)(uint8_t)((lo ? x0 : x1) >> bit) | ((uint32_t)(uint8_t)((lo ? t0 : t1) >> bit) << 8);
+    if (r == 0) { m1 = m; c1 = c; } else { m2 = m; c2 = c; }
+    if (lo) d0 &= ~(0xffull << bit); else d1 &= ~(0xffull << bit);
+  }
+}
+
 // Level geometry of the LCP block minima, staged in LDS.
 struct Lv {
   const uint32_t* len;  // lvlLen
@@ -282,6 +302,21 @@ constexpr bool kCoopRefill = CMSBWT_COOP_REFILL != 0;
 #define CMSBWT_PROBE_NOSKIP 1
 #endif
 constexpr bool kProbeNoSkip = CMSBWT_PROBE_NOSKIP != 0;
+// the text side of cooperative extensions read non-temporally (r03: 15.12 ->
+// 14.96 ms); CMSBWT_COOP_TEXT_NT=0 reads it through L2 (the bytes past the
+// mismatch are read again by the next extension and the skip)
+#ifndef CMSBWT_COOP_TEXT_NT
+#define CMSBWT_COOP_TEXT_NT 1
+#endif
+// alignment memo: a cooperative extension that ends at a mismatch (a SNP of a
+// copy) also reports the next mismatch at the same text-to-reference offset in
+// the bytes its round read, or how far they are clean; the extension at that
+// offset after the SNP (the copy's next long match) starts there instead of
+// reading those bytes again (CMSBWT_ALIGN_MEMO=1)
+#ifndef CMSBWT_ALIGN_MEMO
+#define CMSBWT_ALIGN_MEMO 0
+#endif
+constexpr bool kAlignMemo = CMSBWT_ALIGN_MEMO != 0;
 // waves per SIMD of the walk (Makefile W2WAVES; measured 3 -> 16.50 ms,
 // 4 -> 16.44-16.68, 5 -> 16.9, 6 -> 31.3 with register spills)
 #ifndef CMSBWT_W2_WAVES
@@ -338,6 +373,10 @@ k_ms_walk2(Walk2Args A) {
   // windows from them instead of loading the text again
   uint4 t32a = make_uint4(0, 0, 0, 0), t32b = t32a;
   uint32_t t32At = 0xfffffff0u;
+  // alignment memo (kAlignMemo): at offset amAlign = pos - i the text
+  // positions [amLo, amFront) match the reference; amC bit 16: the bytes at
+  // amFront differ (x byte | text byte << 8)
+  uint32_t amAlign = 0, amLo = 0xffffffffu, amFront = 0, amC = 0;
   // emission
   // pool blocks are reserved kPoolBatch at a time (blk .. blkEnd) and kept
   // across this lane's chunks; blocks never started keep blkChunk = ~0
@@ -519,6 +558,23 @@ k_ms_walk2(Walk2Args A) {
       skip_done((uint32_t)u2);
     }
   };
+  // FN:52-62 from (pos, len): 16 bytes of x and of the text, unless the
+  // alignment memo already knows where this offset's match ends
+  auto start_lce = [&]() {
+    if (kAlignMemo && pos - i == amAlign && i + len >= amLo && i + len <= amFront) {
+      len = amFront - i;
+      if (amC & 0x10000u) {  // the mismatch at amFront (FN:55)
+        smaller = (int8_t)(uint8_t)amC > (int8_t)(uint8_t)(amC >> 8);
+        phase = PC_POST;
+        use = 0;
+        return;
+      }
+    }
+    phase = PH_LCE;
+    ad0 = X + pos + len;
+    ad2 = T + i + len;
+    use = U0Q | U2Q;
+  };
   auto set_adj_addr = [&]() {
     use = 0;
     if ((uint32_t)u4 != kScanDone) { ad0 = scan_addr<false>(V, u0, (uint32_t)u4); use |= U0Q | U1Q; }
@@ -573,6 +629,7 @@ k_ms_walk2(Walk2Args A) {
           smaller = false;
           twAt = 0xffffffffu;
           t32At = 0xfffffff0u;  // (another document's bytes)
+          amLo = 0xffffffffu;
           if (hasPfx) {
             phase = PH_PFX_TEXT;
             ad0 = T + i;
@@ -839,10 +896,7 @@ k_ms_walk2(Walk2Args A) {
       }
       case PH_LCE_SA: {
         pos = v0.x;
-        phase = PH_LCE;
-        ad0 = X + pos + len;
-        ad2 = T + i + len;
-        use = U0Q | U2Q;
+        start_lce();
         break;
       }
       case PH_LCE: {
@@ -1014,10 +1068,7 @@ k_ms_walk2(Walk2Args A) {
           lb = rb = 0;
           len = m;
           pos = v0.x;
-          phase = PH_LCE;
-          ad0 = X + pos + len;
-          ad2 = T + i + len;
-          use = U0Q | U2Q;
+          start_lce();
           break;
         }
         if (!(v0.y & kPfxAns)) {  // t[i..i+m) occurs: its interval, depth m
@@ -1098,25 +1149,35 @@ k_ms_walk2(Walk2Args A) {
       uint32_t runT = 0, open = 15u;
       while (open) {
         uint32_t mine = 16, mj = 0, cc = 0;
+        uint32_t pm = 0, mine2 = 16, cc2 = 0;  // (memo) pieces with a mismatch; 2nd mismatch of piece mj
         if ((open >> g) & 1) {
           uint4 xv[kCoopJ], tv[kCoopJ];
 #pragma unroll
           for (uint32_t j = 0; j < kCoopJ; j++) {
             const uint32_t o = runT + 16 * (k + (j << 4));
             xv[j] = ldu16(xa + o);
-            tv[j] = ldu16_nt(ta + o);
+            tv[j] = CMSBWT_COOP_TEXT_NT ? ldu16_nt(ta + o) : ldu16(ta + o);
           }
 #pragma unroll
           for (int j = (int)kCoopJ - 1; j >= 0; j--) {
-            uint8_t xc = 0, tc = 0;
-            const uint32_t m = diff16(xv[j], tv[j], xc, tc);
-            if (m < 16) { mine = m; mj = (uint32_t)j; cc = (uint32_t)xc | ((uint32_t)tc << 8); }
+            if (kAlignMemo) {
+              uint32_t m1, c1, m2, c2;
+              diff16x2(xv[j], tv[j], m1, c1, m2, c2);
+              if (m1 < 16) { mine = m1; mj = (uint32_t)j; cc = c1; mine2 = m2; cc2 = c2; pm |= 1u << j; }
+            } else {
+              uint8_t xc = 0, tc = 0;
+              const uint32_t m = diff16(xv[j], tv[j], xc, tc);
+              if (m < 16) { mine = m; mj = (uint32_t)j; cc = (uint32_t)xc | ((uint32_t)tc << 8); }
+            }
           }
         }
         if (STATS && lane == 0) atomicAdd(&sc[31], 1ull);
-        uint64_t mask[kCoopJ];
+        uint64_t mask[kCoopJ], anyM[kCoopJ];
 #pragma unroll
-        for (uint32_t j = 0; j < kCoopJ; j++) mask[j] = __ballot(mine < 16 && mj == j);
+        for (uint32_t j = 0; j < kCoopJ; j++) {
+          mask[j] = __ballot(mine < 16 && mj == j);
+          anyM[j] = kAlignMemo ? __ballot((pm >> j) & 1) : 0ull;
+        }
         uint32_t fresh = 0;  // slots given a new lane this round
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) {
@@ -1130,7 +1191,40 @@ k_ms_walk2(Walk2Args A) {
               const uint32_t mm = (uint32_t)__shfl((int)mine, (int)f);
               const uint32_t c2 = (uint32_t)__shfl((int)cc, (int)f);
               const uint32_t rq = (uint32_t)__shfl((int)runT, (int)f);
+              // memo: the next mismatch after (piece j, thread f) in byte
+              // order (the same piece of f, a later thread's piece j, then
+              // a later piece), else the round's end, clean
+              uint32_t off2 = rq + 16u * 16u * kCoopJ, c2b = 0;
+              if (kAlignMemo) {
+                const uint32_t m2f = (uint32_t)__shfl((int)mine2, (int)f);
+                const uint32_t c2f = (uint32_t)__shfl((int)cc2, (int)f);
+                if (m2f < 16) {
+                  off2 = rq + 16 * ((f - (q << 4)) + (j << 4)) + m2f;
+                  c2b = c2f | 0x10000u;
+                } else {
+                  uint32_t j2 = j, f2 = 64;
+                  const uint64_t later = anyM[j] & sm & ~((2ull << f) - 1);
+                  if (later) {
+                    f2 = (uint32_t)__builtin_ctzll(later);
+                  } else {
+#pragma unroll
+                    for (uint32_t jj = 0; jj < kCoopJ; jj++)
+                      if (jj > j && f2 == 64 && (anyM[jj] & sm)) { j2 = jj; f2 = (uint32_t)__builtin_ctzll(anyM[jj] & sm); }
+                  }
+                  if (f2 < 64) {  // (f2's first mismatch is in piece j2: an earlier one would precede (j, f))
+                    off2 = rq + 16 * ((f2 - (q << 4)) + (j2 << 4)) + (uint32_t)__shfl((int)mine, (int)f2);
+                    c2b = (uint32_t)__shfl((int)cc, (int)f2) | 0x10000u;
+                  }
+                }
+              }
               if (lane == Ls[q]) {
+                if (kAlignMemo) {
+                  const uint32_t base = i + len;  // text index of this slot's byte 0
+                  amAlign = pos - i;
+                  amLo = base + rq + 16 * ((f - (q << 4)) + (j << 4)) + mm + 1;
+                  amFront = base + off2;
+                  amC = c2b;
+                }
                 len += rq + 16 * ((f - (q << 4)) + (j << 4)) + mm;
                 smaller = (int8_t)(uint8_t)c2 > (int8_t)(uint8_t)(c2 >> 8);  // FN:55
                 phase = PC_POST;
@@ -1188,7 +1282,7 @@ k_ms_walk2(Walk2Args A) {
           for (uint32_t j = 0; j < JR; j++) {
             const uint32_t o = run + 16 * (k + (j << lgW));
             xv[j] = ldu16(xa + o);
-            tv[j] = ldu16_nt(ta + o);
+            tv[j] = CMSBWT_COOP_TEXT_NT ? ldu16_nt(ta + o) : ldu16(ta + o);
           }
 #pragma unroll
           for (int j = (int)JR - 1; j >= 0; j--) {
