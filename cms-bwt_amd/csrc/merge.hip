@@ -1158,6 +1158,13 @@ constexpr uint32_t kTgtRec = TGT_REC;   // item records staged per chunk
 constexpr uint32_t kTgtQ = 256;     // undecided queries listed per wave before a search pass
 constexpr uint32_t kTgtS = 256;     // queries listed per wave for binary searches
 constexpr uint32_t kNoSlot = 0xffffffffu;
+// a staged record covering all 64 targets of its wave carries this range word
+// (no window-relative range is 0xffff..ffff) and skips the range test
+#ifndef CMSBWT_TGT_FULL
+#define CMSBWT_TGT_FULL 1
+#endif
+constexpr bool kTgtFull = CMSBWT_TGT_FULL != 0;
+constexpr uint32_t kFullRec = 0xffffffffu;
 
 // v (wave-uniform) in the lanes of mask m, 0 elsewhere: one v_cndmask on the
 // SGPR-pair mask (keeps decision masks out of VGPRs)
@@ -1221,13 +1228,14 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
   }
   const bool hasF0 = fs0 != kNoSlot, hasF1 = fs1 != kNoSlot, hasF2 = fs2 != kNoSlot;
   const uint64_t hasF1M = __ballot(hasF1);  // per wave
+  const uint64_t hasF0M = __ballot(hasF0);  // (an F item implies items: in-range F lanes = in-range lanes & hasF0M)
+  const uint64_t hasM = __ballot(has);
   const uint32_t flags = (hasF0 ? 1u : 0u) | (hasF1 ? 2u : 0u) | (hasF2 ? 4u : 0u) | (nS3 ? 8u : 0u) |
                          (nF3 ? 16u : 0u) | (nS8 << 8) | (nF8 << 16);
   for (uint32_t k = 0; k < 6; k++) accL[k][tid] = 0;
   // lanes without items never fall in a record's range (their pairs are
   // counted once per staged record: counterDoNothing, FN:1530)
   const uint32_t tofH = has ? toff : 0x40000000u;
-  const uint32_t tofF = hasF0 ? toff : 0x40000000u;  // (an F item implies items)
   {
     const uint64_t hm = __ballot(has);
     if (lane == 0) noItL[wv] = ~hm;
@@ -1282,9 +1290,15 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
     const uint32_t ab = __builtin_amdgcn_readlane(my.y, e);
     const uint32_t cqv = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(my.z, e));
     const uint32_t L = __builtin_amdgcn_readlane(my.x, e) - t;
-    const uint32_t aO = ab & 0xffffu, span = ab >> 16;
-    const uint64_t mIn = ucmp<kULE>(tofH - aO, span);    // targets with items
-    const uint64_t mInF = ucmp<kULE>(tofF - aO, span);   // ... and a smaller=false item
+    uint64_t mIn, mInF;
+    if (kTgtFull && ab == kFullRec) {  // the record reaches all 64 targets of the wave: no range test
+      mIn = hasM;
+      mInF = hasF0M;
+    } else {
+      const uint32_t aO = ab & 0xffffu, span = ab >> 16;
+      mIn = ucmp<kULE>(tofH - aO, span);  // targets with items
+      mInF = mIn & hasF0M;                // ... and a smaller=false item
+    }
     uint64_t mF0, mX, msl;
     if (S) {  // smaller=true: S items ascending, then F items
       const uint64_t m1 = ucmp<kUGT>(L, sl0) & ucmp<kNE>(L, fl0);  // past every S item: f (or end)
@@ -1302,7 +1316,7 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
       msl = mIn & ~(m1 | m2);
     }
     aF0 += sel_u32(cqv, mF0);
-    nGood = addc_mask(addc_mask(nGood, mF0), mX);
+    nGood = addc_mask(nGood, mF0 | mX);  // (disjoint masks)
     if (msl) {
       if ((msl >> lane) & 1) {
         const uint32_t rk =
@@ -1420,7 +1434,8 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
             const uint32_t a = k == (aO >> 6) ? (aO & 63u) : 0u, b = k == (bO >> 6) ? (bO & 63u) : 63u;
             nNothing += (uint32_t)__popcll(noItL[k] & (~0ull >> (63u - b)) & (~0ull << a));
             const uint32_t o = atomicAdd(&nG[2 * k + (sm ? 0 : 1)], 1u);
-            recG[k][sm ? o : kTgtRec - 1 - o] = rec;
+            const bool full = kTgtFull && aO <= 64 * k && bO >= 64 * k + 63;
+            recG[k][sm ? o : kTgtRec - 1 - o] = full ? make_uint4(rec.x, kFullRec, rec.z, rec.w) : rec;
           }
         }
       }

@@ -7,9 +7,9 @@ mkdir -p gpurun_out
 timeout -k 10 300 python -u -m pytest tests/test_gpu_sharded.py tests/test_gpu_cli_multi.py -x -v -k "labels_past" --timeout 240 --timeout-method thread > gpurun_out/r04_bias.log 2>&1 || { tail -60 gpurun_out/r04_bias.log; exit 1; }
 tail -1 gpurun_out/r04_bias.log
 lib() { case $1 in new) echo cms-bwt_amd/build/libcmsbwt.so;; *) echo exp/$1/libcmsbwt.so;; esac; }
-for v in new memo tnt refill base new memo tnt refill base; do
+for v in new memo tnt cbase refill base new memo tnt cbase refill base; do
   CMSBWT_LIB=$(lib $v) timeout -k 10 240 python -u bench.py --steps 10 --warmup 2 --no-cpu --no-e2e > gpurun_out/r04c_ab_$v.log 2>&1 || { tail -30 gpurun_out/r04c_ab_$v.log; exit 1; }
-  echo "$v $(tail -1 gpurun_out/r04c_ab_$v.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); s=d["stages_ms"]; print(d["ms_per_step"], s["ms_walk"], s["ms_walk_kernel"], d["parity"]["verdict"])')"
+  echo "$v $(tail -1 gpurun_out/r04c_ab_$v.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); s=d["stages_ms"]; print(d["ms_per_step"], s["ms_walk"], s["ms_walk_kernel"], s["counter_kernel"], d["parity"]["verdict"])')"
 done
 CMSBWT_W2_STATS=1 timeout -k 10 240 python -u bench.py --steps 1 --warmup 0 --no-cpu --no-e2e --no-check > gpurun_out/r04c_stats_new.log 2>&1 || { tail -30 gpurun_out/r04c_stats_new.log; exit 1; }
 grep -E "w2stats" gpurun_out/r04c_stats_new.log | tail -30
