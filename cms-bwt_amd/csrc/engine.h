@@ -468,19 +468,30 @@ struct Engine {
     for (auto v : lvlLen) total += pad(v);
     dlcp.alloc(total);
     dlcp.zero(st);
+    const bool saTm = env_u32("CMSBWT_TIMING", 0) != 0;
+    auto saMark = [&](const char* what, uint64_t v) {
+      if (!saTm) return;
+      sync();
+      fprintf(stderr, "[index]   %-12s %.3f s  (%llu)\n", what, std::chrono::duration<double>(now() - t0).count(),
+              (unsigned long long)v);
+    };
     {  // SA by prefix doubling
       DBuf<unsigned long long> k0, k1;
       DBuf<uint32_t> v0, v1, rank, headIn, head, tie, act, act2;
       k0.alloc(n); k1.alloc(n); v0.alloc(n); v1.alloc(n);
       rank.alloc(n); headIn.alloc(n); head.alloc(n); tie.alloc(n); act.alloc(n); act2.alloc(n);
+      saMark("alloc", n);
       int32_t* sa = dsa.p;
       launch_ix_init(dx.p, n, k0.p, v0.p, st);
+      saMark("keys", n);
       sort_pairs(k0.p, k1.p, v0.p, v1.p, n, 9 * kIdxH0);
+      saMark("sort", n);
       launch_ix_heads(k1.p, nullptr, n, headIn.p, tie.p, st);
       inscan(headIn.p, head.p, n, rocprim::maximum<uint32_t>());
       launch_ix_place(v1.p, nullptr, head.p, n, sa, rank.p, st);
       mk_iota(act2.p, n, st);
       uint32_t U = select_flagged(act2.p, tie.p, act.p, n);
+      saMark("first sort", U);
       const int bits = 32 + bits_for(n);
       uint64_t h = kIdxH0;
       int rounds = 0;
@@ -494,6 +505,7 @@ struct Engine {
         U = select_flagged(act.p, tie.p, act2.p, U);
         act.swap_in(act2);
         h <<= 1;
+        saMark("round", U);
       }
     }
     sync();

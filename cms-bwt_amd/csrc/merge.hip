@@ -1161,7 +1161,7 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 // a staged record covering all 64 targets of its wave carries this range word
 // (no window-relative range is 0xffff..ffff) and skips the range test
 #ifndef CMSBWT_TGT_FULL
-#define CMSBWT_TGT_FULL 1
+#define CMSBWT_TGT_FULL 0  // r04 A/B: 12.56-12.58 ms without, 12.67-12.73 ms with (the uniform branch costs more)
 #endif
 constexpr bool kTgtFull = CMSBWT_TGT_FULL != 0;
 constexpr uint32_t kFullRec = 0xffffffffu;

@@ -314,7 +314,7 @@ constexpr bool kProbeNoSkip = CMSBWT_PROBE_NOSKIP != 0;
 // offset after the SNP (the copy's next long match) starts there instead of
 // reading those bytes again (CMSBWT_ALIGN_MEMO=1)
 #ifndef CMSBWT_ALIGN_MEMO
-#define CMSBWT_ALIGN_MEMO 0
+#define CMSBWT_ALIGN_MEMO 1
 #endif
 constexpr bool kAlignMemo = CMSBWT_ALIGN_MEMO != 0;
 // waves per SIMD of the walk (Makefile W2WAVES; measured 3 -> 16.50 ms,
@@ -349,6 +349,11 @@ k_ms_walk2(Walk2Args A) {
   const bool pfxExact = FAST || R.pfxExact != 0;
   const bool hasLd = FAST || R.ld != nullptr;
   const bool hasIr = FAST || R.ir != nullptr;
+  // the alignment memo in the specialised instance only: in the generic one
+  // (95 SGPRs spilled to VGPR lanes) it changed results on a raw reference
+  // with N (tests/test_gpu_parity.py raw_reference_with_N) while a build with
+  // extra checking code did not -- kept out there until understood
+  const bool memo = kAlignMemo && FAST;
   const Lv V{lvlL, lvlL + kMaxLevels, R.nlvl, (int32_t)R.n, R.lcp};
   const uint32_t n = R.n;
   const uintptr_t X = (uintptr_t)R.x;
@@ -561,7 +566,7 @@ k_ms_walk2(Walk2Args A) {
   // FN:52-62 from (pos, len): 16 bytes of x and of the text, unless the
   // alignment memo already knows where this offset's match ends
   auto start_lce = [&]() {
-    if (kAlignMemo && pos - i == amAlign && i + len >= amLo && i + len <= amFront) {
+    if (memo && pos - i == amAlign && i + len >= amLo && i + len <= amFront) {
       len = amFront - i;
       if (amC & 0x10000u) {  // the mismatch at amFront (FN:55)
         smaller = (int8_t)(uint8_t)amC > (int8_t)(uint8_t)(amC >> 8);
@@ -1160,7 +1165,7 @@ k_ms_walk2(Walk2Args A) {
           }
 #pragma unroll
           for (int j = (int)kCoopJ - 1; j >= 0; j--) {
-            if (kAlignMemo) {
+            if (memo) {
               uint32_t m1, c1, m2, c2;
               diff16x2(xv[j], tv[j], m1, c1, m2, c2);
               if (m1 < 16) { mine = m1; mj = (uint32_t)j; cc = c1; mine2 = m2; cc2 = c2; pm |= 1u << j; }
@@ -1176,7 +1181,7 @@ k_ms_walk2(Walk2Args A) {
 #pragma unroll
         for (uint32_t j = 0; j < kCoopJ; j++) {
           mask[j] = __ballot(mine < 16 && mj == j);
-          anyM[j] = kAlignMemo ? __ballot((pm >> j) & 1) : 0ull;
+          anyM[j] = memo ? __ballot((pm >> j) & 1) : 0ull;
         }
         uint32_t fresh = 0;  // slots given a new lane this round
 #pragma unroll
@@ -1195,7 +1200,7 @@ k_ms_walk2(Walk2Args A) {
               // order (the same piece of f, a later thread's piece j, then
               // a later piece), else the round's end, clean
               uint32_t off2 = rq + 16u * 16u * kCoopJ, c2b = 0;
-              if (kAlignMemo) {
+              if (memo) {
                 const uint32_t m2f = (uint32_t)__shfl((int)mine2, (int)f);
                 const uint32_t c2f = (uint32_t)__shfl((int)cc2, (int)f);
                 if (m2f < 16) {
@@ -1211,14 +1216,16 @@ k_ms_walk2(Walk2Args A) {
                     for (uint32_t jj = 0; jj < kCoopJ; jj++)
                       if (jj > j && f2 == 64 && (anyM[jj] & sm)) { j2 = jj; f2 = (uint32_t)__builtin_ctzll(anyM[jj] & sm); }
                   }
-                  if (f2 < 64) {  // (f2's first mismatch is in piece j2: an earlier one would precede (j, f))
+                  if (f2 == f) {  // f's own later piece: its first mismatch there is not kept; clean up to it
+                    off2 = rq + 16 * ((f - (q << 4)) + (j2 << 4));
+                  } else if (f2 < 64) {  // (f2 != f: its first mismatch is in piece j2, an earlier one would precede (j, f))
                     off2 = rq + 16 * ((f2 - (q << 4)) + (j2 << 4)) + (uint32_t)__shfl((int)mine, (int)f2);
                     c2b = (uint32_t)__shfl((int)cc, (int)f2) | 0x10000u;
                   }
                 }
               }
               if (lane == Ls[q]) {
-                if (kAlignMemo) {
+                if (memo) {
                   const uint32_t base = i + len;  // text index of this slot's byte 0
                   amAlign = pos - i;
                   amLo = base + rq + 16 * ((f - (q << 4)) + (j << 4)) + mm + 1;
@@ -1274,6 +1281,7 @@ k_ms_walk2(Walk2Args A) {
       uint32_t jr = S < kCoopJ ? S : kCoopJ;
       while (open) {
         uint32_t mine = 16, mj = 0, cc = 0;  // this thread's first mismatch: piece, offset, chars
+        uint32_t pm = 0, mine2 = 16, cc2 = 0;  // (memo) pieces with a mismatch; 2nd mismatch of piece mj
         // one round of JR pieces (fixed-size arrays: no register spills)
         auto cmp_round = [&](auto jrc) {
           constexpr uint32_t JR = decltype(jrc)::value;
@@ -1286,9 +1294,15 @@ k_ms_walk2(Walk2Args A) {
           }
 #pragma unroll
           for (int j = (int)JR - 1; j >= 0; j--) {
-            uint8_t xc = 0, tc = 0;
-            const uint32_t m = diff16(xv[j], tv[j], xc, tc);
-            if (m < 16) { mine = m; mj = (uint32_t)j; cc = (uint32_t)xc | ((uint32_t)tc << 8); }
+            if (memo) {
+              uint32_t m1, c1, m2, c2;
+              diff16x2(xv[j], tv[j], m1, c1, m2, c2);
+              if (m1 < 16) { mine = m1; mj = (uint32_t)j; cc = c1; mine2 = m2; cc2 = c2; pm |= 1u << j; }
+            } else {
+              uint8_t xc = 0, tc = 0;
+              const uint32_t m = diff16(xv[j], tv[j], xc, tc);
+              if (m < 16) { mine = m; mj = (uint32_t)j; cc = (uint32_t)xc | ((uint32_t)tc << 8); }
+            }
           }
         };
         if ((open >> g) & 1) {
@@ -1298,9 +1312,12 @@ k_ms_walk2(Walk2Args A) {
         }
         if (STATS && lane == 0) atomicAdd(&sc[31], 1ull);
         // per piece index j: threads whose first mismatch lies in piece j
-        uint64_t mask[kCoopJ];
+        uint64_t mask[kCoopJ], anyM[kCoopJ];
 #pragma unroll
-        for (uint32_t j = 0; j < kCoopJ; j++) mask[j] = __ballot(mine < 16 && mj == j);
+        for (uint32_t j = 0; j < kCoopJ; j++) {
+          mask[j] = __ballot(mine < 16 && mj == j);
+          anyM[j] = memo ? __ballot((pm >> j) & 1) : 0ull;
+        }
 #pragma unroll
         for (uint32_t q = 0; q < 4; q++) {
           if (q >= S || !((open >> q) & 1)) continue;
@@ -1312,7 +1329,41 @@ k_ms_walk2(Walk2Args A) {
               const uint32_t f = (uint32_t)__builtin_ctzll(hit);
               const uint32_t mm = (uint32_t)__shfl((int)mine, (int)f);
               const uint32_t c2 = (uint32_t)__shfl((int)cc, (int)f);
+              // memo (as in the refill loop): the next mismatch in byte order,
+              // else the round's end
+              uint32_t off2 = run + 16u * W * jr, c2b = 0;
+              if (memo) {
+                const uint32_t m2f = (uint32_t)__shfl((int)mine2, (int)f);
+                const uint32_t c2f = (uint32_t)__shfl((int)cc2, (int)f);
+                if (m2f < 16) {
+                  off2 = run + 16 * ((f - (q << lgW)) + (j << lgW)) + m2f;
+                  c2b = c2f | 0x10000u;
+                } else {
+                  uint32_t j2 = j, f2 = 64;
+                  const uint64_t later = anyM[j] & sm & ~((2ull << f) - 1);
+                  if (later) {
+                    f2 = (uint32_t)__builtin_ctzll(later);
+                  } else {
+#pragma unroll
+                    for (uint32_t jj = 0; jj < kCoopJ; jj++)
+                      if (jj > j && f2 == 64 && (anyM[jj] & sm)) { j2 = jj; f2 = (uint32_t)__builtin_ctzll(anyM[jj] & sm); }
+                  }
+                  if (f2 == f) {
+                    off2 = run + 16 * ((f - (q << lgW)) + (j2 << lgW));
+                  } else if (f2 < 64) {
+                    off2 = run + 16 * ((f2 - (q << lgW)) + (j2 << lgW)) + (uint32_t)__shfl((int)mine, (int)f2);
+                    c2b = (uint32_t)__shfl((int)cc, (int)f2) | 0x10000u;
+                  }
+                }
+              }
               if (lane == Ls[q]) {
+                if (memo) {
+                  const uint32_t base = i + len;
+                  amAlign = pos - i;
+                  amLo = base + run + 16 * ((f - (q << lgW)) + (j << lgW)) + mm + 1;
+                  amFront = base + off2;
+                  amC = c2b;
+                }
                 len += run + 16 * ((f - (q << lgW)) + (j << lgW)) + mm;
                 smaller = (int8_t)(uint8_t)c2 > (int8_t)(uint8_t)(c2 >> 8);  // FN:55
                 phase = PC_POST;
