@@ -4,11 +4,11 @@
 set -e
 cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 OUT=gpurun_out/prof; rm -rf $OUT; mkdir -p $OUT
-B="python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e"
+B="python3 bench.py --steps 3 --warmup 1 --no-cpu --no-e2e --no-check"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $OUT/kt -o kt --output-format csv -- $B > $OUT/kt.log 2>&1
 python3 tools/kstats.py $OUT/kt/kt_kernel_stats.csv > $OUT/kt_summary.txt
 python3 tools/launches.py $OUT/kt/kt_kernel_trace.csv > $OUT/launches.txt
-B1="python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e"
+B1="python3 bench.py --steps 1 --warmup 0 --no-cpu --no-e2e --no-check"
 i=0
 for grp in "FETCH_SIZE" "WRITE_SIZE" "TCC_EA0_RDREQ_sum TCC_EA0_WRREQ_sum TCC_HIT_sum TCC_MISS_sum" \
            "SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU SQ_WAVES" \
