@@ -159,3 +159,18 @@ def test_shard_bounds_split_at_document_ends(built, tmp_path, world):
         for k in range(world):
             got += cases.py_read_docs(body[b[k]:b[k + 1]])[0]
         assert got == want, (i, world, b)
+
+
+def test_walk_alignment_memo_search_replica(tmp_path):
+    """The alignment memo of the walk (ms_walk2.hip)
+    finds, in one cooperative round, the first mismatch and the next one (or
+    how far the bytes are clean) from per-thread differences and per-piece
+    ballots; a host replica of that search equals brute force on 200 k random
+    slots."""
+    import shutil
+    import subprocess
+    src = os.path.join(ROOT, "tools", "memo_check.cpp")
+    exe = str(tmp_path / "memo_check")
+    subprocess.run([shutil.which("g++") or "g++", "-O2", "-o", exe, src], check=True)
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0 and r.stdout.strip().endswith("bad 0"), r.stdout[-500:]
