@@ -266,7 +266,8 @@ struct Engine {
   uint32_t K = 0;
   DBuf<int32_t> T;
   DBuf<uint32_t> saT;
-  DBuf<uint8_t> bwtHeads;
+  DBuf<uint8_t> bwtHeads;  // parity copies only (CMSBWT_KEEP_STAGES)
+  DBuf<uint8_t> bwtSlot;   // the character before each head, by slot in head-rank order
   DBuf<unsigned long long> counter;
   DBuf<int64_t> bucket;
   DBuf<uint8_t> runs;
@@ -1911,6 +1912,9 @@ struct Engine {
       mk_slot_members(S, itemOfSlot.p, P.p, H, Pm.p, st);
     }
     const uint32_t* const PmP = IS.slotIsFirst ? P.p : Pm.p;
+    // first sa position of each item (the BWT characters' slot base)
+    DBuf<uint32_t> gItem;
+    gItem.alloc(K);
     {
       DBuf<uint32_t> rankBase, gBase;
       rankBase.alloc(n);
@@ -1918,7 +1922,7 @@ struct Engine {
       mk_pos_rank_base(posBegin.p, sSlot.p, disa.p, itemRankBase.p, headBase.p, n, E, keepT ? rankBase.p : nullptr,
                        gBase.p, st);
       mk_ranks_slot(S, itemOfSlot.p, PmP, H, rankBase.p, gBase.p, n, keepT ? T.p : nullptr, saT.p, grp.p, nullptr,
-                    st);
+                    st, gItem.p);
     }
     itemRankBase.release();
     keptT = keepT;
@@ -1991,8 +1995,15 @@ struct Engine {
     rthFL.alloc(2);
     HIPCHK(hipMemcpyAsync(rthFL.p, grp.p, 4, hipMemcpyDeviceToDevice, st));
     HIPCHK(hipMemcpyAsync(rthFL.p + 1, grp.p + (H - 1), 4, hipMemcpyDeviceToDevice, st));
-    bwtHeads.alloc(H);
-    mk_head_chars(saT.p, hChar.p, H, bwtHeads.p, st);
+    // BWTheads in head-rank order only for the parity copies: the writer
+    // reads the characters by slot, placed by k_nhr_rank below
+    if (keepT) {
+      bwtHeads.alloc(H);
+      mk_head_chars(saT.p, hChar.p, H, bwtHeads.p, st);
+    } else {
+      bwtHeads.release();
+    }
+    bwtSlot.alloc(H);
 
     // ---- next-head ranks, sorted per item (FN:1480-1494): small items by an
     // in-place insertion sort, large ones by one global (item, nhr) sort
@@ -2002,11 +2013,14 @@ struct Engine {
       const bool fused = !env_u32("CMSBWT_NHR_SORT", 0);  // 1: gather, then per-item insertion sorts
       {
         DBuf<uint32_t> nbi;
-        nbi.alloc(H);
-        if (fused) {  // gather + rank inside the item in one pass
-          mk_nhr_idx(grp.p, 1u, hNext.p, H, nbi.p, st);
-          mk_nhr_rank(PmP, nbi.p, itemOfSlot.p, H, nhr.p, st);
+        if (fused) {  // gather + rank inside the item in one pass, placing the characters
+          DBuf<uint4> rec;
+          rec.alloc(H);
+          mk_nhr_rec(grp.p, hNext.p, hChar.p, H, rec.p, st);
+          mk_nhr_rank(PmP, nullptr, itemOfSlot.p, H, nhr.p, st, rec.p, S.slot, gItem.p, bwtSlot.p);
         } else {
+          nbi.alloc(H);
+          mk_head_chars_slot(PmP, grp.p, hChar.p, S, itemOfSlot.p, gItem.p, H, bwtSlot.p, st);
           mk_nhr_slot(PmP, grp.p, 1u, hNext.p, H, nbi.p, nhr.p, st);
         }
       }
@@ -2092,6 +2106,7 @@ struct Engine {
       info1.alloc(n); info2.alloc(n);
       ElemIn ei{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, itemOfSlot.p, headBase.p, eBase.p, rOf.p, bwtHeads.p,
                 counter.p, cum.p, info1.p, info2.p, n, E, H, rle};
+      ei.bwtSlot = bwtSlot.p;
       mk_el_info(ei, st);
       DBuf<uint32_t> wruns, whl, wprev;
       DBuf<unsigned long long> wsym, wrunOff, wsymOff;

@@ -652,7 +652,8 @@ __global__ void k_pos_rank_base(const uint32_t* __restrict__ posBegin, const uin
 __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ itemOfSlot,
                              const uint32_t* __restrict__ Pm, uint32_t H, const uint32_t* __restrict__ rankBase,
                              const uint32_t* __restrict__ gBase, uint32_t n, int32_t* __restrict__ T,
-                             uint32_t* __restrict__ sa, uint32_t* __restrict__ grp, uint32_t* __restrict__ actv) {
+                             uint32_t* __restrict__ sa, uint32_t* __restrict__ grp, uint32_t* __restrict__ actv,
+                             uint32_t* __restrict__ gItem) {
   uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= H) return;
   const uint32_t q = itemOfSlot[s], idx = Pm[s];
@@ -662,9 +663,13 @@ __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ ite
     sa[1 + m] = idx;
     grp[idx] = 1 + m;
     if (actv) actv[s] = 0xffffffffu;
+    if (gItem && m == 0) gItem[q] = 1;
     return;
   }
   const uint32_t g = gBase[p] + sq;
+  // the item's members hold the sa positions g .. g + count - 1: its first
+  // head rank is g - 1 whatever the suffix sort does inside it
+  if (gItem && m == 0) gItem[q] = g;
   if (T) T[idx] = (int32_t)(rankBase[p] + q);  // rank2head: kept for parity copies only
   sa[g + m] = idx;
   grp[idx] = g;
@@ -679,6 +684,26 @@ __global__ void k_nhr_idx(const uint32_t* __restrict__ headRank, uint32_t sub, c
   uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= H) return;
   nbi[idx] = headRank[idx + nexthead[idx]] - sub;
+}
+// the character before each head at its slot in head-rank order (the
+// CMSBWT_NHR_SORT=1 path; the default places them inside k_nhr_rank)
+__global__ void k_head_chars_slot(const uint32_t* __restrict__ Pm, const uint32_t* __restrict__ grp,
+                                  const uint8_t* __restrict__ lchar, const ItemsSoA it,
+                                  const uint32_t* __restrict__ itemOfSlot, const uint32_t* __restrict__ gItem,
+                                  uint32_t H, uint8_t* __restrict__ bwtSlot) {
+  uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= H) return;
+  const uint32_t idx = Pm[s], q = itemOfSlot[s];
+  bwtSlot[it.slot[q] + grp[idx] - gItem[q]] = lchar[idx];
+}
+// per head in document order: (next-head rank, head rank, BWT character) for
+// k_nhr_rank's one gather per slot (the character then lands at its slot in
+// head-rank order, where the writer reads it; no BWTheads gather by rank)
+__global__ void k_nhr_rec(const uint32_t* __restrict__ grp, const uint16_t* __restrict__ nexthead,
+                          const uint8_t* __restrict__ lchar, uint32_t H, uint4* __restrict__ rec) {
+  uint32_t idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= H) return;
+  rec[idx] = make_uint4(grp[idx + nexthead[idx]] - 1, grp[idx] - 1, lchar[idx], 0u);
 }
 // BWTheads (FN:1471): the character before each head, in head-rank order
 __global__ void k_head_chars(const uint32_t* __restrict__ sa, const uint8_t* __restrict__ lchar, uint32_t H,
@@ -704,13 +729,27 @@ constexpr uint32_t kSmallSeg = 32;
 constexpr uint32_t kNhrBlock = 256, kNhrHalo = kSmallSeg + 1;  // the scans go kSmallSeg + 1 slots either way
 __global__ void __launch_bounds__(256) k_nhr_rank(const uint32_t* __restrict__ Pm, const uint32_t* __restrict__ nbi,
                                                   const uint32_t* __restrict__ itemOfSlot, uint32_t H,
-                                                  uint32_t* __restrict__ nhr) {
+                                                  uint32_t* __restrict__ nhr, const uint4* __restrict__ rec,
+                                                  const uint32_t* __restrict__ slot, const uint32_t* __restrict__ gItem,
+                                                  uint8_t* __restrict__ bwtSlot) {
   __shared__ uint32_t vL[kNhrBlock + 2 * kNhrHalo], qL2[kNhrBlock + 2 * kNhrHalo];
   const uint32_t s0 = blockIdx.x * kNhrBlock;
   const int64_t base = (int64_t)s0 - kNhrHalo;
+  // rec (one GPU): each block's own slots also place their head's character at
+  // slot[q] + rank - first rank of the item (FN:1468-1472)
   for (uint32_t i = threadIdx.x; i < kNhrBlock + 2 * kNhrHalo; i += blockDim.x) {
     const int64_t j = base + i;
-    if (j >= 0 && j < (int64_t)H) { vL[i] = nbi[Pm ? Pm[j] : (uint32_t)j]; qL2[i] = itemOfSlot[j]; }
+    if (j >= 0 && j < (int64_t)H) {
+      const uint32_t q = itemOfSlot[j];
+      qL2[i] = q;
+      if (rec) {
+        const uint4 w = rec[Pm[j]];
+        vL[i] = w.x;
+        if (i >= kNhrHalo && i < kNhrHalo + kNhrBlock) bwtSlot[slot[q] + w.y - (gItem[q] - 1)] = (uint8_t)w.z;
+      } else {
+        vL[i] = nbi[Pm ? Pm[j] : (uint32_t)j];
+      }
+    }
   }
   __syncthreads();
   const uint32_t s = s0 + threadIdx.x;
@@ -1632,6 +1671,8 @@ __global__ void k_el_info(const int32_t* __restrict__ sa, const uint8_t* __restr
     const int64_t b = bucket[p];
     if (b < 0 && nh) s0 = slot[posBegin[p]];
     j = ((unsigned long long)b & 0x00ffffffffffffffull) | ((unsigned long long)bwt[r] << 56);
+  } else if (E) {
+    s0 = slot[posBegin[n - 1]];  // the end phrases' item
   }
   info1[r] = make_uint4(elemBase[r], r == 0 ? E : nh, s0, hb);
   info2[r] = j;
@@ -2031,10 +2072,20 @@ void mk_pos_rank_base(const uint32_t* posBegin, const uint32_t* slot, const uint
 }
 void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
                    const uint32_t* rankBase, const uint32_t* gBase, uint32_t n, int32_t* T, uint32_t* sa,
-                   uint32_t* grp, uint32_t* actv, hipStream_t st) {
+                   uint32_t* grp, uint32_t* actv, hipStream_t st, uint32_t* gItem) {
   if (H)
     hipLaunchKernelGGL(k_ranks_slot, g1(H), dim3(256), 0, st, it, itemOfSlot, Pm, H, rankBase, gBase, n, T, sa, grp,
-                       actv);
+                       actv, gItem);
+}
+void mk_head_chars_slot(const uint32_t* Pm, const uint32_t* grp, const uint8_t* lchar, const ItemsSoA& it,
+                        const uint32_t* itemOfSlot, const uint32_t* gItem, uint32_t H, uint8_t* bwtSlot,
+                        hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_head_chars_slot, g1(H), dim3(256), 0, st, Pm, grp, lchar, it, itemOfSlot, gItem, H,
+                            bwtSlot);
+}
+void mk_nhr_rec(const uint32_t* grp, const uint16_t* nexthead, const uint8_t* lchar, uint32_t H, uint4* rec,
+                hipStream_t st) {
+  if (H) hipLaunchKernelGGL(k_nhr_rec, g1(H), dim3(256), 0, st, grp, nexthead, lchar, H, rec);
 }
 void mk_head_chars(const uint32_t* sa, const uint8_t* lchar, uint32_t H, uint8_t* bwtHeads, hipStream_t st) {
   if (H) hipLaunchKernelGGL(k_head_chars, g1(H), dim3(256), 0, st, sa, lchar, H, bwtHeads);
@@ -2050,9 +2101,9 @@ void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, uint32_t sub, con
   hipLaunchKernelGGL(k_nhr_slot, g1(H), dim3(256), 0, st, Pm, nbi, H, nhr);
 }
 void mk_nhr_rank(const uint32_t* Pm, const uint32_t* nbi, const uint32_t* itemOfSlot, uint32_t H, uint32_t* nhr,
-                 hipStream_t st) {
+                 hipStream_t st, const uint4* rec, const uint32_t* slot, const uint32_t* gItem, uint8_t* bwtSlot) {
   if (H) hipLaunchKernelGGL(k_nhr_rank, dim3((H + kNhrBlock - 1) / kNhrBlock), dim3(kNhrBlock), 0, st, Pm, nbi,
-                            itemOfSlot, H, nhr);
+                            itemOfSlot, H, nhr, rec, slot, gItem, bwtSlot);
 }
 // items of more than kSmallSeg members, for the big path
 __global__ void k_nhr_big_list(const ItemsSoA it, uint32_t K, uint32_t* __restrict__ bigList) {

@@ -45,9 +45,17 @@ void mk_slot_members(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint3
 void mk_pos_rank_base(const uint32_t* posBegin, const uint32_t* slot, const uint32_t* isaRef,
                       const uint32_t* itemRankBase, const uint32_t* headBase, uint32_t n, uint32_t E,
                       uint32_t* rankBase, uint32_t* gBase, hipStream_t st);
+// gItem (optional, K): the first sa position (= 1 + first head rank) of each item
 void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
                    const uint32_t* rankBase, const uint32_t* gBase, uint32_t n, int32_t* T, uint32_t* sa,
-                   uint32_t* grp, uint32_t* actv, hipStream_t st);
+                   uint32_t* grp, uint32_t* actv, hipStream_t st, uint32_t* gItem = nullptr);
+// the character before each head at slot[q] + rank - (gItem[q] - 1)
+void mk_head_chars_slot(const uint32_t* Pm, const uint32_t* grp, const uint8_t* lchar, const ItemsSoA& it,
+                        const uint32_t* itemOfSlot, const uint32_t* gItem, uint32_t H, uint8_t* bwtSlot,
+                        hipStream_t st);
+// per head in document order: (next-head rank, head rank, BWT character)
+void mk_nhr_rec(const uint32_t* grp, const uint16_t* nexthead, const uint8_t* lchar, uint32_t H, uint4* rec,
+                hipStream_t st);
 // nbi: H scratch words (next-head rank per head in document order)
 // headRank - sub = rank of each head (sub 1 with the final group labels)
 void mk_nhr_slot(const uint32_t* Pm, const uint32_t* headRank, uint32_t sub, const uint16_t* nexthead, uint32_t H,
@@ -58,8 +66,11 @@ void mk_nhr_idx(const uint32_t* headRank, uint32_t sub, const uint16_t* nexthead
 void mk_nhr_sort_small(const ItemsSoA& it, uint32_t K, uint32_t* nhr, uint32_t* bigList, hipStream_t st);
 // next-head rank of each slot's member ranked inside its item (items <= kSmallSeg);
 // nbi in document order read through Pm, or already in slot order (Pm null)
+// rec (with Pm): records of mk_nhr_rec instead of nbi; each slot also writes
+// its head's character at slot[q] + rank - (gItem[q] - 1) of bwtSlot
 void mk_nhr_rank(const uint32_t* Pm, const uint32_t* nbi, const uint32_t* itemOfSlot, uint32_t H, uint32_t* nhr,
-                 hipStream_t st);
+                 hipStream_t st, const uint4* rec = nullptr, const uint32_t* slot = nullptr,
+                 const uint32_t* gItem = nullptr, uint8_t* bwtSlot = nullptr);
 void mk_nhr_big_list(const ItemsSoA& it, uint32_t K, uint32_t* bigList, hipStream_t st);
 void mk_nhr_big_fill(const uint32_t* items, const uint32_t* off, uint32_t nb, const ItemsSoA& it, const uint32_t* nhr,
                      unsigned long long* key, uint32_t* slots, hipStream_t st);
