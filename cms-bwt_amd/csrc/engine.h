@@ -9,6 +9,21 @@
 //   merge ............ FN:1387-1416 grouping (radix sorts), FN:1432-1494 ranks
 //                      + suffix sort of the head string (prefix doubling),
 //                      FN:1504-1603 counters, FN:1618-1777 inversion + runs
+#ifndef CMSBWT_COUNTER_OVERLAP
+// 1: the counter runs on the side stream beside the ranks and the suffix
+// sort, equal-key queries answered afterwards (measured slower: 62.5 -> 89 ms
+// per step, the two chains slow each other down more than they overlap)
+#define CMSBWT_COUNTER_OVERLAP 0
+#endif
+#ifndef CMSBWT_MAIN_PRIO
+#define CMSBWT_MAIN_PRIO 0  // 1: the engine stream at the highest priority (side stream: default)
+#endif
+#ifndef CMSBWT_POS_SORT_BITS
+#define CMSBWT_POS_SORT_BITS 0  // 0: rocPRIM's default digits for the position sort
+#endif
+#ifndef CMSBWT_POS_SORT_IPT
+#define CMSBWT_POS_SORT_IPT 12
+#endif
 #include <stdarg.h>
 #include <stdio.h>
 #include <string.h>
@@ -121,6 +136,7 @@ struct InputError {
 // request of a similar size (all work runs on one stream, so stream order
 // makes reuse safe).  hipMalloc/hipFree of multi-GB buffers otherwise cost
 // tens of milliseconds per step.
+constexpr bool kCounterOverlap = CMSBWT_COUNTER_OVERLAP != 0;
 struct DevAlloc {
   std::multimap<uint64_t, void*> freeBlocks;
   std::unordered_map<void*, uint64_t> sizes;
@@ -225,6 +241,9 @@ static int bits_for(uint64_t v) {  // bits to represent values in [0, v]
 
 struct Engine {
   DevAlloc alloc;  // first member: destroyed last
+  // side-stream buffers (merge): a pool of their own, so a block the main
+  // stream may still read is never handed to side work inside one fork epoch
+  DevAlloc sideAlloc;
   int device = 0;
   hipStream_t st = nullptr;
   std::string err;
@@ -274,6 +293,35 @@ struct Engine {
   uint64_t nruns = 0;
   int lastRle = 1;
   DBuf<uint8_t> tmp;  // rocPRIM scratch
+  // Side stream of the merge: work off the main chain (the counter's windows
+  // beside the ranks and the suffix sort, the writer's inputs beside the
+  // counter) runs there concurrently.  Inside a Side scope every helper
+  // (scans, sorts, read-backs, scratch) follows st / tmp, which it swaps, and
+  // new buffers come from sideAlloc.  Buffers a side epoch hands to the main
+  // stream live until the merge's final synchronisation.
+  hipStream_t st2 = nullptr;
+  DBuf<uint8_t> tmp2;
+  hipEvent_t evFork[2] = {}, evJoin = nullptr;
+  struct Side {
+    Engine& e;
+    DevAlloc* prev;
+    Side(Engine& en, hipEvent_t fork) : e(en), prev(g_alloc) {
+      HIPCHK(hipStreamWaitEvent(e.st2, fork, 0));
+      std::swap(e.st, e.st2);
+      e.tmp.swap_in(e.tmp2);
+      g_alloc = &e.sideAlloc;
+    }
+    ~Side() {
+      std::swap(e.st, e.st2);
+      e.tmp.swap_in(e.tmp2);
+      g_alloc = prev;
+    }
+  };
+  // the main stream waits for everything enqueued on the side stream so far
+  void join_side() {
+    HIPCHK(hipEventRecord(evJoin, st2));
+    HIPCHK(hipStreamWaitEvent(st, evJoin, 0));
+  }
 
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   // merge phase marks for the reference's log timers: ranks start, doubling
@@ -284,7 +332,17 @@ struct Engine {
   explicit Engine(int dev) : device(dev) {
     g_alloc = &alloc;
     HIPCHK(hipSetDevice(dev));
+#if CMSBWT_MAIN_PRIO
+    // the main chain (ranks, suffix sort) before the side stream's counter
+    int least = 0, greatest = 0;
+    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    HIPCHK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest));
+#else
     HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+#endif
+    HIPCHK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
+    for (auto& e : evFork) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    HIPCHK(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
     HIPCHK(hipEventCreate(&ev0));
     HIPCHK(hipEventCreate(&ev1));
     for (auto& e : evm) HIPCHK(hipEventCreate(&e));
@@ -300,6 +358,9 @@ struct Engine {
     if (ev0) (void)hipEventDestroy(ev0);
     if (ev1) (void)hipEventDestroy(ev1);
     for (auto e : evm) if (e) (void)hipEventDestroy(e);
+    for (auto e : evFork) if (e) (void)hipEventDestroy(e);
+    if (evJoin) (void)hipEventDestroy(evJoin);
+    if (st2) { (void)hipStreamSynchronize(st2); (void)hipStreamDestroy(st2); }
     if (st) (void)hipStreamDestroy(st);
   }
 
@@ -1507,8 +1568,21 @@ struct Engine {
         auto kvIn = rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint32_t>(0u),
                                                      MakeHeadKV{h.len, h.isa, h.smaller, h.tonext});
         size_t b = 0;
+#if CMSBWT_POS_SORT_BITS
+        // wider digits: ceil(bN / bits) onesweep passes instead of ceil(bN / 8)
+        using PosCfg = rocprim::radix_sort_config<
+            rocprim::default_config, rocprim::default_config,
+            rocprim::radix_sort_onesweep_config<rocprim::kernel_config<256, 12>,
+                                                rocprim::kernel_config<256, CMSBWT_POS_SORT_IPT>,
+                                                CMSBWT_POS_SORT_BITS>>;
+        HIPCHK(rocprim::radix_sort_pairs<PosCfg>(nullptr, b, h.pos, posS.p, kvIn, kv.p, (size_t)H, 0u, (unsigned)bN,
+                                                 st));
+        HIPCHK(rocprim::radix_sort_pairs<PosCfg>(scratch(b), b, h.pos, posS.p, kvIn, kv.p, (size_t)H, 0u,
+                                                 (unsigned)bN, st));
+#else
         HIPCHK(rocprim::radix_sort_pairs(nullptr, b, h.pos, posS.p, kvIn, kv.p, (size_t)H, 0u, (unsigned)bN, st));
         HIPCHK(rocprim::radix_sort_pairs(scratch(b), b, h.pos, posS.p, kvIn, kv.p, (size_t)H, 0u, (unsigned)bN, st));
+#endif
         mk_pos_begin(posS.p, H, n, hb.p, st);
         // run buckets from the sorted heads: starts per position from hb,
         // ends counted in k_grp_seg (LDS histogram near the block's positions)
@@ -1654,6 +1728,11 @@ struct Engine {
   // counterSmallerThanHead (FN:1523-1603) over the target positions [P0, P1):
   // windows of positions whose slots fit the LDS budget, items reaching into a
   // window from the left in its crossing list (items before P0 included).
+  struct WinPlan {
+    bool tgt = false;
+    uint32_t nw = 0, ncross = 0, slotCap = 0;
+    DBuf<uint32_t> winStart, crossOff, crossList, wflag, wincl, crossCnt, itemOff, keyW, keyW2, valQ;
+  };
   void counter_phase(const ItemsSoA& S, uint32_t K, const uint32_t* posBegin, const uint32_t* posF,
                      const uint32_t* nhrP, unsigned long long* counterP, unsigned long long* cstatsP, uint32_t n,
                      uint32_t P0, uint32_t P1, bool check, const HostRoute* hr = nullptr) {
@@ -1668,54 +1747,75 @@ struct Engine {
       none = HostRoute{noneMask.p, noneAmb.p, nullptr, noneCnt.p, 0};
       hr = &none;
     }
-    // windows over reference positions
-    DBuf<uint32_t> wflag, wincl, winStart, crossCnt, crossOff, crossList;
-    wflag.alloc(n);
-    wincl.alloc(n);
+    WinPlan W;
+    win_prep(S, K, posBegin, n, P0, P1, check, cstatsP, W);
+    counter_run(W, S, posBegin, posF, nhrP, counterP, cstatsP, n, check, hr);
+    sync();
+    counter_time();
+  }
+  // the windows and crossing lists (one read-back: the crossing count)
+  void win_prep(const ItemsSoA& S, uint32_t K, const uint32_t* posBegin, uint32_t n, uint32_t P0, uint32_t P1,
+                bool check, unsigned long long* cstatsP, WinPlan& W) {
     // target-major kernel (default): windows of 256 targets, slots unbounded;
     // k_counter_win (checked queries, or CMSBWT_COUNTER_WIN=1): windows cut
     // by the LDS slot budget
-    const bool tgt = !check && !env_u32("CMSBWT_COUNTER_WIN", 0);
-    const uint32_t winPos = tgt ? std::max(1u, std::min(256u, env_u32("CMSBWT_TGTWIN", 256)))
-                                : std::min(1024u, env_u32("CMSBWT_WINPOS", 1024)),
-                   slotCap = std::min(3584u, env_u32("CMSBWT_WINSLOTS", 3584));  // kWinSlots (merge.hip)
-    mk_win_flags(posBegin, S.slot, n, P0, P1, std::max(1u, winPos), tgt ? 0xfffffffeu : slotCap, wflag.p, st);
-    inscan(wflag.p, wincl.p, n, rocprim::plus<uint32_t>());
-    const uint32_t nw = P1 > P0 ? read1(wincl.p + (n - 1)) : 0;
-    winStart.alloc((uint64_t)nw + 1);
-    mk_win_starts(wflag.p, wincl.p, n, winStart.p, st);
-    HIPCHK(hipMemcpyAsync(winStart.p + nw, &P1, 4, hipMemcpyHostToDevice, st));
-    wflag.release();
+    W.tgt = !check && !env_u32("CMSBWT_COUNTER_WIN", 0);
+    const uint32_t winPos = W.tgt ? std::max(1u, std::min(256u, env_u32("CMSBWT_TGTWIN", 256)))
+                                  : std::min(1024u, env_u32("CMSBWT_WINPOS", 1024));
+    W.slotCap = std::min(3584u, env_u32("CMSBWT_WINSLOTS", 3584));  // kWinSlots (merge.hip)
+    W.wincl.alloc(n);
+    if (W.tgt) {
+      // fixed windows of winPos targets: their starts and the inclusive
+      // window count of every position need no scan
+      W.nw = P1 > P0 ? (P1 - P0 + winPos - 1) / winPos : 0;
+      W.winStart.alloc((uint64_t)W.nw + 1);
+      mk_win_fixed(n, P0, P1, winPos, W.nw, W.wincl.p, W.winStart.p, st);
+    } else {
+      W.wflag.alloc(n);
+      mk_win_flags(posBegin, S.slot, n, P0, P1, std::max(1u, winPos), W.slotCap, W.wflag.p, st);
+      inscan(W.wflag.p, W.wincl.p, n, rocprim::plus<uint32_t>());
+      W.nw = P1 > P0 ? read1(W.wincl.p + (n - 1)) : 0;
+      W.winStart.alloc((uint64_t)W.nw + 1);
+      mk_win_starts(W.wflag.p, W.wincl.p, n, W.winStart.p, st);
+      mk_set_u32(W.winStart.p + W.nw, P1, st);
+    }
     // crossing lists: (window, item) pairs sorted by window
-    DBuf<uint32_t> itemOff, keyW, keyW2, valQ;
-    crossCnt.alloc(K);
-    itemOff.alloc(K);
-    mk_win_cross(S, K, wincl.p, n, crossCnt.p, nullptr, nullptr, nullptr, cstatsP + 4, 0, st);
-    exscan(crossCnt.p, itemOff.p, 0u, K);
-    const uint32_t ncross = K ? (uint32_t)sum2(itemOff.p + (K - 1), crossCnt.p + (K - 1)) : 0;
-    keyW.alloc(std::max<uint32_t>(ncross, 1));
-    keyW2.alloc(std::max<uint32_t>(ncross, 1));
-    valQ.alloc(std::max<uint32_t>(ncross, 1));
-    crossList.alloc(std::max<uint32_t>(ncross, 1));
-    mk_win_cross(S, K, wincl.p, n, crossCnt.p, itemOff.p, keyW.p, valQ.p, cstatsP + 4, 1, st);
-    sort_pairs(keyW.p, keyW2.p, valQ.p, crossList.p, ncross, bits_for(nw));
-    crossOff.alloc((uint64_t)nw + 1);
-    mk_win_cross_off(keyW2.p, ncross, nw, crossOff.p, st);
-    wincl.release();
+    W.crossCnt.alloc(K);
+    W.itemOff.alloc(K);
+    mk_win_cross(S, K, W.wincl.p, n, W.crossCnt.p, nullptr, nullptr, nullptr, cstatsP + 4, 0, st);
+    exscan(W.crossCnt.p, W.itemOff.p, 0u, K);
+    W.ncross = K ? (uint32_t)sum2(W.itemOff.p + (K - 1), W.crossCnt.p + (K - 1)) : 0;
+    W.keyW.alloc(std::max<uint32_t>(W.ncross, 1));
+    W.keyW2.alloc(std::max<uint32_t>(W.ncross, 1));
+    W.valQ.alloc(std::max<uint32_t>(W.ncross, 1));
+    W.crossList.alloc(std::max<uint32_t>(W.ncross, 1));
+    mk_win_cross(S, K, W.wincl.p, n, W.crossCnt.p, W.itemOff.p, W.keyW.p, W.valQ.p, cstatsP + 4, 1, st);
+    sort_pairs(W.keyW.p, W.keyW2.p, W.valQ.p, W.crossList.p, W.ncross, bits_for(W.nw));
+    W.crossOff.alloc((uint64_t)W.nw + 1);
+    mk_win_cross_off(W.keyW2.p, W.ncross, W.nw, W.crossOff.p, st);
+  }
+  // the counter kernel between ev0 and ev1 (no synchronisation; counter_time
+  // reads the duration once the stream has passed ev1)
+  void counter_run(WinPlan& W, const ItemsSoA& S, const uint32_t* posBegin, const uint32_t* posF,
+                   const uint32_t* nhrP, unsigned long long* counterP, unsigned long long* cstatsP, uint32_t n,
+                   bool check, const HostRoute* hr, EqList eq = EqList{}) {
     HIPCHK(hipEventRecord(ev0, st));
-    if (tgt)
-      mk_counter_tgt(S, posBegin, posF, nhrP, winStart.p, nw, crossOff.p, crossList.p, counterP, cstatsP, n, st);
+    if (eq.rec && !W.tgt) throw InputError{CMSBWT_EINTERNAL, "internal: equal-key listing needs the target-major counter"};
+    if (W.tgt)
+      mk_counter_tgt(S, posBegin, posF, nhrP, W.winStart.p, W.nw, W.crossOff.p, W.crossList.p, counterP, cstatsP,
+                     n, st, eq);
     else
-      mk_counter_win(S, posBegin, posF, nhrP, winStart.p, nw, crossOff.p, crossList.p, counterP, cstatsP, n,
-                     slotCap, check ? hr : nullptr, st);
+      mk_counter_win(S, posBegin, posF, nhrP, W.winStart.p, W.nw, W.crossOff.p, W.crossList.p, counterP, cstatsP,
+                     n, W.slotCap, check ? hr : nullptr, st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(ev1, st));
-    sync();
+    windows = W.nw;
+    crossings = W.ncross;
+  }
+  void counter_time() {
     float ms = 0;
     HIPCHK(hipEventElapsedTime(&ms, ev0, ev1));
     counter_kernel_ms = ms;
-    windows = nw;
-    crossings = ncross;
   }
 
   // ---- comparator-ambiguity fallback (map_replay.h)
@@ -1884,6 +1984,14 @@ struct Engine {
     if (keepT) exscan(itemsSA.p, itemRankBase.p, 0u, n);
     exscan(headsSA.p, headBase.p, 0u, n);
     itemsSA.release(); headsSA.release();
+    // The counter (FN:1523-1603) reads the items alone except for equal-key
+    // queries, which compare next-head ranks: it runs on the side stream
+    // beside the ranks and the head-string suffix sort, with those queries
+    // listed and answered once the ranks exist (k_counter_eq).  The writer's
+    // inputs that do not read the counters go there too.
+    counter.alloc((uint64_t)H + 1);
+    counter.zero(st);
+    HIPCHK(hipEventRecord(evFork[0], st));
     T.alloc((uint64_t)H + 1);
     saT.alloc((uint64_t)H + 1);
     DBuf<uint32_t> grp;
@@ -1915,6 +2023,8 @@ struct Engine {
     // first sa position of each item (the BWT characters' slot base)
     DBuf<uint32_t> gItem;
     gItem.alloc(K);
+    DBuf<uint8_t> unres;  // per sa position: member of an item with >= 2 heads
+    unres.alloc((uint64_t)H + 1);
     {
       DBuf<uint32_t> rankBase, gBase;
       rankBase.alloc(n);
@@ -1922,7 +2032,58 @@ struct Engine {
       mk_pos_rank_base(posBegin.p, sSlot.p, disa.p, itemRankBase.p, headBase.p, n, E, keepT ? rankBase.p : nullptr,
                        gBase.p, st);
       mk_ranks_slot(S, itemOfSlot.p, PmP, H, rankBase.p, gBase.p, n, keepT ? T.p : nullptr, saT.p, grp.p, nullptr,
-                    st, gItem.p);
+                    st, gItem.p, unres.p);
+    }
+    // (enqueued after the ranks: the host waits for the side stream's
+    // crossing count while the main stream ranks)
+    // ---- buckets (FN:1162-1171) and inversion (FN:1618-1628, done as a
+    // gather); writer elements: the E end phrases, then per SA rank its heads
+    // (or one element)
+    DBuf<int32_t> bcnt;
+    DBuf<uint32_t> wm, eBase, rOf;
+    DBuf<uint4> info1;
+    DBuf<unsigned long long> info2;
+    uint32_t V = 0;
+    auto writer_inputs = [&]() {
+      bucket.alloc(n);
+      bcnt.alloc(n);
+      inscan(diff.p, bcnt.p, n, rocprim::plus<int32_t>());
+      mk_bucket(bcnt.p, hasHead.p, n, bucket.p, st);
+      wm.alloc(n); eBase.alloc(n);
+      mk_el_count(headBase.p, n, E, H, wm.p, st);
+      exscan(wm.p, eBase.p, 0u, n);
+      const uint64_t V64 = sum2(eBase.p + (n - 1), wm.p + (n - 1));
+      if (V64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer elements"};
+      V = (uint32_t)V64;
+      rOf.alloc(V);
+      mk_el_rof(eBase.p, wm.p, n, rOf.p, st);
+      info1.alloc(n); info2.alloc(n);
+      ElemIn ei{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, itemOfSlot.p, headBase.p, eBase.p, rOf.p, nullptr,
+                nullptr, nullptr, info1.p, info2.p, n, E, H, rle};
+      mk_el_info(ei, st);
+    };
+    WinPlan wp;
+    DBuf<uint4> eqRec;
+    DBuf<unsigned long long> eqCnt;
+    EqList eql;
+    if (!check) {
+      Side sd(*this, evFork[0]);
+      win_prep(S, K, posBegin.p, n, 0, n, false, cstats.p, wp);
+      writer_inputs();
+    }
+    // (the slot-window kernel, CMSBWT_COUNTER_WIN=1, runs after the ranks)
+    const bool listed = !check && wp.tgt && kCounterOverlap;
+    if (listed) {
+      Side sd(*this, evFork[0]);
+      eql.cap = std::max<uint64_t>(1, std::min<uint64_t>(H, 1ull << 27));
+      eqRec.alloc(eql.cap);
+      eqCnt.alloc(1);
+      eqCnt.zero(st);
+      eql.rec = eqRec.p;
+      eql.cnt = eqCnt.p;
+      HIPCHK(hipEventRecord(evm[4], st));
+      counter_run(wp, S, posBegin.p, posF.p, nullptr, counter.p, cstats.p, n, false, nullptr, eql);
+      HIPCHK(hipEventRecord(evm[5], st));
     }
     itemRankBase.release();
     keptT = keepT;
@@ -1938,15 +2099,17 @@ struct Engine {
       DBuf<uint32_t> act, act2, val, val2, lab, labMax, keep;
       uint32_t U = 0;
       {
-        DBuf<uint32_t> cntR, offR;
-        cntR.alloc(n);
-        offR.alloc(n);
-        cntR.zero(st);
-        mk_act_count(posBegin.p, sCount.p, disa.p, n, cntR.p, st);
-        exscan(cntR.p, offR.p, 0u, n);
-        U = (uint32_t)sum2(offR.p + (n - 1), cntR.p + (n - 1));
+        // the flagged sa positions, ascending (k_ranks_slot's flags)
+        const uint32_t nf = H + 1, nt = sel_tiles(nf);
+        DBuf<uint32_t> tc, to;
+        tc.alloc(nt);
+        to.alloc(nt);
+        mk_sel_count8(unres.p, nf, tc.p, st);
+        exscan(tc.p, to.p, 0u, nt);
+        U = (uint32_t)sum2(to.p + (nt - 1), tc.p + (nt - 1));
         act.alloc(std::max<uint32_t>(U, 1)); act2.alloc(std::max<uint32_t>(U, 1));
-        mk_act_fill(posBegin.p, sSlot.p, sCount.p, disa.p, headBase.p, offR.p, n, act.p, st);
+        mk_sel_write_idx8(unres.p, nf, to.p, act.p, st);
+        unres.release();
       }
       DBuf<uint64_t> k64, k64b;
       val.alloc(U); val2.alloc(U); lab.alloc(U); labMax.alloc(U); keep.alloc(U);
@@ -2031,8 +2194,6 @@ struct Engine {
     HIPCHK(hipEventRecord(evm[3], st));
 
     // ---- counterSmallerThanHead (FN:1523-1603)
-    counter.alloc((uint64_t)H + 1);
-    counter.zero(st);
     uint64_t W = 0;
     // work volume (statistics only): sum of untilNext, read back with the
     // counter statistics
@@ -2043,10 +2204,30 @@ struct Engine {
       size_t b = 0;
       HIPCHK(rocprim::reduce(nullptr, b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
       HIPCHK(rocprim::reduce(scratch(b), b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
-      HIPCHK(hipEventRecord(evm[4], st));
-      if (!check) counter_phase(S, K, posBegin.p, posF.p, nhr.p, counter.p, cstats.p, n, 0, n, false);
-      HIPCHK(hipEventRecord(evm[5], st));
+      if (!check) {
+        join_side();
+        const uint64_t nEq = listed ? read1(eqCnt.p) : 0;
+        if (!listed) {
+          HIPCHK(hipEventRecord(evm[4], st));
+          counter_run(wp, S, posBegin.p, posF.p, nhr.p, counter.p, cstats.p, n, false, nullptr);
+          HIPCHK(hipEventRecord(evm[5], st));
+        } else if (nEq > eql.cap) {  // list overflow: the counter again, with the ranks
+          counter.zero(st);
+          HIPCHK(hipMemsetAsync(cstats.p, 0, 4 * 8, st));                // bad, good, nothing, violations
+          HIPCHK(hipMemsetAsync(cstats.p + 5, 0, 3 * 8, st));            // (errors stay)
+          HIPCHK(hipEventRecord(evm[4], st));
+          counter_run(wp, S, posBegin.p, posF.p, nhr.p, counter.p, cstats.p, n, false, nullptr);
+          HIPCHK(hipEventRecord(evm[5], st));
+        } else {
+          mk_counter_eq(eqRec.p, (uint32_t)nEq, nhr.p, counter.p, cstats.p, st);
+        }
+        eqListed = nEq;
+      } else {  // (checked counter below: timed on the host)
+        HIPCHK(hipEventRecord(evm[4], st));
+        HIPCHK(hipEventRecord(evm[5], st));
+      }
     }
+
     unsigned long long cs[8];
     uint64_t queryViol = 0;
     HIPCHK(hipMemcpyAsync(&W, wsum.p, 8, hipMemcpyDeviceToHost, st));
@@ -2058,10 +2239,24 @@ struct Engine {
     } else {
       HIPCHK(hipMemcpyAsync(cs, cstats.p, sizeof(cs), hipMemcpyDeviceToHost, st));
       sync();
+      counter_time();
     }
     if (env_u32("CMSBWT_COUNTER_STATS", 0))
-      fprintf(stderr, "[counter] bad %llu good %llu nothing %llu windows %u crossings %u searched %llu\n", cs[0], cs[1],
-              cs[2], windows, crossings, cs[5]);
+      fprintf(stderr, "[counter] bad %llu good %llu nothing %llu windows %u crossings %u searched %llu equal-key %llu\n",
+              cs[0], cs[1], cs[2], windows, crossings, cs[5], (unsigned long long)eqListed);
+    if (env_u32("CMSBWT_COUNTER_STATS", 0) >= 2) {
+      DBuf<unsigned long long> sh;
+      sh.alloc(40);
+      sh.zero(st);
+      mk_counter_shape(S, K, n, sh.p, st);
+      unsigned long long hs[40];
+      HIPCHK(hipMemcpyAsync(hs, sh.p, sizeof(hs), hipMemcpyDeviceToHost, st));
+      sync();
+      fprintf(stderr, "[counter shape] records %llu full %llu pairs %llu pairs-in-full %llu\n", hs[0], hs[1], hs[2],
+              hs[3]);
+      for (int b = 0; b < 32; b++)
+        if (hs[8 + b]) fprintf(stderr, "[counter shape] range 2^%d: pairs %llu\n", b, hs[8 + b]);
+    }
     stats.counter_bad = cs[0];
     stats.counter_good = cs[1];
     stats.counter_nothing = cs[2];
@@ -2072,42 +2267,19 @@ struct Engine {
     stats.counter_kernel_ms = counter_kernel_ms;
     stats.counter_work = W;
 
-    // ---- buckets (FN:1162-1171) and inversion (FN:1618-1628, done as a gather)
-    bucket.alloc(n);
-    {
-      DBuf<int32_t> cnt;
-      cnt.alloc(n);
-      inscan(diff.p, cnt.p, n, rocprim::plus<int32_t>());
-      mk_bucket(cnt.p, hasHead.p, n, bucket.p, st);
-    }
+    if (check) writer_inputs();
 
     // ---- writer (FN:1631-1777) as segments + run-length merge
     uint64_t Rn = 0, symbols = 0;
     DBuf<unsigned long long> runStart;
     DBuf<uint8_t> runChar;
     {
-      // elements: end phrases, then per SA rank its heads (or one element)
-      DBuf<uint32_t> m, eBase;
-      m.alloc(n); eBase.alloc(n);
-      mk_el_count(headBase.p, n, E, H, m.p, st);
-      exscan(m.p, eBase.p, 0u, n);
-      const uint64_t V64 = sum2(eBase.p + (n - 1), m.p + (n - 1));
-      if (V64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer elements"};
-      const uint32_t V = (uint32_t)V64;
-      DBuf<uint32_t> rOf;
-      rOf.alloc(V);
-      mk_el_rof(eBase.p, m.p, n, rOf.p, st);
-      m.release();
       DBuf<unsigned long long> cum;
       cum.alloc(H);
       inscan(rocprim::make_transform_iterator(counter.p, PlusOneU64()), cum.p, H, rocprim::plus<unsigned long long>());
-      DBuf<uint4> info1;
-      DBuf<unsigned long long> info2;
-      info1.alloc(n); info2.alloc(n);
       ElemIn ei{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, itemOfSlot.p, headBase.p, eBase.p, rOf.p, bwtHeads.p,
                 counter.p, cum.p, info1.p, info2.p, n, E, H, rle};
       ei.bwtSlot = bwtSlot.p;
-      mk_el_info(ei, st);
       DBuf<uint32_t> wruns, whl, wprev;
       DBuf<unsigned long long> wsym, wrunOff, wsymOff;
       wruns.alloc(V); whl.alloc(V); wprev.alloc(V); wsym.alloc(V); wrunOff.alloc(V); wsymOff.alloc(V);
@@ -2219,6 +2391,7 @@ struct Engine {
   float counter_kernel_ms = 0;
   bool keptT = false;  // rank2head written by the last merge
   uint32_t windows = 0, crossings = 0;
+  uint64_t eqListed = 0;  // equal-key counter queries answered after the ranks (last merge)
   bool orderInvariant = false;  // set by ms_walk (k_finalize), false for imported shards
   uint64_t W_work = 0;
 

@@ -27,7 +27,7 @@ CtxView ctx_view(const cmsbwt_ctx* c) {
   v.dmU = e.dm.U;
   v.dmLabelBias = e.dm.labelBias;
   v.stats = e.stats;
-  v.devicePeak = e.alloc.peak;
+  v.devicePeak = e.alloc.peak + e.sideAlloc.peak;
   return v;
 }
 void* ctx_alloc(cmsbwt_ctx* c, uint64_t bytes) {
@@ -228,7 +228,7 @@ int cmsbwt_walk_import(cmsbwt_ctx* ctx, uint64_t heads, uint64_t ndocs, uint64_t
 int cmsbwt_get_stats(const cmsbwt_ctx* ctx, cmsbwt_stats* out) {
   if (!ctx || !out) return CMSBWT_EARG;
   *out = ctx->e->stats;
-  out->device_peak_bytes = ctx->e->alloc.peak;
+  out->device_peak_bytes = ctx->e->alloc.peak + ctx->e->sideAlloc.peak;
   return CMSBWT_OK;
 }
 
@@ -396,6 +396,7 @@ int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path
     e.upload_file_end(false);
     cmsbwt::g_alloc = &e.alloc;
     e.alloc.trim();
+    e.sideAlloc.trim();
     rc = cmsbwt_load_reference_file(ctx, ref_path);
   }
   if (rc) {

@@ -440,37 +440,6 @@ __global__ void k_dbl_gstart(const uint64_t* __restrict__ key, uint32_t U, uint3
 // Unresolved members (items with >= 2 heads, end phrases excluded) in sa
 // position order, without a sort: per position p its count at rank ISA[p],
 // then each position writes its members' sa positions at its rank's offset.
-__global__ void k_act_count(const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ count,
-                            const uint32_t* __restrict__ isaRef, uint32_t n, uint32_t* __restrict__ cntR) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p + 1 >= n) return;  // position n-1: end phrases, ranked one by one
-  const uint32_t b = posBegin[p], e = posBegin[p + 1];
-  uint32_t c = 0;
-  for (uint32_t q = b; q < e; q++) {
-    const uint32_t k = count[q];
-    c += k >= 2 ? k : 0u;
-  }
-  if (c) cntR[isaRef[p]] = c;
-}
-__global__ void k_act_fill(const uint32_t* __restrict__ posBegin, const uint32_t* __restrict__ slot,
-                           const uint32_t* __restrict__ count, const uint32_t* __restrict__ isaRef,
-                           const uint32_t* __restrict__ headBase, const uint32_t* __restrict__ offR, uint32_t n,
-                           uint32_t* __restrict__ act) {
-  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
-  if (p + 1 >= n) return;
-  const uint32_t b = posBegin[p], e = posBegin[p + 1];
-  if (b == e) return;
-  const uint32_t r = isaRef[p];
-  uint32_t o = offR[r];
-  const uint32_t g0 = 1 + headBase[r] - slot[b];
-  for (uint32_t q = b; q < e; q++) {
-    const uint32_t k = count[q];
-    if (k < 2) continue;
-    const uint32_t g = g0 + slot[q];
-    for (uint32_t m = 0; m < k; m++) act[o++] = g + m;
-  }
-}
-
 // Group leaders (gflag) sort their group when it has <= maxSmall members;
 // members of larger groups are appended to bigList (group by group) for the
 // radix path (bigList[0] counts them).
@@ -653,9 +622,10 @@ __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ ite
                              const uint32_t* __restrict__ Pm, uint32_t H, const uint32_t* __restrict__ rankBase,
                              const uint32_t* __restrict__ gBase, uint32_t n, int32_t* __restrict__ T,
                              uint32_t* __restrict__ sa, uint32_t* __restrict__ grp, uint32_t* __restrict__ actv,
-                             uint32_t* __restrict__ gItem) {
+                             uint32_t* __restrict__ gItem, uint8_t* __restrict__ unres) {
   uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= H) return;
+  if (unres && s == 0) unres[0] = 0;  // sa position 0: the sentinel
   const uint32_t q = itemOfSlot[s], idx = Pm[s];
   const uint32_t sq = it.slot[q], m = s - sq, p = it.pos[q];
   if (p == n - 1) {  // end phrases: one rank each, in document order
@@ -663,6 +633,7 @@ __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ ite
     sa[1 + m] = idx;
     grp[idx] = 1 + m;
     if (actv) actv[s] = 0xffffffffu;
+    if (unres) unres[1 + m] = 0;
     if (gItem && m == 0) gItem[q] = 1;
     return;
   }
@@ -675,6 +646,7 @@ __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ ite
   grp[idx] = g;
   // unresolved members (items with >= 2 heads): their sa positions
   if (actv) actv[s] = it.count[q] >= 2 ? g + m : 0xffffffffu;
+  if (unres) unres[g + m] = it.count[q] >= 2 ? 1 : 0;
 }
 // next-head rank of each member, in slot order (FN:1480-1494): first per head
 // in document order (nexthead is small, so headRank[idx + nexthead] is read
@@ -727,7 +699,7 @@ constexpr uint32_t kSmallSeg = 32;
 // members, the rest keep their order here and are sorted by the big path).
 // Writes the item's members' ranks sorted (std::sort of idxs, FN:1492).
 constexpr uint32_t kNhrBlock = 256, kNhrHalo = kSmallSeg + 1;  // the scans go kSmallSeg + 1 slots either way
-__global__ void __launch_bounds__(256) k_nhr_rank(const uint32_t* __restrict__ Pm, const uint32_t* __restrict__ nbi,
+__global__ void __launch_bounds__(kNhrBlock) k_nhr_rank(const uint32_t* __restrict__ Pm, const uint32_t* __restrict__ nbi,
                                                   const uint32_t* __restrict__ itemOfSlot, uint32_t H,
                                                   uint32_t* __restrict__ nhr, const uint4* __restrict__ rec,
                                                   const uint32_t* __restrict__ slot, const uint32_t* __restrict__ gItem,
@@ -836,6 +808,7 @@ struct CounterArgs {
   uint32_t n;
   uint32_t slotCap;          // windows with more slots use global atomics
   HostRoute hr;              // CHECK only: targets answered by the host std::map replay
+  EqList eq;                 // k_counter_tgt before the next-head ranks: equal-key queries listed
 };
 
 struct QueryStats {  // per lane; a lane serves far fewer than 2^32 queries per window
@@ -865,7 +838,7 @@ __device__ __forceinline__ uint32_t d_lower_u64(const unsigned long long* a, uin
 template <bool CHECK, class View, class AddFn>
 __device__ __forceinline__ void d_counter_query_L(const View& V, uint32_t L, uint32_t qi, bool S, uint32_t cq,
                                                   uint32_t slq, uint32_t t, QueryStats& qs, AddFn add,
-                                                  const HostRoute* hr = nullptr) {
+                                                  const HostRoute* hr = nullptr, const EqList* eql = nullptr) {
   const uint32_t b0 = V.begin(t), b1 = V.begin(t + 1);
   if (b0 == b1) { qs.nothing++; return; }  // bucket >= 0: no heads at t (FN:1530)
   if (CHECK && hr->mask[t]) {  // answered by the host's std::map replay of t
@@ -914,6 +887,21 @@ __device__ __forceinline__ void d_counter_query_L(const View& V, uint32_t L, uin
   if (eq) {  // same key: FN:1537-1589
     const uint32_t co = V.slot(ans + 1) - so;
     const bool hasNext = ans + 1 < b1;
+    if (eql) {  // the next-head ranks do not exist yet: listed for k_counter_eq
+      // one atomic per wave for the lanes listing here (a single counter
+      // takes every listing of the grid)
+      const uint64_t am = __ballot(1);
+      const uint32_t lane = __lane_id(), leader = (uint32_t)__builtin_ctzll(am);
+      unsigned long long base = 0;
+      if (lane == leader) base = atomicAdd(eql->cnt, (unsigned long long)__popcll(am));
+      base = ((unsigned long long)__builtin_amdgcn_readlane((uint32_t)(base >> 32), leader) << 32) |
+             __builtin_amdgcn_readlane((uint32_t)base, leader);
+      const unsigned long long e =
+          base + __builtin_amdgcn_mbcnt_hi((uint32_t)(am >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)am, 0u));
+      if ((co | cq) >> 31) atomicAdd(eql->cnt, eql->cap + 1);  // not representable: overflow
+      else if (e < eql->cap) eql->rec[e] = make_uint4(slq, cq, so, co | (hasNext ? 0x80000000u : 0u));
+      return;
+    }
     const uint32_t* me = V.nhr + slq;
     const uint32_t* ot = V.nhr + so;
     if (me[cq - 1] < ot[0]) {
@@ -1203,6 +1191,8 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 #define CMSBWT_TGT_FULL 0  // r04 A/B: 12.56-12.58 ms without, 12.67-12.73 ms with (the uniform branch costs more)
 #endif
 constexpr bool kTgtFull = CMSBWT_TGT_FULL != 0;
+
+
 constexpr uint32_t kFullRec = 0xffffffffu;
 
 // v (wave-uniform) in the lanes of mask m, 0 elsewhere: one v_cndmask on the
@@ -1306,11 +1296,12 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
         qs.slow++;
         auto addG = [&](uint32_t s, uint32_t v) { atomicAdd(&A.counter[s], (unsigned long long)v); };
         const uint32_t nS = (fl >> 8) & 0xffu, nF = (fl >> 16) & 0xffu;
+        const EqList* eql = A.eq.rec ? &A.eq : nullptr;
         if (nS < 255u && nF < 255u) {
           const KnownView KV{&A.it, A.nhr, tq, fo - nS, fo + nF, fo};
-          d_counter_query_L<false>(KV, L, it.isa[q], S, rc.z & 0x7fffffffu, it.slot[q], tq, qs, addG);
+          d_counter_query_L<false>(KV, L, it.isa[q], S, rc.z & 0x7fffffffu, it.slot[q], tq, qs, addG, nullptr, eql);
         } else {
-          d_counter_query_L<false>(GV, L, it.isa[q], S, rc.z & 0x7fffffffu, it.slot[q], tq, qs, addG);
+          d_counter_query_L<false>(GV, L, it.isa[q], S, rc.z & 0x7fffffffu, it.slot[q], tq, qs, addG, nullptr, eql);
         }
       }
     }
@@ -1365,12 +1356,61 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
       qn += (uint32_t)__popcll(msl);
     }
   };
+  // search pass over the listed queries, 64 at a time: first the three
+  // longest items of the class, read from the target's owning lane
+  // (ds_bpermute); what they do not settle goes to the wave's search list,
+  // binary-searched 64 at a time
+  auto retest = [&](auto cls, uint32_t qn) {
+    constexpr bool S = decltype(cls)::value;
+    __builtin_amdgcn_wave_barrier();
+    for (uint32_t d = 0; d < qn; d += 64) {
+      const bool act = d + lane < qn;
+      const uint32_t en = act ? myQ[d + lane] : 0u;
+      const int own = (int)((en >> 16) & 63u);
+      const uint32_t o0 = __shfl(S ? sl0 : fl0, own), o1 = __shfl(S ? sl1 : fl1, own);
+      const uint32_t o2 = __shfl(S ? sl2 : fl2, own), of0 = __shfl(fl0, own);
+      const uint32_t fl = __shfl(flags, own);
+      uint32_t dst = 6;  // 0 f, 1..3 S top 0..2, 4..5 F items 1..2; 6 end / none; 7 search
+      uint32_t cq = 0;
+      if (act) {
+        const uint4 rc = myR[en & 0xffffu];
+        const uint32_t L = rc.x - (T0 + (en >> 16));
+        cq = rc.z & 0x7fffffffu;
+        const bool g0 = L < o0, g1 = L < o1, g2 = L < o2;
+        const bool ne = (L != o0) & (L != o1) & (L != o2);
+        dst = 7;
+        if (S) {
+          if (!g0 & ne) dst = (fl & 1u) ? ((L != of0) ? 0u : 7u) : 6u;
+          else if (g0 & !g1 & ne) dst = 1;
+          else if (g1 & !g2 & ne) dst = 2;
+          else if (g2 & ne & ((fl & 8u) != 0)) dst = 3;
+        } else {
+          if (!g0 & ne) dst = (fl & 1u) ? 0u : 6u;
+          else if (g0 & !g1 & ne) dst = (fl & 2u) ? 4u : 6u;
+          else if (g1 & !g2 & ne) dst = (fl & 4u) ? 5u : 6u;
+          else if (g2 & ne & ((fl & 16u) != 0)) dst = 6;
+        }
+        if (dst < 6) {
+          atomicAdd(&accL[dst][en >> 16], cq);
+          qs.good++;
+        }
+      }
+      const uint64_t smS = __ballot(dst == 7);
+      if (dst == 7) {
+        const uint32_t rk =
+            __builtin_amdgcn_mbcnt_hi((uint32_t)(smS >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)smS, 0u));
+        myS[nSearch + rk] = en | (S ? 0x80000000u : 0u);
+      }
+      nSearch += (uint32_t)__popcll(smS);
+      if (nSearch >= kTgtS - 64) search();
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
   // one walk over a wave's records of one class (smaller=true records from
   // the front of its list, smaller=false ones from the back)
   auto walk = [&](auto cls, uint32_t rb, uint32_t re) {
-    constexpr bool S = decltype(cls)::value;
     uint32_t r = rb;
-    for (;;) {
+    while (r < re) {
       uint32_t qn = 0;  // listed undecided queries (wave-uniform)
       while (r < re && qn <= kTgtQ - 64) {
         const uint32_t nb = min(64u, re - r);
@@ -1388,54 +1428,7 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
         }
         r += e;
       }
-      if (qn == 0) break;  // (the walk is done: an empty list never stops it)
-      // search pass over the listed queries, 64 at a time: first the three
-      // longest items of the class, read from the target's owning lane
-      // (ds_bpermute); what they do not settle goes to the wave's search
-      // list, binary-searched 64 at a time
-      __builtin_amdgcn_wave_barrier();
-      for (uint32_t d = 0; d < qn; d += 64) {
-        const bool act = d + lane < qn;
-        const uint32_t en = act ? myQ[d + lane] : 0u;
-        const int own = (int)((en >> 16) & 63u);
-        const uint32_t o0 = __shfl(S ? sl0 : fl0, own), o1 = __shfl(S ? sl1 : fl1, own);
-        const uint32_t o2 = __shfl(S ? sl2 : fl2, own), of0 = __shfl(fl0, own);
-        const uint32_t fl = __shfl(flags, own);
-        uint32_t dst = 6;  // 0 f, 1..3 S top 0..2, 4..5 F items 1..2; 6 end / none; 7 search
-        uint32_t cq = 0;
-        if (act) {
-          const uint4 rc = myR[en & 0xffffu];
-          const uint32_t L = rc.x - (T0 + (en >> 16));
-          cq = rc.z & 0x7fffffffu;
-          const bool g0 = L < o0, g1 = L < o1, g2 = L < o2;
-          const bool ne = (L != o0) & (L != o1) & (L != o2);
-          dst = 7;
-          if (S) {
-            if (!g0 & ne) dst = (fl & 1u) ? ((L != of0) ? 0u : 7u) : 6u;
-            else if (g0 & !g1 & ne) dst = 1;
-            else if (g1 & !g2 & ne) dst = 2;
-            else if (g2 & ne & ((fl & 8u) != 0)) dst = 3;
-          } else {
-            if (!g0 & ne) dst = (fl & 1u) ? 0u : 6u;
-            else if (g0 & !g1 & ne) dst = (fl & 2u) ? 4u : 6u;
-            else if (g1 & !g2 & ne) dst = (fl & 4u) ? 5u : 6u;
-            else if (g2 & ne & ((fl & 16u) != 0)) dst = 6;
-          }
-          if (dst < 6) {
-            atomicAdd(&accL[dst][en >> 16], cq);
-            qs.good++;
-          }
-        }
-        const uint64_t smS = __ballot(dst == 7);
-        if (dst == 7) {
-          const uint32_t rk =
-              __builtin_amdgcn_mbcnt_hi((uint32_t)(smS >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)smS, 0u));
-          myS[nSearch + rk] = en | (S ? 0x80000000u : 0u);
-        }
-        nSearch += (uint32_t)__popcll(smS);
-        if (nSearch >= kTgtS - 64) search();
-      }
-      __builtin_amdgcn_wave_barrier();
+      if (qn) retest(cls, qn);
     }
   };
   for (uint32_t ch = 0; ch < nList; ch += kTgtRec) {
@@ -1502,6 +1495,27 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
   if (qs.slow) atomicAdd(&A.stats[5], (unsigned long long)qs.slow);
 }
 
+// statistics only (CMSBWT_COUNTER_STATS=2): per item, its target range cut
+// into 64-target groups; out: [0] records, [1] full records, [2] pairs,
+// [3] pairs in full records, [8 + b] pairs of items with 2^b <= range < 2^(b+1)
+__global__ void k_counter_shape(const ItemsSoA it, uint32_t K, uint32_t n, unsigned long long* __restrict__ out) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q >= K) return;
+  const uint32_t p = it.pos[q], u = it.until[q];
+  if (!u || p + 1 >= n) return;
+  const uint32_t lo = p + 1, hi = (uint32_t)min((uint64_t)p + u, (uint64_t)n - 1);
+  const uint32_t g0 = lo >> 6, g1 = hi >> 6, pr = hi - lo + 1;
+  uint32_t full = 0;
+  for (uint32_t g = g0; g <= g1; g++) full += (64 * g >= lo && 64 * g + 63 <= hi) ? 1u : 0u;
+  atomicAdd(&out[0], (unsigned long long)(g1 - g0 + 1));
+  atomicAdd(&out[1], (unsigned long long)full);
+  atomicAdd(&out[2], (unsigned long long)pr);
+  atomicAdd(&out[3], 64ull * full);
+  atomicAdd(&out[8 + (31 - __builtin_clz(pr))], (unsigned long long)pr);
+}
+void mk_counter_shape(const ItemsSoA& it, uint32_t K, uint32_t n, unsigned long long* out, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_counter_shape, dim3((K + 255) / 256), dim3(256), 0, st, it, K, n, out);
+}
 __global__ void k_item_sk(ItemsSoA it, uint32_t K) {
   uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q >= K) return;
@@ -1522,6 +1536,15 @@ __global__ void k_win_flags(const uint32_t* __restrict__ posBegin, const uint32_
   flag[p] = a != b ? 1u : 0u;
 }
 
+// fixed windows of winPos targets over [P0, P1): the inclusive window count
+// of every position (k_win_flags + scan of the general path) and the starts
+__global__ void k_win_fixed(uint32_t n, uint32_t P0, uint32_t P1, uint32_t winPos, uint32_t nw,
+                            uint32_t* __restrict__ wincl, uint32_t* __restrict__ winStart) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n) wincl[p] = p < P0 ? 0u : (p >= P1 ? nw : (p - P0) / winPos + 1);
+  if (p <= nw) winStart[p] = p < nw ? P0 + p * winPos : P1;
+}
+__global__ void k_set_u32(uint32_t* __restrict__ p, uint32_t v) { *p = v; }
 __global__ void k_win_starts(const uint32_t* __restrict__ flag, const uint32_t* __restrict__ winIncl, uint32_t n,
                              uint32_t* __restrict__ winStart) {
   uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
@@ -1904,7 +1927,8 @@ __global__ void k_count_distinct(const uint32_t* __restrict__ v, uint32_t K, uns
 // by wave ballots and writes the kept values (replaces rocprim::select, which
 // ran at ~1/8 of the bandwidth this needs).
 constexpr uint32_t kSelRows = 8, kSelTile = kSelRows * 256;
-__global__ void __launch_bounds__(256) k_sel_count(const uint32_t* __restrict__ flags, uint32_t n,
+template <class F>
+__global__ void __launch_bounds__(256) k_sel_count(const F* __restrict__ flags, uint32_t n,
                                                    uint32_t* __restrict__ tileCnt) {
   __shared__ uint32_t wc[4];
   const uint64_t t0 = (uint64_t)blockIdx.x * kSelTile;
@@ -1919,7 +1943,9 @@ __global__ void __launch_bounds__(256) k_sel_count(const uint32_t* __restrict__ 
   __syncthreads();
   if (threadIdx.x == 0) tileCnt[blockIdx.x] = wc[0] + wc[1] + wc[2] + wc[3];
 }
-__global__ void __launch_bounds__(256) k_sel_write(const uint32_t* __restrict__ in, const uint32_t* __restrict__ flags,
+// in == nullptr: the kept indices themselves
+template <class F>
+__global__ void __launch_bounds__(256) k_sel_write(const uint32_t* __restrict__ in, const F* __restrict__ flags,
                                                    uint32_t n, const uint32_t* __restrict__ tileOff,
                                                    uint32_t* __restrict__ out) {
   __shared__ uint32_t wc[kSelRows][4];
@@ -1941,7 +1967,8 @@ __global__ void __launch_bounds__(256) k_sel_write(const uint32_t* __restrict__ 
   for (uint32_t j = 0; j < kSelRows; j++) {
     uint32_t before = 0;
     for (uint32_t w = 0; w < wv; w++) before += wc[j][w];
-    if (keep[j]) out[base + before + rk[j]] = in[t0 + j * 256 + threadIdx.x];
+    const uint32_t e = (uint32_t)(t0 + j * 256 + threadIdx.x);
+    if (keep[j]) out[base + before + rk[j]] = in ? in[e] : e;
     base += wc[j][0] + wc[j][1] + wc[j][2] + wc[j][3];
   }
 }
@@ -2026,11 +2053,18 @@ void mk_scan_tiles(const uint32_t* in, uint32_t* out, uint64_t n, const uint32_t
 
 uint32_t sel_tiles(uint32_t n) { return (uint32_t)(((uint64_t)n + kSelTile - 1) / kSelTile); }
 void mk_sel_count(const uint32_t* flags, uint32_t n, uint32_t* tileCnt, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_sel_count, dim3(sel_tiles(n)), dim3(256), 0, st, flags, n, tileCnt);
+  if (n) hipLaunchKernelGGL(k_sel_count<uint32_t>, dim3(sel_tiles(n)), dim3(256), 0, st, flags, n, tileCnt);
 }
 void mk_sel_write(const uint32_t* in, const uint32_t* flags, uint32_t n, const uint32_t* tileOff, uint32_t* out,
                   hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_sel_write, dim3(sel_tiles(n)), dim3(256), 0, st, in, flags, n, tileOff, out);
+  if (n) hipLaunchKernelGGL(k_sel_write<uint32_t>, dim3(sel_tiles(n)), dim3(256), 0, st, in, flags, n, tileOff, out);
+}
+void mk_sel_count8(const uint8_t* flags, uint32_t n, uint32_t* tileCnt, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_sel_count<uint8_t>, dim3(sel_tiles(n)), dim3(256), 0, st, flags, n, tileCnt);
+}
+void mk_sel_write_idx8(const uint8_t* flags, uint32_t n, const uint32_t* tileOff, uint32_t* out, hipStream_t st) {
+  if (n)
+    hipLaunchKernelGGL(k_sel_write<uint8_t>, dim3(sel_tiles(n)), dim3(256), 0, st, nullptr, flags, n, tileOff, out);
 }
 
 
@@ -2072,10 +2106,10 @@ void mk_pos_rank_base(const uint32_t* posBegin, const uint32_t* slot, const uint
 }
 void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
                    const uint32_t* rankBase, const uint32_t* gBase, uint32_t n, int32_t* T, uint32_t* sa,
-                   uint32_t* grp, uint32_t* actv, hipStream_t st, uint32_t* gItem) {
+                   uint32_t* grp, uint32_t* actv, hipStream_t st, uint32_t* gItem, uint8_t* unres) {
   if (H)
     hipLaunchKernelGGL(k_ranks_slot, g1(H), dim3(256), 0, st, it, itemOfSlot, Pm, H, rankBase, gBase, n, T, sa, grp,
-                       actv, gItem);
+                       actv, gItem, unres);
 }
 void mk_head_chars_slot(const uint32_t* Pm, const uint32_t* grp, const uint8_t* lchar, const ItemsSoA& it,
                         const uint32_t* itemOfSlot, const uint32_t* gItem, uint32_t H, uint8_t* bwtSlot,
@@ -2167,14 +2201,6 @@ void mk_map_order(const uint32_t* posBegin, const uint32_t* len, const uint8_t* 
 void mk_dbl_gstart(const uint64_t* key, uint32_t U, uint32_t* flag, hipStream_t st) {
   if (U) hipLaunchKernelGGL(k_dbl_gstart, g1(U), dim3(256), 0, st, key, U, flag);
 }
-void mk_act_count(const uint32_t* posBegin, const uint32_t* count, const uint32_t* isaRef, uint32_t n, uint32_t* cntR,
-                  hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_act_count, g1(n), dim3(256), 0, st, posBegin, count, isaRef, n, cntR);
-}
-void mk_act_fill(const uint32_t* posBegin, const uint32_t* slot, const uint32_t* count, const uint32_t* isaRef,
-                 const uint32_t* headBase, const uint32_t* offR, uint32_t n, uint32_t* act, hipStream_t st) {
-  if (n) hipLaunchKernelGGL(k_act_fill, g1(n), dim3(256), 0, st, posBegin, slot, count, isaRef, headBase, offR, n, act);
-}
 void mk_dbl_rank(uint32_t U, const uint32_t* act, const uint64_t* key, const uint32_t* val, uint32_t* sa,
                  uint32_t* grp, uint32_t* keep, uint32_t* bigList, uint32_t maxSmall, hipStream_t st) {
   if (U) hipLaunchKernelGGL(k_dbl_rank, dim3((U + kDblBlock - 1) / kDblBlock), dim3(kDblBlock), 0, st, U, act, key, val,
@@ -2223,10 +2249,50 @@ void mk_counter_win(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t
 }
 void mk_counter_tgt(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
                     const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
-                    unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st) {
+                    unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st,
+                    EqList eq) {
   if (!nw) return;
-  CounterArgs A{it, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n, 0u, HostRoute{}};
+  CounterArgs A{it, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n, 0u, HostRoute{}, eq};
   hipLaunchKernelGGL(k_counter_tgt, dim3(nw), dim3(256), 0, st, A);
+}
+// FN:1537-1589 for the listed equal-key queries (the branch of
+// d_counter_query_L that reads the next-head ranks)
+__global__ void k_counter_eq(const uint4* __restrict__ rec, uint32_t m, const uint32_t* __restrict__ nhr,
+                             unsigned long long* __restrict__ counter, unsigned long long* __restrict__ stats) {
+  const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+  bool good = false, bad = false;
+  if (i < m) {
+    const uint4 r = rec[i];
+    const uint32_t slq = r.x, cq = r.y, so = r.z, co = r.w & 0x7fffffffu;
+    const bool hasNext = (r.w >> 31) != 0;
+    const uint32_t* me = nhr + slq;
+    const uint32_t* ot = nhr + so;
+    if (me[cq - 1] < ot[0]) {
+      atomicAdd(&counter[so], (unsigned long long)cq);
+      good = true;
+    } else if (me[0] > ot[co - 1]) {
+      if (hasNext) atomicAdd(&counter[so + co], (unsigned long long)cq);
+      good = true;
+    } else {
+      bad = true;
+      uint32_t rest = 0;
+      for (uint32_t a = 0; a < cq; a++) {
+        const uint32_t bpos = d_upper_u32(ot, 0, co, me[a]);
+        if (bpos < co) atomicAdd(&counter[so + bpos], 1ull);
+        else rest++;
+      }
+      if (rest && hasNext) atomicAdd(&counter[so + co], (unsigned long long)rest);
+    }
+  }
+  const uint64_t gm = __ballot(good), bm = __ballot(bad);
+  if ((threadIdx.x & 63) == 0) {
+    if (bm) atomicAdd(&stats[0], (unsigned long long)__popcll(bm));
+    if (gm) atomicAdd(&stats[1], (unsigned long long)__popcll(gm));
+  }
+}
+void mk_counter_eq(const uint4* rec, uint32_t m, const uint32_t* nhr, unsigned long long* counter,
+                   unsigned long long* stats, hipStream_t st) {
+  if (m) hipLaunchKernelGGL(k_counter_eq, dim3((m + 255) / 256), dim3(256), 0, st, rec, m, nhr, counter, stats);
 }
 __global__ void k_counter_adds(const uint32_t* __restrict__ slot, const unsigned long long* __restrict__ add, uint32_t m,
                                unsigned long long* __restrict__ counter) {
@@ -2257,6 +2323,13 @@ static ElemArgs elem_args(const ElemIn& w) {
   return ElemArgs{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.itemOfSlot, w.headBase, w.elemBase, w.rOf,
                   w.bwtHeads, w.counter, w.cum, w.info1, w.info2, w.n, w.E, w.H, w.rle, w.bwtSlot};
 }
+void mk_win_fixed(uint32_t n, uint32_t P0, uint32_t P1, uint32_t winPos, uint32_t nw, uint32_t* wincl,
+                  uint32_t* winStart, hipStream_t st) {
+  const uint64_t m = std::max<uint64_t>(n, (uint64_t)nw + 1);
+  hipLaunchKernelGGL(k_win_fixed, dim3((unsigned)((m + 255) / 256)), dim3(256), 0, st, n, P0, P1, winPos, nw, wincl,
+                     winStart);
+}
+void mk_set_u32(uint32_t* p, uint32_t v, hipStream_t st) { hipLaunchKernelGGL(k_set_u32, dim3(1), dim3(1), 0, st, p, v); }
 void mk_el_info(const ElemIn& w, hipStream_t st) {
   if (w.n) hipLaunchKernelGGL(k_el_info, g1(w.n), dim3(256), 0, st, w.sa, w.bwt, w.bucket, w.posBegin, w.slot,
                               w.headBase, w.elemBase, w.n, w.E, w.H, w.info1, w.info2);

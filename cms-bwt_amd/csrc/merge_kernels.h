@@ -45,14 +45,27 @@ void mk_slot_members(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint3
 void mk_pos_rank_base(const uint32_t* posBegin, const uint32_t* slot, const uint32_t* isaRef,
                       const uint32_t* itemRankBase, const uint32_t* headBase, uint32_t n, uint32_t E,
                       uint32_t* rankBase, uint32_t* gBase, hipStream_t st);
-// gItem (optional, K): the first sa position (= 1 + first head rank) of each item
+// gItem (optional, K): the first sa position (= 1 + first head rank) of each
+// item; unres (optional, H + 1): per sa position, 1 when its item has >= 2 heads
 void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
                    const uint32_t* rankBase, const uint32_t* gBase, uint32_t n, int32_t* T, uint32_t* sa,
-                   uint32_t* grp, uint32_t* actv, hipStream_t st, uint32_t* gItem = nullptr);
+                   uint32_t* grp, uint32_t* actv, hipStream_t st, uint32_t* gItem = nullptr,
+                   uint8_t* unres = nullptr);
+// byte-flag compaction into the kept indices (k_sel_count / k_sel_write)
+void mk_sel_count8(const uint8_t* flags, uint32_t n, uint32_t* tileCnt, hipStream_t st);
+void mk_sel_write_idx8(const uint8_t* flags, uint32_t n, const uint32_t* tileOff, uint32_t* out, hipStream_t st);
 // the character before each head at slot[q] + rank - (gItem[q] - 1)
 void mk_head_chars_slot(const uint32_t* Pm, const uint32_t* grp, const uint8_t* lchar, const ItemsSoA& it,
                         const uint32_t* itemOfSlot, const uint32_t* gItem, uint32_t H, uint8_t* bwtSlot,
                         hipStream_t st);
+// fixed counter windows of winPos targets over [P0, P1): inclusive window
+// count per position and the nw + 1 window starts
+void mk_win_fixed(uint32_t n, uint32_t P0, uint32_t P1, uint32_t winPos, uint32_t nw, uint32_t* wincl,
+                  uint32_t* winStart, hipStream_t st);
+// *p = v, stream-ordered (no host staging of a stack value)
+void mk_set_u32(uint32_t* p, uint32_t v, hipStream_t st);
+// statistics of the counter's (item, target) pairs (CMSBWT_COUNTER_STATS=2)
+void mk_counter_shape(const ItemsSoA& it, uint32_t K, uint32_t n, unsigned long long* out, hipStream_t st);
 // per head in document order: (next-head rank, head rank, BWT character)
 void mk_nhr_rec(const uint32_t* grp, const uint16_t* nexthead, const uint8_t* lchar, uint32_t H, uint4* rec,
                 hipStream_t st);
@@ -110,10 +123,6 @@ void mk_sel_write(const uint32_t* in, const uint32_t* flags, uint32_t n, const u
 void mk_map_order(const uint32_t* posBegin, const uint32_t* len, const uint8_t* sm, uint32_t n, uint32_t* order,
                   hipStream_t st);
 // per-group doubling round (small groups sorted by one thread each)
-void mk_act_count(const uint32_t* posBegin, const uint32_t* count, const uint32_t* isaRef, uint32_t n, uint32_t* cntR,
-                  hipStream_t st);
-void mk_act_fill(const uint32_t* posBegin, const uint32_t* slot, const uint32_t* count, const uint32_t* isaRef,
-                 const uint32_t* headBase, const uint32_t* offR, uint32_t n, uint32_t* act, hipStream_t st);
 void mk_dbl_small2(const uint32_t* gflag, uint32_t U, const uint32_t* act, uint64_t* key, uint32_t* val, uint32_t* sa,
                    uint32_t* grp, uint32_t* keep, uint32_t* bigList, uint32_t maxSmall, hipStream_t st);
 void mk_dbl_rank(uint32_t U, const uint32_t* act, const uint64_t* key, const uint32_t* val, uint32_t* sa,
@@ -143,6 +152,20 @@ struct HostRoute {
   unsigned long long* cnt = nullptr;
   unsigned long long cap = 0;
 };
+// Equal-key counter queries (FN:1537-1589: the answer compares next-head
+// ranks) listed by a counter pass that runs before the next-head ranks exist:
+// 16-byte records (query slot, query count, item slot, item count | hasNext
+// << 31).  cnt[0] counts every listing, so cnt[0] > cap means overflow (the
+// counter is then run again with the ranks).
+struct EqList {
+  uint4* rec = nullptr;
+  unsigned long long* cnt = nullptr;
+  unsigned long long cap = 0;
+};
+// the listed equal-key queries against the next-head ranks (adds and the
+// good / bad statistics of FN:1537-1589)
+void mk_counter_eq(const uint4* rec, uint32_t m, const uint32_t* nhr, unsigned long long* counter,
+                   unsigned long long* stats, hipStream_t st);
 void mk_counter_win(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
                     const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
                     unsigned long long* counter, unsigned long long* stats, uint32_t n, uint32_t slotCap,
@@ -153,9 +176,11 @@ void mk_counter_adds(const uint32_t* slot, const unsigned long long* add, uint32
 // mask[i] |= other[i]
 void mk_or_mask(uint8_t* mask, const uint8_t* other, uint32_t n, hipStream_t st);
 // target-major counter: windows of <= 256 targets (winStart), register accumulators
+// eq.rec != nullptr (nhr unused): equal-key queries are listed in eq
 void mk_counter_tgt(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
                     const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
-                    unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st);
+                    unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st,
+                    EqList eq = EqList{});
 void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st);
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st);
 // run writer: units = E end phrases + SA ranks 1..n-1 (sharded merge), or
