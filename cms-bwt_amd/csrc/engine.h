@@ -9,15 +9,6 @@
 //   merge ............ FN:1387-1416 grouping (radix sorts), FN:1432-1494 ranks
 //                      + suffix sort of the head string (prefix doubling),
 //                      FN:1504-1603 counters, FN:1618-1777 inversion + runs
-#ifndef CMSBWT_COUNTER_OVERLAP
-// 1: the counter runs on the side stream beside the ranks and the suffix
-// sort, equal-key queries answered afterwards (measured slower: 62.5 -> 89 ms
-// per step, the two chains slow each other down more than they overlap)
-#define CMSBWT_COUNTER_OVERLAP 0
-#endif
-#ifndef CMSBWT_MAIN_PRIO
-#define CMSBWT_MAIN_PRIO 0  // 1: the engine stream at the highest priority (side stream: default)
-#endif
 #ifndef CMSBWT_POS_SORT_BITS
 #define CMSBWT_POS_SORT_BITS 0  // 0: rocPRIM's default digits for the position sort
 #endif
@@ -136,7 +127,6 @@ struct InputError {
 // request of a similar size (all work runs on one stream, so stream order
 // makes reuse safe).  hipMalloc/hipFree of multi-GB buffers otherwise cost
 // tens of milliseconds per step.
-constexpr bool kCounterOverlap = CMSBWT_COUNTER_OVERLAP != 0;
 struct DevAlloc {
   std::multimap<uint64_t, void*> freeBlocks;
   std::unordered_map<void*, uint64_t> sizes;
@@ -332,14 +322,7 @@ struct Engine {
   explicit Engine(int dev) : device(dev) {
     g_alloc = &alloc;
     HIPCHK(hipSetDevice(dev));
-#if CMSBWT_MAIN_PRIO
-    // the main chain (ranks, suffix sort) before the side stream's counter
-    int least = 0, greatest = 0;
-    HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-    HIPCHK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, greatest));
-#else
     HIPCHK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-#endif
     HIPCHK(hipStreamCreateWithFlags(&st2, hipStreamNonBlocking));
     for (auto& e : evFork) HIPCHK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     HIPCHK(hipEventCreateWithFlags(&evJoin, hipEventDisableTiming));
@@ -2071,11 +2054,14 @@ struct Engine {
       win_prep(S, K, posBegin.p, n, 0, n, false, cstats.p, wp);
       writer_inputs();
     }
-    // (the slot-window kernel, CMSBWT_COUNTER_WIN=1, runs after the ranks)
-    const bool listed = !check && wp.tgt && kCounterOverlap;
+    // CMSBWT_COUNTER_OVERLAP=1: the counter itself on the side stream, its
+    // equal-key queries answered after the ranks (bit-exact, but slower:
+    // DESIGN.md §3.6a); the slot-window kernel (CMSBWT_COUNTER_WIN=1) always
+    // runs after the ranks.  CMSBWT_EQ_CAP: list capacity (tests: overflow)
+    const bool listed = !check && wp.tgt && env_u32("CMSBWT_COUNTER_OVERLAP", 0) != 0;
     if (listed) {
       Side sd(*this, evFork[0]);
-      eql.cap = std::max<uint64_t>(1, std::min<uint64_t>(H, 1ull << 27));
+      eql.cap = std::max<uint64_t>(1, std::min<uint64_t>(H, env_u32("CMSBWT_EQ_CAP", 1u << 27)));
       eqRec.alloc(eql.cap);
       eqCnt.alloc(1);
       eqCnt.zero(st);

@@ -165,6 +165,19 @@ def test_doubling_group_paths(engine, oracle, tmp_path, case, env):
     _compare(engine, oracle, tmp_path, case, env=env)
 
 
+@pytest.mark.parametrize("env", [{"CMSBWT_COUNTER_OVERLAP": "1"}, {"CMSBWT_COUNTER_OVERLAP": "1", "CMSBWT_EQ_CAP": "1"},
+                                 {"CMSBWT_COUNTER_STATS": "2"}],
+                         ids=["counter_beside_ranks", "equal_key_overflow", "pair_shape_stats"])
+@pytest.mark.parametrize("case", cases.small_cases()[:6], ids=lambda c: c[0])
+def test_counter_stream_paths(engine, oracle, tmp_path, case, env):
+    """counterSmallerThanHead (FN:1523-1603) on the side stream beside the
+    ranks and the suffix sort: the equal-key queries (FN:1537-1589, the only
+    ones that read next-head ranks) are listed and answered after the ranks
+    (k_counter_eq); an overflowing list (capacity 1) runs the counter again
+    with the ranks.  The pair-shape statistics pass leaves the output alone."""
+    _compare(engine, oracle, tmp_path, case, env=env)
+
+
 @pytest.mark.parametrize("geom", [{"CMSBWT_RUN_BIN_SHIFT": "3"},
                                   {"CMSBWT_RUN_BIN_SHIFT": "5", "CMSBWT_RUN_BIN_GLOBAL": "1"},
                                   {"CMSBWT_RUN_BIN_GLOBAL": "1"}],
