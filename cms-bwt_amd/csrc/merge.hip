@@ -1191,6 +1191,12 @@ constexpr uint32_t kNoSlot = 0xffffffffu;
 #define CMSBWT_TGT_FULL 0  // r04 A/B: 12.56-12.58 ms without, 12.67-12.73 ms with (the uniform branch costs more)
 #endif
 constexpr bool kTgtFull = CMSBWT_TGT_FULL != 0;
+// attribution builds only (wrong counters): 1 staging, 2 + record walks and
+// re-tests, 3 (default) + binary searches
+#ifndef CMSBWT_TGT_PHASES
+#define CMSBWT_TGT_PHASES 3
+#endif
+constexpr int kTgtPhases = CMSBWT_TGT_PHASES;
 
 
 constexpr uint32_t kFullRec = 0xffffffffu;
@@ -1474,8 +1480,11 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
     }
     __syncthreads();
     const uint32_t nS = nG[2 * wv], nF = nG[2 * wv + 1];
-    walk(std::true_type{}, 0u, nS);
-    walk(std::false_type{}, kTgtRec - nF, kTgtRec);
+    if (kTgtPhases >= 2) {
+      walk(std::true_type{}, 0u, nS);
+      walk(std::false_type{}, kTgtRec - nF, kTgtRec);
+    }
+    if (kTgtPhases < 3) nSearch = 0;
     if (nSearch) search();  // before the next chunk replaces the records
   }
   __syncthreads();
