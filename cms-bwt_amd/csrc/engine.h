@@ -1918,6 +1918,12 @@ struct Engine {
     if (H == 0) throw InputError{CMSBWT_EINPUT, "collection has no documents (reference behaviour undefined, FN:1359-1385)"};
     auto t0 = std::chrono::steady_clock::now();
     dm.on = false;
+    // an error thrown while side work is pending: drain the side stream
+    // before this scope's buffers go back to the pools (no-op otherwise)
+    struct SideDrain {
+      hipStream_t s;
+      ~SideDrain() { (void)hipStreamSynchronize(s); }
+    } sideDrain{st2};
     const uint32_t n = R.n;
     const uint32_t E = (uint32_t)ndocs;
     HeadsSoA h = heads();
