@@ -1395,7 +1395,14 @@ struct Engine {
     DBuf<uint32_t> errf;
     errf.alloc(1);
     errf.zero(st);
-    launch_finalize(R, h, H, docEnd.p, (uint32_t)ndocs, dtext.p, ddoc.p, errf.p, hDoc.p, st);
+    DBuf<uint32_t> isax;
+    const bool packIsax = R.n < (1u << 24) && !env_u32("CMSBWT_NO_ISAX", 0);
+    if (packIsax) {
+      isax.alloc(R.n);
+      launch_isax(R.isa, R.x, R.n, isax.p, st);
+    }
+    launch_finalize(R, h, H, docEnd.p, (uint32_t)ndocs, dtext.p, ddoc.p, errf.p, hDoc.p, st,
+                    packIsax ? isax.p : nullptr);
     HIPCHK(hipGetLastError());
     // run buckets (diff, hasHead): from the grouping's position sort in
     // merge(), or through position bins on demand (ensure_runs)
@@ -1715,6 +1722,7 @@ struct Engine {
     bool tgt = false;
     uint32_t nw = 0, ncross = 0, slotCap = 0;
     DBuf<uint32_t> winStart, crossOff, crossList, wflag, wincl, crossCnt, itemOff, keyW, keyW2, valQ;
+    DBuf<uint4> irec;  // target-major kernel: packed item fields
   };
   void counter_phase(const ItemsSoA& S, uint32_t K, const uint32_t* posBegin, const uint32_t* posF,
                      const uint32_t* nhrP, unsigned long long* counterP, unsigned long long* cstatsP, uint32_t n,
@@ -1776,6 +1784,10 @@ struct Engine {
     sort_pairs(W.keyW.p, W.keyW2.p, W.valQ.p, W.crossList.p, W.ncross, bits_for(W.nw));
     W.crossOff.alloc((uint64_t)W.nw + 1);
     mk_win_cross_off(W.keyW2.p, W.ncross, W.nw, W.crossOff.p, st);
+    if (W.tgt && !env_u32("CMSBWT_NO_IREC", 0)) {
+      W.irec.alloc(std::max<uint32_t>(K, 1));
+      mk_item_rec(S, K, W.irec.p, st);
+    }
   }
   // the counter kernel between ev0 and ev1 (no synchronisation; counter_time
   // reads the duration once the stream has passed ev1)
@@ -1786,7 +1798,7 @@ struct Engine {
     if (eq.rec && !W.tgt) throw InputError{CMSBWT_EINTERNAL, "internal: equal-key listing needs the target-major counter"};
     if (W.tgt)
       mk_counter_tgt(S, posBegin, posF, nhrP, W.winStart.p, W.nw, W.crossOff.p, W.crossList.p, counterP, cstatsP,
-                     n, st, eq);
+                     n, st, eq, W.irec.p);
     else
       mk_counter_win(S, posBegin, posF, nhrP, W.winStart.p, W.nw, W.crossOff.p, W.crossList.p, counterP, cstatsP,
                      n, W.slotCap, check ? hr : nullptr, st);

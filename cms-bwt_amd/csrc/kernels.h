@@ -55,9 +55,13 @@ void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t nd
                         const uint32_t* docLastChunk, const uint32_t* chunkCount,
                         const unsigned long long* chunkBase, uint32_t n, const HeadsSoA& h, uint32_t* docEndIdx,
                         uint32_t* hdoc, hipStream_t st);
+// ISA[p] | x[p] << 24 (references shorter than 2^24): k_finalize's isaNext
+// and order-check reads in one random line
+void launch_isax(const uint32_t* isa, const uint8_t* x, uint32_t n, uint32_t* out, hipStream_t st);
 void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint32_t* docEndIdx,
                      uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, uint32_t* errFlags,
-                     const uint32_t* hdoc, hipStream_t st);
+                     const uint32_t* hdoc, hipStream_t st,
+                     const uint32_t* isax = nullptr);
 // run buckets: diff[0..n] and hasHead[0..n) from the heads' runs, through
 // nb = (n >> sh) + 1 bins of 2^sh positions, sh <= kRunBinShift (count into
 // zeroed binCnt[nb+1]; scatter with binCur = exclusive prefix of the counts;

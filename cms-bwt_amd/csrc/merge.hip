@@ -809,6 +809,7 @@ struct CounterArgs {
   uint32_t slotCap;          // windows with more slots use global atomics
   HostRoute hr;              // CHECK only: targets answered by the host std::map replay
   EqList eq;                 // k_counter_tgt before the next-head ranks: equal-key queries listed
+  const uint4* irec;         // k_counter_tgt: (pos, until, len, count | smaller << 31) per item, or null
 };
 
 struct QueryStats {  // per lane; a lane serves far fewer than 2^32 queries per window
@@ -1459,14 +1460,17 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
         const uint32_t full = nSt - 4 * (qs4 - 1);  // quarters with qs4 items (1..4)
         q = iBeg + (rq < full ? rq * qs4 : full * qs4 + (rq - full) * (qs4 - 1)) + kq;
       }
-      const uint32_t p = it.pos[q], u = it.until[q];
+      // the item's fields in one 16-byte load (crossing items are random)
+      const uint4 iw = A.irec ? A.irec[q] : make_uint4(it.pos[q], it.until[q], 0u, 0u);
+      const uint32_t p = iw.x, u = iw.y;
       if (u) {
         const uint32_t lo = max(p + 1, T0);
         const uint32_t hi = (uint32_t)min((uint64_t)p + u, (uint64_t)T1 - 1);
         if (lo <= hi) {
           const uint32_t aO = lo - T0, bO = hi - T0;
-          const bool sm = it.smaller[q] != 0;
-          const uint4 rec = make_uint4(it.len[q] + p, aO | ((bO - aO) << 16), it.count[q], q);
+          const bool sm = A.irec ? (iw.w >> 31) != 0 : it.smaller[q] != 0;
+          const uint32_t ln = A.irec ? iw.z : it.len[q], cnt = A.irec ? iw.w & 0x7fffffffu : it.count[q];
+          const uint4 rec = make_uint4(ln + p, aO | ((bO - aO) << 16), cnt, q);
           for (uint32_t k = aO >> 6; k <= (bO >> 6); k++) {
             // pairs of this record whose target has no heads (FN:1530)
             const uint32_t a = k == (aO >> 6) ? (aO & 63u) : 0u, b = k == (bO >> 6) ? (bO & 63u) : 63u;
@@ -1524,6 +1528,14 @@ __global__ void k_counter_shape(const ItemsSoA it, uint32_t K, uint32_t n, unsig
 }
 void mk_counter_shape(const ItemsSoA& it, uint32_t K, uint32_t n, unsigned long long* out, hipStream_t st) {
   if (K) hipLaunchKernelGGL(k_counter_shape, dim3((K + 255) / 256), dim3(256), 0, st, it, K, n, out);
+}
+__global__ void k_item_rec(const ItemsSoA it, uint32_t K, uint4* __restrict__ out) {
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
+  if (q < K)
+    out[q] = make_uint4(it.pos[q], it.until[q], it.len[q], (it.count[q] & 0x7fffffffu) | (it.smaller[q] ? 0x80000000u : 0u));
+}
+void mk_item_rec(const ItemsSoA& it, uint32_t K, uint4* out, hipStream_t st) {
+  if (K) hipLaunchKernelGGL(k_item_rec, dim3((K + 255) / 256), dim3(256), 0, st, it, K, out);
 }
 __global__ void k_item_sk(ItemsSoA it, uint32_t K) {
   uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2259,9 +2271,10 @@ void mk_counter_win(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t
 void mk_counter_tgt(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
                     const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
                     unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st,
-                    EqList eq) {
+                    EqList eq, const uint4* irec) {
   if (!nw) return;
-  CounterArgs A{it, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n, 0u, HostRoute{}, eq};
+  CounterArgs A{it, posBegin, posF, nhr, winStart, crossOff, crossList, counter, stats, n, 0u, HostRoute{}, eq,
+                irec};
   hipLaunchKernelGGL(k_counter_tgt, dim3(nw), dim3(256), 0, st, A);
 }
 // FN:1537-1589 for the listed equal-key queries (the branch of

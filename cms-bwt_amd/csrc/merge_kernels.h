@@ -180,7 +180,10 @@ void mk_or_mask(uint8_t* mask, const uint8_t* other, uint32_t n, hipStream_t st)
 void mk_counter_tgt(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t* posF, const uint32_t* nhr,
                     const uint32_t* winStart, uint32_t nw, const uint32_t* crossOff, const uint32_t* crossList,
                     unsigned long long* counter, unsigned long long* stats, uint32_t n, hipStream_t st,
-                    EqList eq = EqList{});
+                    EqList eq = EqList{}, const uint4* irec = nullptr);
+// per item (pos, until, len, count | smaller << 31): the counter's staging
+// loads of an item in one 16-byte read
+void mk_item_rec(const ItemsSoA& it, uint32_t K, uint4* out, hipStream_t st);
 void mk_count_distinct(const uint32_t* v, uint32_t K, unsigned long long* out, hipStream_t st);
 void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int64_t* bucket, hipStream_t st);
 // run writer: units = E end phrases + SA ranks 1..n-1 (sharded merge), or

@@ -70,7 +70,8 @@ __global__ void k_end_phrases(const uint8_t* __restrict__ text, const uint64_t* 
 // replaces the per-position bucket increments.
 __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __restrict__ docEndIdx,
                            uint32_t ndocs, const uint8_t* __restrict__ text, const uint64_t* __restrict__ docOff,
-                           uint32_t* __restrict__ errFlags, const uint32_t* __restrict__ hdoc) {
+                           uint32_t* __restrict__ errFlags, const uint32_t* __restrict__ hdoc,
+                           const uint32_t* __restrict__ isax) {
   uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= H) return;
   const uint32_t leni = h.len[i];
@@ -104,7 +105,9 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
   const uint32_t sj = h.start[j];
   uint32_t q = h.pos[j] + (ei - sj);
   if (q >= R.n) { atomicOr(errFlags, 2u); q = R.n - 1; }
-  h.isa[i] = R.isa[q];
+  // isax (n < 2^24): ISA[q] | x[q] << 24, one random line instead of two
+  const uint32_t ix = isax ? isax[q] : 0u;
+  h.isa[i] = isax ? ix & 0xffffffu : R.isa[q];
   // Order invariant: the isaNext suffix starts with the mismatching text byte
   // (or the head ends at the document separator and isaNext is the smallest
   // suffix).  When it holds for every head and the reference has no byte >=
@@ -114,7 +117,8 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
   const uint8_t* dt = text + docOff[lo];
   {
     const uint8_t c = dt[ei];
-    if (!(c == R.x[q] || (c == kSep && q == R.n - 1))) atomicOr(errFlags, 8u);
+    const uint8_t xq = isax ? (uint8_t)(ix >> 24) : R.x[q];
+    if (!(c == xq || (c == kSep && q == R.n - 1))) atomicOr(errFlags, 8u);
   }
   // BWT character of the phrase (FN:1158-1161): the text byte before it, 0x02
   // at a document start.  Read here rather than in k_scatter_heads: heads are
@@ -239,12 +243,20 @@ void launch_end_phrases(const uint8_t* text, const uint64_t* docOff, uint32_t nd
                      docLastChunk, chunkCount, chunkBase, n, h, docEndIdx, hdoc);
 }
 
+__global__ void k_isax(const uint32_t* __restrict__ isa, const uint8_t* __restrict__ x, uint32_t n,
+                       uint32_t* __restrict__ out) {
+  const uint32_t p = blockIdx.x * blockDim.x + threadIdx.x;
+  if (p < n) out[p] = isa[p] | ((uint32_t)x[p] << 24);
+}
+void launch_isax(const uint32_t* isa, const uint8_t* x, uint32_t n, uint32_t* out, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_isax, dim3((n + 255) / 256), dim3(256), 0, st, isa, x, n, out);
+}
 void launch_finalize(const DevRef& R, const HeadsSoA& h, uint32_t H, const uint32_t* docEndIdx,
                      uint32_t ndocs, const uint8_t* text, const uint64_t* docOff, uint32_t* errFlags,
-                     const uint32_t* hdoc, hipStream_t st) {
+                     const uint32_t* hdoc, hipStream_t st, const uint32_t* isax) {
   if (!H) return;
   hipLaunchKernelGGL(k_finalize, dim3((H + 255) / 256), dim3(256), 0, st, R, h, H, docEndIdx, ndocs, text, docOff,
-                     errFlags, hdoc);
+                     errFlags, hdoc, isax);
 }
 
 static unsigned run_bin_grid(uint32_t H) { return std::max(1u, std::min((H + 255) / 256, 1024u)); }
