@@ -2067,10 +2067,15 @@ struct Engine {
     DBuf<uint4> eqRec;
     DBuf<unsigned long long> eqCnt;
     EqList eql;
+    // phrasesSet.size() for the log (distinct positions holding items)
+    DBuf<unsigned long long> posCnt;
     if (!check) {
       Side sd(*this, evFork[0]);
       win_prep(S, K, posBegin.p, n, 0, n, false, cstats.p, wp);
       writer_inputs();
+      posCnt.alloc(1);
+      posCnt.zero(st);  // (on the side stream, like the count)
+      mk_count_distinct(sPos.p, K, posCnt.p, st);
     }
     // CMSBWT_COUNTER_OVERLAP=1: the counter itself on the side stream, its
     // equal-key queries answered after the ranks (bit-exact, but slower:
@@ -2335,7 +2340,12 @@ struct Engine {
     stats.current_sum = H;
     stats.runs = Rn;
     stats.symbols = symbols;
-    stats.positions = count_positions(sPos);
+    if (check) {
+      posCnt.alloc(1);
+      posCnt.zero(st);
+      mk_count_distinct(sPos.p, K, posCnt.p, st);
+    }
+    stats.positions = read1(posCnt.p);  // (side work was joined before the counter)
     {
       uint32_t fl[2] = {0, 0};
       HIPCHK(hipMemcpy(fl, rthFL.p, 8, hipMemcpyDeviceToHost));
@@ -2399,14 +2409,7 @@ struct Engine {
   bool orderInvariant = false;  // set by ms_walk (k_finalize), false for imported shards
   uint64_t W_work = 0;
 
-  uint64_t count_positions(DBuf<uint32_t>& sPos) {
-    // phrasesSet.size(): distinct positions holding items (n-1 always present)
-    DBuf<unsigned long long> c;
-    c.alloc(1);
-    c.zero(st);
-    mk_count_distinct(sPos.p, K, c.p, st);
-    return read1(c.p);
-  }
+
 
   // =====================================================================
   void copy_runs(uint8_t* out, uint64_t cap) {
