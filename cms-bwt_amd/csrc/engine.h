@@ -2069,6 +2069,16 @@ struct Engine {
     EqList eql;
     // phrasesSet.size() for the log (distinct positions holding items)
     DBuf<unsigned long long> posCnt;
+    // work volume (statistics only): sum of untilNext, read back with the
+    // counter statistics
+    DBuf<uint64_t> wsum;
+    auto work_sum = [&]() {
+      wsum.alloc(1);
+      auto u64in = rocprim::make_transform_iterator(sUntil.p, WidenU64());
+      size_t b = 0;
+      HIPCHK(rocprim::reduce(nullptr, b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
+      HIPCHK(rocprim::reduce(scratch(b), b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
+    };
     if (!check) {
       Side sd(*this, evFork[0]);
       win_prep(S, K, posBegin.p, n, 0, n, false, cstats.p, wp);
@@ -2076,6 +2086,7 @@ struct Engine {
       posCnt.alloc(1);
       posCnt.zero(st);  // (on the side stream, like the count)
       mk_count_distinct(sPos.p, K, posCnt.p, st);
+      work_sum();
     }
     // CMSBWT_COUNTER_OVERLAP=1: the counter itself on the side stream, its
     // equal-key queries answered after the ranks (bit-exact, but slower:
@@ -2204,15 +2215,8 @@ struct Engine {
 
     // ---- counterSmallerThanHead (FN:1523-1603)
     uint64_t W = 0;
-    // work volume (statistics only): sum of untilNext, read back with the
-    // counter statistics
-    DBuf<uint64_t> wsum;
-    wsum.alloc(1);
     {
-      auto u64in = rocprim::make_transform_iterator(sUntil.p, WidenU64());
-      size_t b = 0;
-      HIPCHK(rocprim::reduce(nullptr, b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
-      HIPCHK(rocprim::reduce(scratch(b), b, u64in, wsum.p, (uint64_t)0, (size_t)K, rocprim::plus<uint64_t>(), st));
+      if (check) work_sum();
       if (!check) {
         join_side();
         const uint64_t nEq = listed ? read1(eqCnt.p) : 0;
