@@ -230,9 +230,21 @@ def main():
                     help="plain .bwt instead of .rl_bwt (BASELINE config 5 runs without -r)")
     args = ap.parse_args()
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
+    env_world = os.environ.get("WORLD_SIZE")
+    world = int(env_world or "1")
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if env_world is not None and world != args.gpus:
+        # the line's n_gpus must be the ranks that actually ran
+        print(json.dumps({"error": f"--gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a "
+                                   "number for a different rank count"}), flush=True)
+        sys.exit(2)
+    # --gpus N > 1 without a launcher: the product's in-process multi-GPU path
+    # (multi.hip rank group: one host thread and context per rank, rank k on
+    # device k % devices, the same walk + position-sharded merge as cmsbwt -n N)
+    in_process = env_world is None and args.gpus > 1
+    if in_process:
+        world = args.gpus
     import torch
     dist = None
     # Rehearsal of the N>1 path on a one-GPU box (never set by the driver):
@@ -241,23 +253,35 @@ def main():
     same_gpu = os.environ.get("CMSBWT_BENCH_SAME_GPU", "0") == "1"
     if same_gpu:
         local = 0
-    if world > 1:
+    if world > 1 and not in_process:
         import torch.distributed as dist
         torch.cuda.set_device(local)
         dist.init_process_group("gloo" if same_gpu else "nccl", init_method="env://")
 
     import cmsbwt
     import cmsbwt.dist as cdist
-    eng = cmsbwt.Engine(local)
     ref = synth_reference(args.ref_len, args.seed)
-    eng.load_reference_bytes(ref)
-    # documents shard by contiguous ranges (the walk and j-scan are document-local)
-    c0, c1 = cdist.shard_range(args.copies, world, rank)
-    eng.load_synth(args.seed, 1 + c0, c1 - c0, args.p, leading_empty_doc=(rank == 0))
+    grp = None
+    backend = os.environ.get("CMSBWT_BENCH_BACKEND", "peer")  # in-process transport: peer | rccl
+    if in_process:
+        grp = cmsbwt.Group(world, device=0, backend=backend)
+        for k in range(world):
+            e = grp.engine(k)
+            e.load_reference_bytes(ref)
+            c0, c1 = cdist.shard_range(args.copies, world, k)
+            e.load_synth(args.seed, 1 + c0, c1 - c0, args.p, leading_empty_doc=(k == 0))
+        eng = grp.engine(0)
+    else:
+        eng = cmsbwt.Engine(local)
+        eng.load_reference_bytes(ref)
+        # documents shard by contiguous ranges (the walk and j-scan are document-local)
+        c0, c1 = cdist.shard_range(args.copies, world, rank)
+        eng.load_synth(args.seed, 1 + c0, c1 - c0, args.p, leading_empty_doc=(rank == 0))
     device = f"cuda:{local}"
     mode = os.environ.get("CMSBWT_DIST", "sharded")  # N>1: sharded | gather; "sharded1": sharded path at N=1
     gather = mode == "gather"
-    xfer = cdist.Transport(device) if (world > 1 or mode == "sharded1") else None
+    xfer = cdist.Transport(device) if ((world > 1 and not in_process) or mode == "sharded1") else None
+    group_rows = []  # in-process: per-rank stage times of each timed step
 
     rle = not args.plain
     # per-step stage wall times of this rank (N > 1: walk, then the sharded
@@ -268,6 +292,9 @@ def main():
     def step():
         if world == 1 and mode != "sharded1":
             eng.step(rle=rle)
+            return
+        if in_process:  # every rank's walk + the sharded merge, synchronous
+            group_rows.append(grp.step(rle))
             return
         t0 = time.perf_counter()
         eng.ms_walk()  # synchronous: ends with the engine stream drained
@@ -291,6 +318,7 @@ def main():
         step()
     barrier()
     stage.update(walk=0.0, merge=0.0, n=0)
+    group_rows.clear()
     t0 = time.perf_counter()
     for _ in range(args.steps):
         step()
@@ -304,13 +332,20 @@ def main():
     # per rank: [step time, walk stage, merge stage, walk kernel] -> max over
     # ranks; the walk roofline below is that of the slowest rank's kernel
     # (algorithmic bytes of the rank whose kernel was slowest)
-    mine = [dt, stage["walk"] / ns, stage["merge"] / ns, walk_local["kernel_ms"],
-            float(walk_local["heads"]), float(walk_local["chars"]), float(st.device_peak_bytes)]
+    mine = None if in_process else [dt, stage["walk"] / ns, stage["merge"] / ns, walk_local["kernel_ms"],
+                                    float(walk_local["heads"]), float(walk_local["chars"]),
+                                    float(st.device_peak_bytes)]
     if dist:
         t = torch.tensor(mine, device="cpu" if same_gpu else f"cuda:{local}", dtype=torch.float64)
         allt = [torch.zeros_like(t) for _ in range(world)]
         dist.all_gather(allt, t)
         rows = [[float(v) for v in x.cpu().tolist()] for x in allt]
+    elif in_process:  # one wall clock for the whole group; per-rank stage means
+        K = max(1, len(group_rows))
+        rows = [[dt] + [sum(getattr(s[k], f) for s in group_rows) / K / (1e3 if f != "walk_kernel_ms" else 1)
+                        for f in ("walk_ms", "merge_ms", "walk_kernel_ms")] +
+                [float(group_rows[-1][k].heads), float(group_rows[-1][k].chars),
+                 float(group_rows[-1][k].device_peak_bytes)] for k in range(world)]
     else:
         rows = [mine]
     dt = max(r[0] for r in rows)
@@ -344,7 +379,11 @@ def main():
                                + ("" if args.plain else ", -r"),
                    "ref_len": args.ref_len, "copies": args.copies, "snp": args.p, "seed": args.seed,
                    "collection_bytes": chars_total, "heads": st.heads, "keys": st.keys, "runs": st.runs,
-                   "parallelism": ((f"documents sharded over {world} GPUs, heads gathered to rank 0 over RCCL, merge on rank 0"
+                   "parallelism": ((f"{world} in-process ranks (multi.hip rank group, rank k on device "
+                                    f"k % {torch.cuda.device_count()}), {backend} transport; walk: documents "
+                                    "sharded; merge: reference positions sharded, runs gathered to rank 0"
+                                    if in_process else
+                                    f"documents sharded over {world} GPUs, heads gathered to rank 0 over RCCL, merge on rank 0"
                                     if gather else
                                     f"walk: documents sharded over {world} GPUs; merge: reference positions sharded, "
                                     "all-to-all/all-reduce over RCCL, runs gathered to rank 0")
@@ -352,7 +391,7 @@ def main():
         "roofline": {"bound": "hbm", "kernel": "k_ms_walk2", "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src,
-                     "algorithmic_bytes": b_alg, "kernel_ms": round(st.ms_walk_kernel_ms, 3),
+                     "algorithmic_bytes": b_alg, "kernel_ms": round(slow[3], 3),
                      "bytes_model": f"{WALK_B_PER_CHAR} B/char (text + reference byte at the extension frontier) "
                                     f"+ {WALK_B_PER_HEAD} B/head (16-B record, 8-B prefix probe, 4-B PLCP exit); "
                                     "DESIGN.md §3.1",
@@ -388,7 +427,11 @@ def main():
             out["parity"] = parity_check(eng, args, rle)
         except Exception as e:  # reported, never fatal for the GPU number
             out["parity"] = {"error": str(e)[-400:]}
-    eng.close()
+    if grp is not None:
+        out["per_rank_devices"] = [int(r.device) for r in group_rows[-1]] if group_rows else None
+        grp.close()
+    else:
+        eng.close()
     if rank == 0 and world == 1 and not args.no_e2e:
         try:
             out["e2e"] = e2e_leg(args, rle)

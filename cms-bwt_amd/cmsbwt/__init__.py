@@ -82,6 +82,13 @@ class Stats(ctypes.Structure):
 _lib = None
 
 
+class RankTimes(ctypes.Structure):
+    """include/cmsbwt.h cmsbwt_rank_times."""
+    _fields_ = [(k, ctypes.c_double) for k in ("walk_ms", "merge_ms", "walk_kernel_ms")] + \
+        [(k, ctypes.c_uint64) for k in ("heads", "chars", "device_peak_bytes")] + \
+        [("gathered", ctypes.c_int32), ("device", ctypes.c_int32)]
+
+
 def library_path() -> str:
     return _LIB_PATH
 
@@ -148,6 +155,12 @@ def load_library() -> ctypes.CDLL:
         "cmsbwt_dm_emit": (I32, [P, VP, ctypes.POINTER(U64)]),
         "cmsbwt_dm_copy_stream": (I32, [P, VP, VP]),
         "cmsbwt_dm_finish": (I32, [P, ctypes.POINTER(VP), ctypes.POINTER(VP), VP, VP]),
+        # rank groups (in-process multi-GPU step over resident inputs)
+        "cmsbwt_group_create": (I32, [I32, I32, I32, ctypes.POINTER(P)]),
+        "cmsbwt_group_ctx": (P, [P, I32]),
+        "cmsbwt_group_step": (I32, [P, I32, ctypes.POINTER(RankTimes)]),
+        "cmsbwt_group_last_error": (ctypes.c_char_p, [P]),
+        "cmsbwt_group_destroy": (None, [P]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -168,6 +181,8 @@ EXPORTED = [
     "cmsbwt_dm_dbl_init", "cmsbwt_dm_dbl_route", "cmsbwt_dm_dbl_pack", "cmsbwt_dm_dbl_sort", "cmsbwt_dm_dbl_apply",
     "cmsbwt_dm_pack_ranks", "cmsbwt_dm_load_ranks", "cmsbwt_dm_route_halo", "cmsbwt_dm_pack_halo",
     "cmsbwt_dm_counter", "cmsbwt_dm_units", "cmsbwt_dm_emit", "cmsbwt_dm_copy_stream", "cmsbwt_dm_finish",
+    "cmsbwt_group_create", "cmsbwt_group_ctx", "cmsbwt_group_step", "cmsbwt_group_last_error",
+    "cmsbwt_group_destroy",
 ]
 
 
@@ -213,9 +228,9 @@ class Engine:
         self._ctx = p
 
     def close(self):
-        if self._ctx:
+        if self._ctx and not getattr(self, "_borrowed", False):
             self._lib.cmsbwt_ctx_destroy(self._ctx)
-            self._ctx = None
+        self._ctx = None
 
     def __enter__(self):
         return self
@@ -408,6 +423,61 @@ class Engine:
         self._chk(self._lib.cmsbwt_copy_array(self._ctx, name.encode(), out.ctypes.data if out.size else None,
                                               ctypes.byref(nb)))
         return out
+
+
+class Group:
+    """`world` rank contexts in this process (include/cmsbwt.h "Rank groups"):
+    rank k on device (device + k) % devices.  Load each rank through
+    ``engine(k)`` (the ranks' documents, in rank order, are the collection),
+    then ``step()`` runs every rank's walk and the position-sharded merge;
+    the runs and the global statistics end up in ``engine(0)``."""
+
+    def __init__(self, world: int, device: int = 0, backend: str = "peer"):
+        self._lib = load_library()
+        p = ctypes.c_void_p()
+        rc = self._lib.cmsbwt_group_create(world, device, CMSBWT_BACKEND_RCCL if backend == "rccl"
+                                           else CMSBWT_BACKEND_PEER, ctypes.byref(p))
+        if rc != CMSBWT_OK:
+            raise CmsBwtError(rc, f"cannot create a group of {world} ranks on device {device} ({backend})")
+        self._g = p
+        self.world = world
+        self._engines = []
+        for k in range(world):
+            e = Engine.__new__(Engine)  # a view of the group's context (the group owns it)
+            e._lib = self._lib
+            e._ctx = ctypes.c_void_p(self._lib.cmsbwt_group_ctx(p, k))
+            e._borrowed = True
+            self._engines.append(e)
+
+    def engine(self, rank: int) -> "Engine":
+        return self._engines[rank]
+
+    def step(self, rle: bool = True):
+        """One walk + sharded merge on every rank; returns the per-rank RankTimes."""
+        t = (RankTimes * self.world)()
+        rc = self._lib.cmsbwt_group_step(self._g, 1 if rle else 0, t)
+        if rc != CMSBWT_OK:
+            raise CmsBwtError(rc, self._lib.cmsbwt_group_last_error(self._g).decode(errors="replace"))
+        return list(t)
+
+    def close(self):
+        if self._g:
+            for e in self._engines:
+                e._ctx = None
+            self._lib.cmsbwt_group_destroy(self._g)
+            self._g = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def host_read_collection(path: str, prefix: int = UINT64_MAX):

@@ -317,6 +317,22 @@ constexpr bool kProbeNoSkip = CMSBWT_PROBE_NOSKIP != 0;
 #define CMSBWT_ALIGN_MEMO 1
 #endif
 constexpr bool kAlignMemo = CMSBWT_ALIGN_MEMO != 0;
+#ifndef CMSBWT_MEMO_GENERIC
+#define CMSBWT_MEMO_GENERIC 0
+#endif
+// diagnostic builds (CMSBWT_MEMO_CHECK=1): a memo hit only predicts; the LCE
+// runs as without the memo and the result is compared with the prediction
+// (and the predicted match end with the reference and text bounds); the
+// first disagreements are printed
+#ifndef CMSBWT_MEMO_CHECK
+#define CMSBWT_MEMO_CHECK 0
+#endif
+constexpr bool kMemoCheck = CMSBWT_MEMO_CHECK != 0;
+#ifndef CMSBWT_MEMO_TRACE
+#define CMSBWT_MEMO_TRACE 0
+#endif
+constexpr bool kMemoTrace = CMSBWT_MEMO_TRACE != 0 && !kMemoCheck;
+__device__ uint32_t g_memo_bad = 0;
 // waves per SIMD of the walk (Makefile W2WAVES; measured 3 -> 16.50 ms,
 // 4 -> 16.44-16.68, 5 -> 16.9, 6 -> 31.3 with register spills)
 #ifndef CMSBWT_W2_WAVES
@@ -353,7 +369,7 @@ k_ms_walk2(Walk2Args A) {
   // (95 SGPRs spilled to VGPR lanes) it changed results on a raw reference
   // with N (tests/test_gpu_parity.py raw_reference_with_N) while a build with
   // extra checking code did not -- kept out there until understood
-  const bool memo = kAlignMemo && FAST;
+  const bool memo = kAlignMemo && (FAST || CMSBWT_MEMO_GENERIC);
   const Lv V{lvlL, lvlL + kMaxLevels, R.nlvl, (int32_t)R.n, R.lcp};
   const uint32_t n = R.n;
   const uintptr_t X = (uintptr_t)R.x;
@@ -382,6 +398,8 @@ k_ms_walk2(Walk2Args A) {
   // positions [amLo, amFront) match the reference; amC bit 16: the bytes at
   // amFront differ (x byte | text byte << 8)
   uint32_t amAlign = 0, amLo = 0xffffffffu, amFront = 0, amC = 0;
+  // CMSBWT_MEMO_CHECK builds: the memo's prediction, checked against the LCE
+  uint32_t chkOn = 0, chkLen = 0, chkC = 0, chkLo = 0, chkLen0 = 0;
   // emission
   // pool blocks are reserved kPoolBatch at a time (blk .. blkEnd) and kept
   // across this lane's chunks; blocks never started keep blkChunk = ~0
@@ -567,12 +585,30 @@ k_ms_walk2(Walk2Args A) {
   // alignment memo already knows where this offset's match ends
   auto start_lce = [&]() {
     if (memo && pos - i == amAlign && i + len >= amLo && i + len <= amFront) {
+      if (kMemoCheck) {  // predict only; the LCE below runs and PC_POST compares
+        chkOn = 1;
+        chkLen = amFront - i;
+        chkC = amC;
+        chkLo = amLo;
+        chkLen0 = len;
+      } else {
+      if (kMemoTrace) {
+        chkOn = 1;
+        chkLen = pos;
+        chkLo = i;
+        chkLen0 = len;
+        const uint32_t k = atomicAdd(&g_memo_bad, 1u);
+        if (k < 6)
+          printf("[memo-hit] chunk %u i %u pos %u len %u -> %u | align %u lo %u front %u c %05x\n", cid, i, pos, len,
+                 amFront - i, amAlign, amLo, amFront, amC);
+      }
       len = amFront - i;
       if (amC & 0x10000u) {  // the mismatch at amFront (FN:55)
         smaller = (int8_t)(uint8_t)amC > (int8_t)(uint8_t)(amC >> 8);
         phase = PC_POST;
         use = 0;
         return;
+      }
       }
     }
     phase = PH_LCE;
@@ -661,6 +697,29 @@ k_ms_walk2(Walk2Args A) {
       adj_or_finish();
     }
     if (phase == PC_POST) {  // head test and record (FN:1154-1171), then contraction
+      if (kMemoTrace && chkOn) {  // (trace builds) the state the memo hit left
+        chkOn = 0;
+        if (pos != chkLen || i != chkLo) {
+          const uint32_t k = atomicAdd(&g_memo_bad, 1u);
+          if (k < 40)
+            printf("[memo-post] chunk %u hit at i %u pos %u len0 %u; at POST i %u pos %u len %u phase-path\n", cid,
+                   chkLo, chkLen, chkLen0, i, pos, len);
+        }
+      }
+      if (kMemoCheck && chkOn) {  // the LCE's result against the memo's prediction
+        chkOn = 0;
+        const bool mm = (chkC & 0x10000u) != 0;
+        const bool sm = (int8_t)(uint8_t)chkC > (int8_t)(uint8_t)(chkC >> 8);
+        const uint32_t got = i + len;  // text index of the LCE's mismatch
+        const bool bad = mm ? (len != chkLen || smaller != sm) : (len < chkLen);
+        if (bad || chkLen + amAlign + i >= n || got + amAlign >= n + (uint32_t)kTextPad) {
+          const uint32_t k = atomicAdd(&g_memo_bad, 1u);
+          if (k < 16)
+            printf("[memo] chunk %u i %u pos %u len0 %u -> lce len %u smaller %d | memo align %u lo %u front %u "
+                   "c %05x predicted len %u smaller %d\n",
+                   cid, i, pos, chkLen0, len, (int)smaller, amAlign, chkLo, chkLen + i, chkC, chkLen, (int)sm);
+        }
+      }
       const bool head = i >= a && pos != prevPos + 1;
       // new pool blocks: one atomic per wave for every lane whose reserved
       // blocks ran out (a single counter takes every reservation of the grid)

@@ -32,9 +32,11 @@
 #include <sys/stat.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <condition_variable>
 #include <fstream>
+#include <functional>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -130,10 +132,19 @@ class Group {
     if (failed) throw Aborted{};
   }
   void fail() {
-    std::lock_guard<std::mutex> lk(mu);
-    failed = true;
-    cv.notify_all();
+    std::function<void()> ab;
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      if (!failed && onFail) ab = onFail;
+      failed = true;
+      cv.notify_all();
+    }
+    // ranks blocked inside an RCCL call (or a stream synchronisation behind
+    // one) wait on a peer that never posts its side: abort the communicators
+    // so those calls return an error and the ranks reach their latch
+    if (ab) ab();
   }
+  std::function<void()> onFail;  // set before the rank threads start
   // every rank, failed or not, passes here once before its context goes away
   void final_latch() {
     std::unique_lock<std::mutex> lk(mu);
@@ -154,6 +165,7 @@ struct Rccl {
   void* h = nullptr;
   decltype(&ncclCommInitAll) commInitAll = nullptr;
   decltype(&ncclCommDestroy) commDestroy = nullptr;
+  decltype(&ncclCommAbort) commAbort = nullptr;
   decltype(&ncclSend) send = nullptr;
   decltype(&ncclRecv) recv = nullptr;
   decltype(&ncclAllReduce) allReduce = nullptr;
@@ -169,7 +181,8 @@ struct Rccl {
       f = (std::remove_reference_t<decltype(f)>)dlsym(h, s);
       ok = ok && f;
     };
-    sym(commInitAll, "ncclCommInitAll"); sym(commDestroy, "ncclCommDestroy"); sym(send, "ncclSend");
+    sym(commInitAll, "ncclCommInitAll"); sym(commDestroy, "ncclCommDestroy"); sym(commAbort, "ncclCommAbort");
+    sym(send, "ncclSend");
     sym(recv, "ncclRecv"); sym(allReduce, "ncclAllReduce"); sym(groupStart, "ncclGroupStart");
     sym(groupEnd, "ncclGroupEnd"); sym(errStr, "ncclGetErrorString");
     if (!ok) err = "librccl lacks an entry point";
@@ -307,8 +320,35 @@ void chk(int rc, cmsbwt_ctx* c) {
   if (rc) throw CtxError{rc, cmsbwt_last_error(c)};
 }
 
+// device bytes per head of the one-GPU merge at 1 % divergence (K ~ H;
+// measured on the config-5 proxies)
+constexpr double kGatherBytesPerHead = 135.0;
+
 using Clock = std::chrono::steady_clock;
 double since_ms(Clock::time_point t) { return std::chrono::duration<double, std::milli>(Clock::now() - t).count(); }
+
+// CMSBWT_MULTI_TIMING=1: host wall time of each exchange / stage of the
+// sharded merge, per rank, on stderr (attributing the multi-rank overhead)
+struct StageClock {
+  bool on = false;
+  int rank = 0;
+  Clock::time_point t = Clock::now();
+  std::string line;
+  explicit StageClock(int r) : rank(r) {
+    const char* e = getenv("CMSBWT_MULTI_TIMING");
+    on = e && *e == '1';
+  }
+  void mark(const char* what) {
+    if (!on) return;
+    char b[64];
+    snprintf(b, sizeof b, " %s %.2f", what, since_ms(t));
+    line += b;
+    t = Clock::now();
+  }
+  ~StageClock() {
+    if (on) fprintf(stderr, "[multi-timing] rank %d:%s\n", rank, line.c_str());
+  }
+};
 
 template <class T>
 uint64_t sum_col(const std::vector<std::vector<uint64_t>>& m, int k) {
@@ -364,6 +404,7 @@ void gather_merge(Xfer& x, cmsbwt_ctx* ctx, int rle, RankOut& ro) {
 // to be redone as a gather step (comparator ambiguity).
 bool sharded_merge(Xfer& x, cmsbwt_ctx* ctx, int rle, RankOut& ro) {
   const int W = x.W, rank = x.rank;
+  StageClock clk(rank);
   const CtxView v = ctx_view(ctx);
   const uint32_t n = v.n;
   const uint64_t H = v.H;
@@ -373,10 +414,12 @@ bool sharded_merge(Xfer& x, cmsbwt_ctx* ctx, int rle, RankOut& ro) {
   for (auto& m : meta) { Htot += m[0]; E += m[1]; chars += m[2]; inv = inv && m[3]; }
   auto tr = Clock::now();
   chk(cmsbwt_dm_begin(ctx, (uint32_t)W, (uint32_t)rank, Htot, E, inv ? 1u : 0u, rle), ctx);
+  clk.mark("meta+begin");
   // 1-2. heads to the owners of their positions; items; initial labels
   std::vector<uint64_t> hc(W);
   chk(cmsbwt_dm_route_heads(ctx, hc.data()), ctx);
   const std::vector<uint64_t> rc = x.counts(hc);
+  clk.mark("route+counts");
   uint64_t Hp = 0;
   for (auto c : rc) Hp += c;
   {
@@ -385,26 +428,32 @@ bool sharded_merge(Xfer& x, cmsbwt_ctx* ctx, int rle, RankOut& ro) {
     recv.alloc(Hp * 5);
     chk(cmsbwt_dm_pack_heads(ctx, send.p), ctx);
     x.a2a(send.p, 20, hc, rc, recv.p);
+    clk.mark("pack+a2a_heads");
     send.release();
     Buf<uint32_t> sa;
     sa.alloc(3ull * n + 1);
     chk(cmsbwt_dm_group(ctx, recv.p, Hp, sa.p), ctx);
+    clk.mark("group");
     recv.release();
     x.allreduce(sa.p, 3ull * n + 1, Red::SumU32);
+    clk.mark("allreduce_sa");
     Buf<unsigned long long> back, labels;
     back.alloc(Hp);
     chk(cmsbwt_dm_labels(ctx, sa.p, (uint64_t*)back.p), ctx);
     sa.release();
     labels.alloc(H);
     x.a2a(back.p, 8, rc, hc, labels.p);
+    clk.mark("labels+a2a");
     back.release();
     uint64_t u0 = 0;
     chk(cmsbwt_dm_dbl_init(ctx, (const uint64_t*)labels.p, &u0), ctx);
+    clk.mark("dbl_init");
   }
   ro.tRanks = since_ms(tr);
   // phrasesSet.size(): distinct positions with items, over the owners
   const CtxView vg = ctx_view(ctx);
   const uint64_t posLocal = ctx_count_distinct(ctx, vg.dmItemPos, vg.dmItems);
+  clk.mark("distinct");
   // 3. prefix doubling of the head string (FN:1455-1459); the count exchange
   // also sums the unresolved members
   auto td = Clock::now();
@@ -432,8 +481,10 @@ bool sharded_merge(Xfer& x, cmsbwt_ctx* ctx, int rle, RankOut& ro) {
     back.alloc(U);
     x.a2a(res.p, 8, r, c, back.p);
     chk(cmsbwt_dm_dbl_apply(ctx, (const uint64_t*)back.p, &U), ctx);
+    clk.mark("dbl_round");
   }
   ro.tDbl = since_ms(td);
+  clk.mark("dbl_end");
   // First / Last rankToHead (FN:1476-1477): ranks of global heads 0 and H-1
   // (the first head is rank 0's, the last one that of the last rank with heads)
   std::vector<uint64_t> fl{0, 0, H ? 1ull : 0ull};
@@ -455,6 +506,7 @@ bool sharded_merge(Xfer& x, cmsbwt_ctx* ctx, int rle, RankOut& ro) {
     x.a2a(rk.p, 12, hc, rc, rr.p);
     rk.release();
     chk(cmsbwt_dm_load_ranks(ctx, rr.p), ctx);
+    clk.mark("ranks");
   }
   ro.tRanks += since_ms(tr2);
   // 5. counters with the halo of items reaching in from earlier ranks
@@ -477,17 +529,34 @@ bool sharded_merge(Xfer& x, cmsbwt_ctx* ctx, int rle, RankOut& ro) {
     x.a2a(hdr.p, 24, ic, ric, hin.p);
     x.a2a(words.p, 4, wc, rwc, win.p);
     chk(cmsbwt_dm_counter(ctx, hin.p, nri, win.p, nrw, c6.data()), ctx);
+    clk.mark("halo+counter");
   }
   ro.tCounter = since_ms(tc);
   std::vector<uint64_t> mine = c6;
   mine.push_back(posLocal);
   mine.insert(mine.end(), fl.begin(), fl.end());
   auto g = x.allgather(mine);  // bad good nothing viol errs keys | positions | first last has
+  clk.mark("stats");
   uint64_t tot[7] = {0, 0, 0, 0, 0, 0, 0};
   for (auto& v : g)
     for (int k = 0; k < 7; k++) tot[k] += v[k];
   if (tot[4]) throw CtxError{CMSBWT_EINPUT, "counter target beyond the reference (reference UB)"};
-  if (tot[3]) return false;  // comparator ambiguity: redo as a gather step
+  // comparator ambiguity (or the test hook CMSBWT_DM_FORCE_GATHER=1): redo
+  // the step as a gather step, whose one-GPU merge on rank 0 holds every
+  // head (~135 B per head at 1 % divergence) -- refused with
+  // a clear error when that cannot fit rank 0's device
+  const char* fg = getenv("CMSBWT_DM_FORCE_GATHER");
+  if (tot[3] || (fg && *fg == '1')) {
+    size_t fr = 0, total = 0;
+    MCHK(hipMemGetInfo(&fr, &total));
+    if ((double)Htot * kGatherBytesPerHead > 0.9 * (double)total)
+      throw CtxError{CMSBWT_ELIMIT, "comparator ambiguity needs a gather step, and a one-GPU merge of " +
+                                        std::to_string(Htot) + " heads (~" +
+                                        std::to_string((uint64_t)((double)Htot * kGatherBytesPerHead) >> 30) +
+                                        " GiB) does not fit rank 0's device (" + std::to_string(total >> 30) +
+                                        " GiB)"};
+    return false;
+  }
   int64_t first = -1, last = -1;
   for (int s = 0; s < W; s++)
     if (g[s][9]) {
@@ -502,7 +571,9 @@ bool sharded_merge(Xfer& x, cmsbwt_ctx* ctx, int rle, RankOut& ro) {
     units.alloc(2 * Uw);
     chk(cmsbwt_dm_units(ctx, units.p), ctx);
     x.allreduce(units.p, 2 * Uw, Red::SumI64);
+    clk.mark("units+allreduce");
     chk(cmsbwt_dm_emit(ctx, units.p, &nloc), ctx);
+    clk.mark("emit");
   }
   Buf<unsigned long long> starts;
   Buf<uint8_t> chs;
@@ -524,6 +595,7 @@ bool sharded_merge(Xfer& x, cmsbwt_ctx* ctx, int rle, RankOut& ro) {
   gch.alloc(Rall);
   x.a2a(starts.p, 8, sc, rcv, gst.p);
   x.a2a(chs.p, 1, sc, rcv, gch.p);
+  clk.mark("gather_runs");
   if (rank == 0) {
     std::vector<const unsigned long long*> sp(W);
     std::vector<const uint8_t*> cp(W);
@@ -535,6 +607,7 @@ bool sharded_merge(Xfer& x, cmsbwt_ctx* ctx, int rle, RankOut& ro) {
     }
     const uint64_t gstats[8] = {Htot, tot[5], E, chars, tot[0], tot[1], tot[2], tot[3]};
     chk(cmsbwt_dm_finish(ctx, (const uint64_t* const*)sp.data(), cp.data(), counts.data(), gstats), ctx);
+    clk.mark("finish");
     ro.positions = tot[6];
     ro.first = first;
     ro.last = last;
@@ -547,6 +620,13 @@ bool sharded_merge(Xfer& x, cmsbwt_ctx* ctx, int rle, RankOut& ro) {
 int run_multi(const cmsbwt_args* a, const char* ref_path, const char* coll_path, cmsbwt_stats* stats_out) {
   const int W = a->n_gpus;
   if (W < 2 || W > 64) return CMSBWT_EARG;
+  // peer-access set-up selects devices on the caller's thread: give the
+  // caller (e.g. the Python mirror next to torch) its current device back
+  struct DeviceGuard {
+    int d = -1;
+    DeviceGuard() { if (hipGetDevice(&d) != hipSuccess) d = -1; }
+    ~DeviceGuard() { if (d >= 0) (void)hipSetDevice(d); }
+  } deviceGuard;
   const std::string out = a->outname;
   std::ofstream log(out + ".log");
   auto t0 = Clock::now();
@@ -588,6 +668,7 @@ int run_multi(const cmsbwt_args* a, const char* ref_path, const char* coll_path,
   // transport
   Rccl nccl;
   std::vector<ncclComm_t> comms;
+  std::atomic<bool> commsAborted{false};
   const bool useRccl = a->backend == CMSBWT_BACKEND_RCCL;
   if (useRccl) {
     std::vector<int> sorted = devs;
@@ -605,6 +686,10 @@ int run_multi(const cmsbwt_args* a, const char* ref_path, const char* coll_path,
       log << "ncclCommInitAll failed\n";
       return CMSBWT_EDEVICE;
     }
+    g.onFail = [&] {
+      commsAborted = true;
+      for (auto c : comms) (void)nccl.commAbort(c);
+    };
   } else {
     for (int i = 0; i < W; i++)
       for (int j = 0; j < W; j++)
@@ -720,7 +805,8 @@ int run_multi(const cmsbwt_args* a, const char* ref_path, const char* coll_path,
       cmsbwt_ctx_destroy(ctx);
     });
   for (auto& t : th) t.join();
-  for (auto c : comms) nccl.commDestroy(c);
+  if (!commsAborted)  // (an aborted communicator is already freed)
+    for (auto c : comms) nccl.commDestroy(c);
   // the first failing rank's error (ranks that left because of it report -1)
   for (int k = 0; k < W; k++)
     if (ro[k].rc > 0) {
@@ -785,4 +871,184 @@ int run_multi(const cmsbwt_args* a, const char* ref_path, const char* coll_path,
   return CMSBWT_OK;
 }
 
+
+// ---------------------------------------------------------------- rank groups
+// The multi-GPU step as a C entry point over resident inputs (bench.py
+// --gpus N without torchrun): W rank contexts the caller loads through the
+// ctx API, and one call that runs the walk and the position-sharded merge on
+// every rank (one host thread per rank, the transports above).
+struct GroupImpl {
+  int W = 0, backend = CMSBWT_BACKEND_PEER;
+  std::vector<int> devs;
+  std::vector<cmsbwt_ctx*> ctx;
+  Rccl nccl;
+  std::vector<ncclComm_t> comms;
+  std::atomic<bool> aborted{false};
+  std::string err;
+};
+
 }  // namespace cmsbwt
+
+struct cmsbwt_group {
+  cmsbwt::GroupImpl g;
+};
+
+using namespace cmsbwt;
+
+extern "C" int cmsbwt_group_create(int world, int device, int backend, cmsbwt_group** out) {
+  if (!out || world < 1 || world > 64) return CMSBWT_EARG;
+  *out = nullptr;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1 || device < 0 || device >= ndev) return CMSBWT_EDEVICE;
+  struct DeviceGuard {
+    int d = -1;
+    DeviceGuard() { if (hipGetDevice(&d) != hipSuccess) d = -1; }
+    ~DeviceGuard() { if (d >= 0) (void)hipSetDevice(d); }
+  } deviceGuard;
+  auto* G = new (std::nothrow) cmsbwt_group;
+  if (!G) return CMSBWT_ELIMIT;
+  GroupImpl& g = G->g;
+  g.W = world;
+  g.backend = backend;
+  for (int k = 0; k < world; k++) g.devs.push_back((device + k) % ndev);
+  if (backend == CMSBWT_BACKEND_RCCL && world > 1) {
+    std::vector<int> sorted = g.devs;
+    std::sort(sorted.begin(), sorted.end());
+    std::string err;
+    if (std::adjacent_find(sorted.begin(), sorted.end()) != sorted.end() || !g.nccl.load(err)) {
+      delete G;
+      return CMSBWT_EARG;
+    }
+    g.comms.resize(world);
+    if (g.nccl.commInitAll(g.comms.data(), world, g.devs.data()) != ncclSuccess) {
+      g.comms.clear();
+      delete G;
+      return CMSBWT_EDEVICE;
+    }
+  } else {
+    for (int i = 0; i < world; i++)
+      for (int j = 0; j < world; j++)
+        if (g.devs[i] != g.devs[j] && hipSetDevice(g.devs[i]) == hipSuccess &&
+            hipDeviceEnablePeerAccess(g.devs[j], 0) != hipSuccess)
+          (void)hipGetLastError();  // already enabled, or staged copies
+  }
+  for (int k = 0; k < world; k++) {
+    cmsbwt_ctx* c = nullptr;
+    const int rc = cmsbwt_ctx_create(g.devs[k], &c);
+    if (rc) {
+      cmsbwt_group_destroy(G);
+      return rc;
+    }
+    g.ctx.push_back(c);
+  }
+  *out = G;
+  return CMSBWT_OK;
+}
+
+extern "C" cmsbwt_ctx* cmsbwt_group_ctx(cmsbwt_group* G, int rank) {
+  if (!G || rank < 0 || rank >= G->g.W) return nullptr;
+  return G->g.ctx[rank];
+}
+
+extern "C" const char* cmsbwt_group_last_error(const cmsbwt_group* G) { return G ? G->g.err.c_str() : ""; }
+
+extern "C" int cmsbwt_group_step(cmsbwt_group* G, int rle, cmsbwt_rank_times* per_rank) {
+  if (!G) return CMSBWT_EARG;
+  GroupImpl& gi = G->g;
+  if (gi.aborted) {
+    gi.err = "the group's RCCL communicators were aborted by an earlier failure";
+    return CMSBWT_EDEVICE;
+  }
+  const int W = gi.W;
+  Group g(W);
+  for (int k = 0; k < W; k++) g.dev[k] = gi.devs[k];
+  const bool useRccl = gi.backend == CMSBWT_BACKEND_RCCL && W > 1;
+  if (useRccl)
+    g.onFail = [&] {
+      gi.aborted = true;
+      for (auto c : gi.comms) (void)gi.nccl.commAbort(c);
+    };
+  const char* dm = getenv("CMSBWT_DIST");
+  const bool forceGather = dm && std::string(dm) == "gather";
+  std::vector<RankOut> ro(W);
+  std::vector<std::thread> th;
+  for (int k = 0; k < W; k++)
+    th.emplace_back([&, k] {
+      cmsbwt_ctx* ctx = gi.ctx[k];
+      RankOut& r = ro[k];
+      try {
+        try {
+          MCHK(hipSetDevice(gi.devs[k]));
+          t_ctx = ctx;
+          Xfer xf(g, k, ctx_view(ctx).st, useRccl ? &gi.nccl : nullptr, useRccl ? gi.comms[k] : nullptr);
+          const bool small = ctx_view(ctx).n < 1000000;  // FN:1792
+          auto tw = Clock::now();
+          chk(cmsbwt_ms_walk(ctx), ctx);
+          r.tWalk = since_ms(tw);
+          const CtxView vw = ctx_view(ctx);
+          r.heads = vw.H;
+          r.chars = vw.chars;
+          r.walkKernelMs = vw.stats.ms_walk_kernel_ms;
+          auto tm = Clock::now();
+          if (W == 1) {
+            chk(cmsbwt_merge(ctx, rle), ctx);
+          } else if (small || forceGather) {
+            gather_merge(xf, ctx, rle, r);
+          } else if (!sharded_merge(xf, ctx, rle, r)) {
+            chk(cmsbwt_ms_walk(ctx), ctx);  // comparator ambiguity: the walk again, then a gather step
+            gather_merge(xf, ctx, rle, r);
+          }
+          MCHK(hipStreamSynchronize(ctx_view(ctx).st));
+          r.tMerge = since_ms(tm);
+          r.st.device_peak_bytes = ctx_view(ctx).devicePeak;
+        } catch (const Aborted&) {
+          r.rc = -1;
+        } catch (const CtxError& ce) {
+          r.rc = ce.code;
+          r.err = ce.msg;
+        } catch (const std::bad_alloc&) {
+          r.rc = CMSBWT_ELIMIT;
+          r.err = "host out of memory";
+        } catch (const std::exception& ex) {
+          r.rc = CMSBWT_EINTERNAL;
+          r.err = std::string("internal error: ") + ex.what();
+        }
+      } catch (...) {
+        r.rc = CMSBWT_EINTERNAL;
+        r.err = "internal error: unknown exception";
+      }
+      if (r.rc > 0) g.fail();
+      (void)hipStreamSynchronize(ctx_view(ctx).st);
+      g.final_latch();
+    });
+  for (auto& t : th) t.join();
+  for (int k = 0; k < W; k++) {
+    if (per_rank) {
+      cmsbwt_rank_times& o = per_rank[k];
+      o.walk_ms = ro[k].tWalk;
+      o.merge_ms = ro[k].tMerge;
+      o.walk_kernel_ms = ro[k].walkKernelMs;
+      o.heads = ro[k].heads;
+      o.chars = ro[k].chars;
+      o.device_peak_bytes = ro[k].st.device_peak_bytes;
+      o.gathered = ro[k].gathered ? 1 : 0;
+      o.device = gi.devs[k];
+    }
+  }
+  for (int k = 0; k < W; k++)
+    if (ro[k].rc > 0) {
+      gi.err = "rank " + std::to_string(k) + ": " + ro[k].err;
+      return ro[k].rc;
+    }
+  gi.err.clear();
+  return CMSBWT_OK;
+}
+
+extern "C" void cmsbwt_group_destroy(cmsbwt_group* G) {
+  if (!G) return;
+  GroupImpl& g = G->g;
+  for (auto c : g.ctx) cmsbwt_ctx_destroy(c);
+  if (!g.aborted)  // (an aborted communicator is already freed)
+    for (auto c : g.comms) g.nccl.commDestroy(c);
+  delete G;
+}

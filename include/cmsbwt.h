@@ -212,6 +212,29 @@ int cmsbwt_dm_copy_stream(cmsbwt_ctx* ctx, uint64_t* starts, uint8_t* chars);
 int cmsbwt_dm_finish(cmsbwt_ctx* ctx, const uint64_t* const* starts, const uint8_t* const* chars,
                      const uint64_t* counts, const uint64_t* gstats);
 
+/* Rank groups: the multi-GPU step over resident inputs (bench.py --gpus N
+ * without torchrun; the same walk + position-sharded merge as cmsbwt_run with
+ * n_gpus > 1, main.cpp:123 / FN:1788-1797).  cmsbwt_group_create makes
+ * `world` rank contexts, rank k on device (device + k) % device count (ranks
+ * may share a GPU; RCCL needs distinct GPUs); the caller loads each rank's
+ * reference and document shard through cmsbwt_group_ctx + the ctx API (the
+ * ranks' documents, in rank order, form the collection); cmsbwt_group_step
+ * runs every rank's walk and the sharded merge (one host thread per rank,
+ * synchronous) and leaves the runs and the global statistics in rank 0's
+ * context.  per_rank (world entries, may be NULL) receives the stage times. */
+typedef struct cmsbwt_group cmsbwt_group;
+typedef struct cmsbwt_rank_times {
+  double walk_ms, merge_ms, walk_kernel_ms;
+  uint64_t heads, chars, device_peak_bytes;
+  int32_t gathered; /* 1: the step ran as a gather step (one-GPU merge on rank 0) */
+  int32_t device;
+} cmsbwt_rank_times;
+int cmsbwt_group_create(int world, int device, int backend, cmsbwt_group** out);
+cmsbwt_ctx* cmsbwt_group_ctx(cmsbwt_group* g, int rank);
+int cmsbwt_group_step(cmsbwt_group* g, int rle, cmsbwt_rank_times* per_rank);
+const char* cmsbwt_group_last_error(const cmsbwt_group* g);
+void cmsbwt_group_destroy(cmsbwt_group* g);
+
 /* Self-test of the device scan / compaction primitives against host results
  * (what = "exscan" | "inscan" | "select"; offset = element offset of both
  * buffers, inplace = scan with out == in).  *mismatches = 0 when equal. */

@@ -61,3 +61,39 @@ def test_config4_sharded_bench_golden(world):
     assert out["stages_ms"]["merge"] > 0 and out["stages_ms"]["ms_walk"] > 0
     print(json.dumps({"world": world, "ms_per_step": out["ms_per_step"], "stages_ms": out["stages_ms"],
                       "per_rank": out["per_rank"], "hbm_peak_gib": out["hbm_peak_gib"]}))
+
+
+def run_bench_in_process(world, extra=(), env_extra=None, timeout=900):
+    """bench.py --gpus N without a launcher: the product's in-process rank
+    group (multi.hip, one host thread + context per rank; on a one-GPU box
+    every rank on device 0, PEER transport as device-local copies)."""
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    env.update(env_extra or {})
+    cmd = [sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", str(world), "--steps", "2", "--warmup", "1",
+           "--no-cpu", "--no-e2e", *extra]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    return json.loads(lines[0])
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_config4_in_process_bench_golden(world):
+    """`bench.py --gpus N` reports n_gpus = N with per-rank rows, and rank 0's
+    runs of the timed step equal the golden (FN:1387-1777 sharded)."""
+    out = run_bench_in_process(world)
+    g = json.load(open(os.path.join(ROOT, "tests", "golden", "golden.json")))["synth_c3"]
+    par = out["parity"]
+    assert par["verdict"] == "bit-exact vs oracle golden", par
+    assert par["heads"] == g["headNumber"] and par["rank"] == g["Rank"]
+    assert (par["counter_bad"], par["counter_good"], par["counter_nothing"]) == \
+        (g["counterBad"], g["counterGood"], g["counterDoNothing"])
+    assert out["n_gpus"] == world and len(out["per_rank"]) == world
+    assert len(out["per_rank_devices"]) == world
+    assert sum(r["chars"] for r in out["per_rank"]) == 10**10
+    assert sum(r["heads"] for r in out["per_rank"]) == g["headNumber"]
+    print(json.dumps({"world": world, "ms_per_step": out["ms_per_step"], "stages_ms": out["stages_ms"],
+                      "per_rank": out["per_rank"]}))

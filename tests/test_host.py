@@ -174,3 +174,17 @@ def test_walk_alignment_memo_search_replica(tmp_path):
     subprocess.run([shutil.which("g++") or "g++", "-O2", "-o", exe, src], check=True)
     r = subprocess.run([exe], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0 and r.stdout.strip().endswith("bad 0"), r.stdout[-500:]
+
+
+def test_bench_refuses_rank_mismatch():
+    """bench.py must not print a line whose n_gpus differs from the ranks that
+    run: --gpus 2 under WORLD_SIZE=1 exits 2 before touching a GPU."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="1", RANK="0", LOCAL_RANK="0")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2
+    assert "refusing" in json.loads(r.stdout.strip().splitlines()[-1])["error"]
