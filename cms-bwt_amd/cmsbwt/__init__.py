@@ -112,6 +112,9 @@ def load_library() -> ctypes.CDLL:
     P, U64, I32, VP = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int, ctypes.c_void_p
     sig = {
         "cmsbwt_run": (I32, [ctypes.POINTER(_Args), ctypes.c_char_p, ctypes.c_char_p, ctypes.POINTER(Stats)]),
+        "cmsbwt_run_sized": (I32, [ctypes.POINTER(_Args), U64, ctypes.c_char_p, ctypes.c_char_p,
+                                   ctypes.POINTER(Stats), U64]),
+        "cmsbwt_abi_version": (I32, []),
         "cmsbwt_ctx_create": (I32, [I32, ctypes.POINTER(P)]),
         "cmsbwt_ctx_destroy": (None, [P]),
         "cmsbwt_last_error": (ctypes.c_char_p, [P]),
@@ -171,7 +174,7 @@ def load_library() -> ctypes.CDLL:
 
 
 EXPORTED = [
-    "cmsbwt_run", "cmsbwt_ctx_create", "cmsbwt_ctx_destroy", "cmsbwt_last_error",
+    "cmsbwt_run", "cmsbwt_run_sized", "cmsbwt_abi_version", "cmsbwt_ctx_create", "cmsbwt_ctx_destroy", "cmsbwt_last_error",
     "cmsbwt_load_reference_file", "cmsbwt_load_reference", "cmsbwt_load_collection_file",
     "cmsbwt_load_collection", "cmsbwt_load_collection_synth", "cmsbwt_ms_walk", "cmsbwt_merge",
     "cmsbwt_step", "cmsbwt_get_stats", "cmsbwt_num_runs", "cmsbwt_copy_runs", "cmsbwt_write_output",
@@ -210,7 +213,8 @@ def computeBWT(arg: Args, refFileName: str, collFileName: str) -> Stats:
               1 if arg.verbose else 0, arg.n_gpus,
               CMSBWT_BACKEND_RCCL if arg.backend == "rccl" else CMSBWT_BACKEND_PEER)
     st = Stats()
-    rc = lib.cmsbwt_run(ctypes.byref(a), refFileName.encode(), collFileName.encode(), ctypes.byref(st))
+    rc = lib.cmsbwt_run_sized(ctypes.byref(a), ctypes.sizeof(a), refFileName.encode(), collFileName.encode(),
+                              ctypes.byref(st), ctypes.sizeof(st))
     if rc != CMSBWT_OK:
         raise CmsBwtError(rc, f"computeBWT failed, see {out}.log")
     return st

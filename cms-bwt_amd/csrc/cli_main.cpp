@@ -94,7 +94,7 @@ int main(int argc, char** argv) {
   std::cout << "==== Processing reference sequence" << std::endl;
   cmsbwt_args a{prefix, buffer, rle, outname.c_str(), device, verbose, ngpus, backend};
   cmsbwt_stats s{};
-  int rc = cmsbwt_run(&a, ref.c_str(), coll.c_str(), &s);
+  int rc = cmsbwt_run_sized(&a, sizeof a, ref.c_str(), coll.c_str(), &s, sizeof s);
   if (rc != CMSBWT_OK) {
     fprintf(stderr, "cmsbwt: failed with code %d (see %s.log)\n", rc, outname.c_str());
     return rc == CMSBWT_EIO ? 1 : 2 + rc;

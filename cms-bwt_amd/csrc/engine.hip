@@ -1,4 +1,5 @@
 // engine.hip — the C ABI of include/cmsbwt.h over cmsbwt::Engine (engine.h).
+#include <cstddef>
 #include "engine.h"
 #include "run_log.h"
 #include "ctx_view.h"
@@ -338,7 +339,31 @@ int cmsbwt_host_suffix_array(const uint8_t* s, uint64_t n, int32_t* sa_out) {
 // Whole run with the reference's log (FN keys in the reference's order,
 // SURVEY.md App. C): initialize_reference FN:151-310, then the large- or
 // small-reference collection pass (FN:1093-1628 / FN:312-936) and a writer.
+static int run_impl(const cmsbwt_args* a, const char* ref_path, const char* coll_path, cmsbwt_stats* stats_out);
+
+// ABI: cmsbwt_run keeps the version-1 layouts (no n_gpus/backend, stats up to
+// host_queries), so a caller built against the old header never has fields
+// read or written past its structs; cmsbwt_run_sized takes the caller's
+// struct sizes (fields it does not know read as zero: one GPU, PEER).
+int cmsbwt_abi_version(void) { return CMSBWT_ABI_VERSION; }
+
+int cmsbwt_run_sized(const cmsbwt_args* a, uint64_t args_size, const char* ref_path, const char* coll_path,
+                     cmsbwt_stats* stats_out, uint64_t stats_size) {
+  if (!a || args_size < offsetof(cmsbwt_args, n_gpus)) return CMSBWT_EARG;
+  cmsbwt_args full{};
+  memcpy(&full, a, std::min<uint64_t>(args_size, sizeof full));
+  cmsbwt_stats st{};
+  const int rc = run_impl(&full, ref_path, coll_path, &st);
+  if (stats_out) memcpy(stats_out, &st, std::min<uint64_t>(stats_size, sizeof st));
+  return rc;
+}
+
 int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path, cmsbwt_stats* stats_out) {
+  return cmsbwt_run_sized(a, offsetof(cmsbwt_args, n_gpus), ref_path, coll_path, stats_out,
+                          offsetof(cmsbwt_stats, device_peak_bytes));
+}
+
+static int run_impl(const cmsbwt_args* a, const char* ref_path, const char* coll_path, cmsbwt_stats* stats_out) {
   if (!a || !ref_path || !coll_path || !a->outname) return CMSBWT_EARG;
   if (a->n_gpus > 1) return cmsbwt::run_multi(a, ref_path, coll_path, stats_out);  // multi.hip
   std::string out = a->outname;

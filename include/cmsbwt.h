@@ -99,9 +99,19 @@ typedef struct cmsbwt_ctx cmsbwt_ctx;
 /* Whole run, replaces computeBWT (FN:1788) for the CLI: index the reference,
  * read the collection with the reference's getline semantics, compute, write
  * <outname>.rl_bwt | .bwt (+ .counterSmallerThanHead_true when _n < 1e6,
- * FN:919-924) and <outname>.log. */
+ * FN:919-924) and <outname>.log.
+ * ABI: cmsbwt_run reads and writes the version-1 layouts only (args up to
+ * `verbose`, stats up to `host_queries`), so binaries built against the
+ * version-1 header stay safe; cmsbwt_run_sized takes sizeof(cmsbwt_args) and
+ * sizeof(cmsbwt_stats) of the caller's header (unknown trailing args fields
+ * read as zero) and is what new callers use (n_gpus, backend,
+ * device_peak_bytes). */
+#define CMSBWT_ABI_VERSION 2
+int cmsbwt_abi_version(void);
 int cmsbwt_run(const cmsbwt_args* args, const char* ref_path, const char* coll_path,
                cmsbwt_stats* stats_out);
+int cmsbwt_run_sized(const cmsbwt_args* args, uint64_t args_size, const char* ref_path, const char* coll_path,
+                     cmsbwt_stats* stats_out, uint64_t stats_size);
 
 int cmsbwt_ctx_create(int device, cmsbwt_ctx** out);
 void cmsbwt_ctx_destroy(cmsbwt_ctx* ctx);

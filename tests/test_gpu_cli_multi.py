@@ -63,11 +63,14 @@ def test_cli_multi_config1_log_equals_one_gpu(built, tmp_path):
     assert sha(pre + "_3p.bwt") == g["bwt_sha256"]
 
 
-@pytest.mark.parametrize("env", [{"CMSBWT_DIST": "gather"}, {"CMSBWT_HOST_READER": "1"}],
-                         ids=["gather", "host_reader"])
+@pytest.mark.parametrize("env", [{"CMSBWT_DIST": "gather"}, {"CMSBWT_HOST_READER": "1"},
+                                 {"CMSBWT_DM_FORCE_GATHER": "1"}],
+                         ids=["gather", "host_reader", "ambiguity_fallback"])
 def test_cli_multi_gather_paths(built, tmp_path, env):
     """The gather merge (every rank's heads to rank 0, one-GPU merge there)
-    and the host reader's document split give the same golden bytes."""
+    and the host reader's document split give the same golden bytes; so does
+    the comparator-ambiguity fallback (sharded step, then the walk again and a
+    gather step), forced by its test hook."""
     g = json.load(open(os.path.join(GOLD, "golden.json")))["c1"]
     pre = str(tmp_path / "c1")
     _gen_np().gen(1_000_000, 10, 0.001, 11, pre)
