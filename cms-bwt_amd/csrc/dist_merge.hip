@@ -126,16 +126,19 @@ void Engine::dm_group(const int32_t* recv, uint64_t nrecv, uint32_t* saCounts) {
   if (nrecv >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many heads on one rank"};
   const uint32_t n = R.n;
   const uint32_t Hp = dm.Hp = (uint32_t)nrecv;
+  dmt(nullptr);
   dm.rPos.alloc(Hp); dm.rLen.alloc(Hp); dm.rIsa.alloc(Hp); dm.rTon.alloc(Hp);
   dm.rSm.alloc(Hp); dm.rCh.alloc(Hp);
   HeadsSoA r{nullptr, dm.rPos.p, dm.rLen.p, dm.rSm.p, dm.rCh.p, dm.rIsa.p, dm.rTon.p, nullptr};
   mk_dm_unpack_heads(recv, Hp, r, st);
+  dmt("unpack");
   // run buckets (FN:1162-1171) of the heads at the owned positions, from the
   // grouping's position sort: head flags of the owned positions are final,
   // the difference array is summed over ranks (a run may end in a later
   // range) with the per-SA-rank counts, in saCounts[2n .. 3n]
   runsValid = false;
   group_items(r, Hp, n, dm.IS);
+  dmt("group_items");
   if (!runsValid) {  // grouped by the composite-key sorts (keys wider than 64 bits): count them here
     diff.alloc((uint64_t)n + 1);
     diff.zero(st);
@@ -154,6 +157,7 @@ void Engine::dm_group(const int32_t* recv, uint64_t nrecv, uint32_t* saCounts) {
     mk_check_items(S, dm.IS.posBegin.p, dm.IS.posF.p, K, v.p, nullptr, st);
     dm.viol = read1(v.p);
   }
+  dmt("check");
   // slot-major members: item of each slot, received index of each slot
   dm.itemOfSlot.alloc(Hp);
   if (Hp) {
@@ -174,6 +178,8 @@ void Engine::dm_group(const int32_t* recv, uint64_t nrecv, uint32_t* saCounts) {
   HIPCHK(hipMemcpyAsync(saCounts + 2ull * n, diff.p, ((uint64_t)n + 1) * 4, hipMemcpyDeviceToDevice, st));
   HIPCHK(hipGetLastError());
   sync();
+  dmt("slots+sa_counts");
+  dmtFlush("dm_group");
 }
 
 void Engine::dm_labels(const uint32_t* saCounts, unsigned long long* back) {
@@ -346,6 +352,7 @@ void Engine::dm_counter(const int32_t* hdr, uint64_t nh, const int32_t* words, u
   if (nh + K >= 0xffffffffull || nw + Hp >= 0x7fffffffull) throw InputError{CMSBWT_ELIMIT, "halo too large"};
   const uint32_t Kh = (uint32_t)nh, Kc = Kh + K, Hc = (uint32_t)nw + Hp;
   const ItemsSoA S = dm.IS.soa();
+  dmt(nullptr);
   if (Kh == 0 && nw == 0) {  // no halo (rank 0, or one rank): the own items as they are
     DBuf<unsigned long long> cst;
     cst.alloc(8);
@@ -353,6 +360,8 @@ void Engine::dm_counter(const int32_t* hdr, uint64_t nh, const int32_t* words, u
     dm.counter.alloc((uint64_t)Hp + 1);
     dm.counter.zero(st);
     counter_phase(S, K, dm.IS.posBegin.p, dm.IS.posF.p, dm.nhr.p, dm.counter.p, cst.p, n, dm.P0, dm.P1, dm.check);
+    dmt("counter_phase");
+    dmtFlush("dm_counter");
     unsigned long long cs[8];
     HIPCHK(hipMemcpyAsync(cs, cst.p, sizeof(cs), hipMemcpyDeviceToHost, st));
     sync();
@@ -370,6 +379,7 @@ void Engine::dm_counter(const int32_t* hdr, uint64_t nh, const int32_t* words, u
   cSk.alloc(Kc); cSlot.alloc((uint64_t)Kc + 1); cNhr.alloc(std::max<uint32_t>(Hc, 1));
   ItemsSoA C{cPos.p, cLen.p, cIsa.p, cSmall.p, cUntil.p, cCount.p, nullptr, cSlot.p, nullptr, cSk.p};
   mk_dm_halo_unpack(hdr, Kh, C, st);
+  dmt("halo_unpack");
   auto cp = [&](void* d, const void* s, uint64_t b) {
     if (b) HIPCHK(hipMemcpyAsync(d, s, b, hipMemcpyDeviceToDevice, st));
   };
@@ -389,6 +399,7 @@ void Engine::dm_counter(const int32_t* hdr, uint64_t nh, const int32_t* words, u
   mk_pos_begin(cPos.p, Kc, n, pb.p, st);
   mk_pos_f(cPos.p, cSmall.p, pb.p, Kc, n, pf.p, st);
   sync();  // Hc is a stack variable
+  dmt("combine");
   if (Kc && read1(cSlot.p + (Kc - 1)) + read1(cCount.p + (Kc - 1)) != Hc)
     throw InputError{CMSBWT_EINPUT, "internal: halo payload does not match its item counts"};
   DBuf<unsigned long long> cc;
@@ -397,6 +408,8 @@ void Engine::dm_counter(const int32_t* hdr, uint64_t nh, const int32_t* words, u
   cst.alloc(8);
   cst.zero(st);
   counter_phase(C, Kc, pb.p, pf.p, cNhr.p, cc.p, cst.p, n, dm.P0, dm.P1, dm.check);
+  dmt("counter_phase");
+  dmtFlush("dm_counter");
   dm.counter.alloc((uint64_t)Hp + 1);
   dm.counter.zero(st);
   cp(dm.counter.p, cc.p + nw, (uint64_t)Hp * 8);

@@ -352,6 +352,28 @@ struct Engine {
     return tmp.p;
   }
   void sync() { HIPCHK(hipStreamSynchronize(st)); }
+  // CMSBWT_DM_TIMING=1: host-timed sub-stages of the sharded merge's calls
+  // (synchronising the stream at every mark; attribution runs only)
+  int dmtOn = -1;
+  std::chrono::steady_clock::time_point dmtT;
+  std::string dmtLine;
+  void dmt(const char* what) {
+    if (dmtOn < 0) dmtOn = env_u32("CMSBWT_DM_TIMING", 0) ? 1 : 0;
+    if (!dmtOn) return;
+    sync();
+    const auto t = std::chrono::steady_clock::now();
+    if (what) {
+      char b[80];
+      snprintf(b, sizeof b, " %s %.2f", what, std::chrono::duration<double, std::milli>(t - dmtT).count());
+      dmtLine += b;
+    }
+    dmtT = t;
+  }
+  void dmtFlush(const char* call) {
+    if (dmtOn != 1) return;
+    fprintf(stderr, "[dm-timing] rank %u %s:%s\n", dm.rank, call, dmtLine.c_str());
+    dmtLine.clear();
+  }
 
   template <class T_>
   T_ read1(const T_* d) {
@@ -1573,6 +1595,7 @@ struct Engine {
         HIPCHK(rocprim::radix_sort_pairs(nullptr, b, h.pos, posS.p, kvIn, kv.p, (size_t)H, 0u, (unsigned)bN, st));
         HIPCHK(rocprim::radix_sort_pairs(scratch(b), b, h.pos, posS.p, kvIn, kv.p, (size_t)H, 0u, (unsigned)bN, st));
 #endif
+        dmt("g.pos_sort");
         mk_pos_begin(posS.p, H, n, hb.p, st);
         // run buckets from the sorted heads: starts per position from hb,
         // ends counted in k_grp_seg (LDS histogram near the block's positions)
@@ -1589,6 +1612,7 @@ struct Engine {
         mk_grp_seg(posS.p, hb.p, kv.p, H, bN, bL, gk2.p, perm2.p, tsS.p, smS.p, bigList.p,
                    env_u32("CMSBWT_GROUP_SMALL", 64), runsHere ? diff.p : nullptr, n, st);
         if (runsHere) runsValid = true;
+        dmt("g.grp_seg");
         kv.release();
         posS.release();
         const uint32_t nb = read1(bigList.p);
@@ -1628,6 +1652,7 @@ struct Engine {
       sort_pairs(key.p, key2.p, perm.p, perm2.p, H, bN);
     }
     perm.release();
+    dmt("g.big");
     DBuf<uint32_t>& P = perm2;  // sorted members
     // items
     uint32_t K = 0;
@@ -1672,6 +1697,7 @@ struct Engine {
     }
     ItemsSoA SS = S.soa();
     mk_item_sk(SS, K, st);
+    dmt("g.items");
     order.release();
     aPos.release(); aLen.release(); aIsa.release(); aUntil.release(); aCount.release(); aFirst.release();
     aSmall.release();
@@ -1740,6 +1766,7 @@ struct Engine {
     }
     WinPlan W;
     win_prep(S, K, posBegin, n, P0, P1, check, cstatsP, W);
+    dmt("win_prep");
     counter_run(W, S, posBegin, posF, nhrP, counterP, cstatsP, n, check, hr);
     sync();
     counter_time();

@@ -308,13 +308,40 @@ __global__ void k_item_permute(ItemsSoA in, const uint32_t* __restrict__ order, 
 }
 
 // posBegin[p] = first item (map order) with pos >= p, p in [0, n]
+// posBegin[p] = first item at a position >= p (p = 0 .. n) from the sorted
+// item positions.  Interior gaps (ipos[q-1], ipos[q]] are written by item q's
+// thread, or by its whole wave when longer than 64 positions; the two end
+// gaps [0, ipos[0]] and (ipos[K-1], n] -- half the positions on each rank of
+// a sharded merge, whose items all sit in its own range -- by k_pos_ends, one
+// thread per position (one thread writing them serially took ~68 ms per rank
+// at config 3 / W = 2).
 __global__ void k_pos_begin(const uint32_t* __restrict__ ipos, uint32_t K, uint32_t n,
                             uint32_t* __restrict__ posBegin) {
-  uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
-  if (q > K) return;
-  uint32_t lo = q == 0 ? 0 : ipos[q - 1] + 1;
-  uint32_t hi = q == K ? n : ipos[q];
-  for (uint32_t p = lo; p <= hi; p++) posBegin[p] = q;
+  const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x, lane = threadIdx.x & 63;
+  const bool act = q >= 1 && q < K;  // interior gaps only
+  uint32_t lo = 1, hi = 0;
+  if (act) {
+    lo = ipos[q - 1] + 1;
+    hi = ipos[q];
+  }
+  const bool wide = act && hi >= lo && hi - lo >= 64;
+  if (act && !wide)
+    for (uint32_t p = lo; p <= hi; p++) posBegin[p] = q;
+  uint64_t m = __ballot(wide);
+  while (m) {
+    const int l = __builtin_ctzll(m);
+    m &= m - 1;
+    const uint32_t L = __shfl(lo, l), Hh = __shfl(hi, l), Q = __shfl(q, l);
+    for (uint32_t p = L + lane; p <= Hh; p += 64) posBegin[p] = Q;
+  }
+}
+__global__ void k_pos_ends(const uint32_t* __restrict__ ipos, uint32_t K, uint32_t n,
+                           uint32_t* __restrict__ posBegin) {
+  const uint64_t p = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (p > n) return;
+  if (K == 0) { posBegin[p] = 0; return; }
+  if (p <= ipos[0]) posBegin[p] = 0;
+  else if (p > ipos[K - 1]) posBegin[p] = K;
 }
 
 // posF[p] = first smaller=false item of position p (= posBegin[p+1] if none)
@@ -2189,7 +2216,8 @@ void mk_item_permute(const ItemsSoA& in, const uint32_t* order, const ItemsSoA& 
   if (K) hipLaunchKernelGGL(k_item_permute, g1(K), dim3(256), 0, st, in, order, out, K);
 }
 void mk_pos_begin(const uint32_t* ipos, uint32_t K, uint32_t n, uint32_t* posBegin, hipStream_t st) {
-  hipLaunchKernelGGL(k_pos_begin, g1((uint64_t)K + 1), dim3(256), 0, st, ipos, K, n, posBegin);
+  hipLaunchKernelGGL(k_pos_ends, g1((uint64_t)n + 1), dim3(256), 0, st, ipos, K, n, posBegin);
+  if (K > 1) hipLaunchKernelGGL(k_pos_begin, g1(K), dim3(256), 0, st, ipos, K, n, posBegin);
 }
 void mk_pos_f(const uint32_t* ipos, const uint8_t* ism, const uint32_t* posBegin, uint32_t K, uint32_t n,
               uint32_t* posF, hipStream_t st) {

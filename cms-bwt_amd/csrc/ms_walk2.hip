@@ -328,6 +328,15 @@ constexpr bool kAlignMemo = CMSBWT_ALIGN_MEMO != 0;
 #define CMSBWT_MEMO_CHECK 0
 #endif
 constexpr bool kMemoCheck = CMSBWT_MEMO_CHECK != 0;
+// experiments on the -O3 generic instance: a register
+// barrier on (pos, i, len) after a memo hit; the hit's result applied in the
+// next step's LCE phase instead of jumping to POST
+#ifndef CMSBWT_MEMO_BARRIER
+#define CMSBWT_MEMO_BARRIER 0
+#endif
+#ifndef CMSBWT_MEMO_VIA_LCE
+#define CMSBWT_MEMO_VIA_LCE 0
+#endif
 #ifndef CMSBWT_MEMO_TRACE
 #define CMSBWT_MEMO_TRACE 0
 #endif
@@ -400,6 +409,9 @@ k_ms_walk2(Walk2Args A) {
   uint32_t amAlign = 0, amLo = 0xffffffffu, amFront = 0, amC = 0;
   // CMSBWT_MEMO_CHECK builds: the memo's prediction, checked against the LCE
   uint32_t chkOn = 0, chkLen = 0, chkC = 0, chkLo = 0, chkLen0 = 0;
+#if CMSBWT_MEMO_VIA_LCE
+  uint32_t memoDone = 0;
+#endif
   // emission
   // pool blocks are reserved kPoolBatch at a time (blk .. blkEnd) and kept
   // across this lane's chunks; blocks never started keep blkChunk = ~0
@@ -603,8 +615,23 @@ k_ms_walk2(Walk2Args A) {
                  amFront - i, amAlign, amLo, amFront, amC);
       }
       len = amFront - i;
+#if CMSBWT_MEMO_BARRIER == 1
+      asm volatile("" : "+v"(pos), "+v"(i), "+v"(len));
+#elif CMSBWT_MEMO_BARRIER == 2
+      asm volatile("" : "+v"(pos));
+#elif CMSBWT_MEMO_BARRIER == 3
+      asm volatile("" : "+v"(i));
+#elif CMSBWT_MEMO_BARRIER == 4
+      asm volatile("" : "+v"(len));
+#endif
       if (amC & 0x10000u) {  // the mismatch at amFront (FN:55)
         smaller = (int8_t)(uint8_t)amC > (int8_t)(uint8_t)(amC >> 8);
+#if CMSBWT_MEMO_VIA_LCE
+        phase = PH_LCE;  // (no load) the LCE step sees m = 0 of its zero slots
+        use = 0;
+        memoDone = 1;
+        return;
+#endif
         phase = PC_POST;
         use = 0;
         return;
@@ -964,6 +991,14 @@ k_ms_walk2(Walk2Args A) {
         break;
       }
       case PH_LCE: {
+#if CMSBWT_MEMO_VIA_LCE
+        if (memoDone) {
+          memoDone = 0;
+          phase = PC_POST;
+          use = 0;
+          break;
+        }
+#endif
         uint8_t xc = 0, tc = 0;
         const uint32_t m = diff16(v0, v2, xc, tc);
         if (m < 16) {
