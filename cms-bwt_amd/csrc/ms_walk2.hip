@@ -317,9 +317,6 @@ constexpr bool kProbeNoSkip = CMSBWT_PROBE_NOSKIP != 0;
 #define CMSBWT_ALIGN_MEMO 1
 #endif
 constexpr bool kAlignMemo = CMSBWT_ALIGN_MEMO != 0;
-#ifndef CMSBWT_MEMO_GENERIC
-#define CMSBWT_MEMO_GENERIC 0
-#endif
 // diagnostic builds (CMSBWT_MEMO_CHECK=1): a memo hit only predicts; the LCE
 // runs as without the memo and the result is compared with the prediction
 // (and the predicted match end with the reference and text bounds); the
@@ -328,19 +325,13 @@ constexpr bool kAlignMemo = CMSBWT_ALIGN_MEMO != 0;
 #define CMSBWT_MEMO_CHECK 0
 #endif
 constexpr bool kMemoCheck = CMSBWT_MEMO_CHECK != 0;
-// experiments on the -O3 generic instance: a register
-// barrier on (pos, i, len) after a memo hit; the hit's result applied in the
-// next step's LCE phase instead of jumping to POST
+// the register barrier after a memo hit in the specialised instance too
+// (the generic instance always has it; A/B: +0.15 ms of walk kernel with
+// (pos, i, len) opaque)
 #ifndef CMSBWT_MEMO_BARRIER
 #define CMSBWT_MEMO_BARRIER 0
 #endif
-#ifndef CMSBWT_MEMO_VIA_LCE
-#define CMSBWT_MEMO_VIA_LCE 0
-#endif
-#ifndef CMSBWT_MEMO_TRACE
-#define CMSBWT_MEMO_TRACE 0
-#endif
-constexpr bool kMemoTrace = CMSBWT_MEMO_TRACE != 0 && !kMemoCheck;
+constexpr bool kMemoBarrier = CMSBWT_MEMO_BARRIER != 0;
 __device__ uint32_t g_memo_bad = 0;
 // waves per SIMD of the walk (Makefile W2WAVES; measured 3 -> 16.50 ms,
 // 4 -> 16.44-16.68, 5 -> 16.9, 6 -> 31.3 with register spills)
@@ -374,11 +365,9 @@ k_ms_walk2(Walk2Args A) {
   const bool pfxExact = FAST || R.pfxExact != 0;
   const bool hasLd = FAST || R.ld != nullptr;
   const bool hasIr = FAST || R.ir != nullptr;
-  // the alignment memo in the specialised instance only: in the generic one
-  // (95 SGPRs spilled to VGPR lanes) it changed results on a raw reference
-  // with N (tests/test_gpu_parity.py raw_reference_with_N) while a build with
-  // extra checking code did not -- kept out there until understood
-  const bool memo = kAlignMemo && (FAST || CMSBWT_MEMO_GENERIC);
+  // the alignment memo runs in both instances (the generic one with the
+  // register barrier at a hit, see start_lce)
+  const bool memo = kAlignMemo;
   const Lv V{lvlL, lvlL + kMaxLevels, R.nlvl, (int32_t)R.n, R.lcp};
   const uint32_t n = R.n;
   const uintptr_t X = (uintptr_t)R.x;
@@ -409,9 +398,6 @@ k_ms_walk2(Walk2Args A) {
   uint32_t amAlign = 0, amLo = 0xffffffffu, amFront = 0, amC = 0;
   // CMSBWT_MEMO_CHECK builds: the memo's prediction, checked against the LCE
   uint32_t chkOn = 0, chkLen = 0, chkC = 0, chkLo = 0, chkLen0 = 0;
-#if CMSBWT_MEMO_VIA_LCE
-  uint32_t memoDone = 0;
-#endif
   // emission
   // pool blocks are reserved kPoolBatch at a time (blk .. blkEnd) and kept
   // across this lane's chunks; blocks never started keep blkChunk = ~0
@@ -604,34 +590,14 @@ k_ms_walk2(Walk2Args A) {
         chkLo = amLo;
         chkLen0 = len;
       } else {
-      if (kMemoTrace) {
-        chkOn = 1;
-        chkLen = pos;
-        chkLo = i;
-        chkLen0 = len;
-        const uint32_t k = atomicAdd(&g_memo_bad, 1u);
-        if (k < 6)
-          printf("[memo-hit] chunk %u i %u pos %u len %u -> %u | align %u lo %u front %u c %05x\n", cid, i, pos, len,
-                 amFront - i, amAlign, amLo, amFront, amC);
-      }
       len = amFront - i;
-#if CMSBWT_MEMO_BARRIER == 1
-      asm volatile("" : "+v"(pos), "+v"(i), "+v"(len));
-#elif CMSBWT_MEMO_BARRIER == 2
-      asm volatile("" : "+v"(pos));
-#elif CMSBWT_MEMO_BARRIER == 3
-      asm volatile("" : "+v"(i));
-#elif CMSBWT_MEMO_BARRIER == 4
-      asm volatile("" : "+v"(len));
-#endif
+      // the generic instance is miscompiled here at -O2/-O3 without this
+      // register barrier: the head recorded after a hit carries pos = i + K
+      // + 1 (tools/memo_repro.py); pos made opaque (or i;
+      // not len) or -O1 keep every case bit-exact
+      if (!FAST || kMemoBarrier) asm volatile("" : "+v"(pos));
       if (amC & 0x10000u) {  // the mismatch at amFront (FN:55)
         smaller = (int8_t)(uint8_t)amC > (int8_t)(uint8_t)(amC >> 8);
-#if CMSBWT_MEMO_VIA_LCE
-        phase = PH_LCE;  // (no load) the LCE step sees m = 0 of its zero slots
-        use = 0;
-        memoDone = 1;
-        return;
-#endif
         phase = PC_POST;
         use = 0;
         return;
@@ -724,15 +690,6 @@ k_ms_walk2(Walk2Args A) {
       adj_or_finish();
     }
     if (phase == PC_POST) {  // head test and record (FN:1154-1171), then contraction
-      if (kMemoTrace && chkOn) {  // (trace builds) the state the memo hit left
-        chkOn = 0;
-        if (pos != chkLen || i != chkLo) {
-          const uint32_t k = atomicAdd(&g_memo_bad, 1u);
-          if (k < 40)
-            printf("[memo-post] chunk %u hit at i %u pos %u len0 %u; at POST i %u pos %u len %u phase-path\n", cid,
-                   chkLo, chkLen, chkLen0, i, pos, len);
-        }
-      }
       if (kMemoCheck && chkOn) {  // the LCE's result against the memo's prediction
         chkOn = 0;
         const bool mm = (chkC & 0x10000u) != 0;
@@ -991,14 +948,6 @@ k_ms_walk2(Walk2Args A) {
         break;
       }
       case PH_LCE: {
-#if CMSBWT_MEMO_VIA_LCE
-        if (memoDone) {
-          memoDone = 0;
-          phase = PC_POST;
-          use = 0;
-          break;
-        }
-#endif
         uint8_t xc = 0, tc = 0;
         const uint32_t m = diff16(v0, v2, xc, tc);
         if (m < 16) {

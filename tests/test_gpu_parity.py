@@ -66,6 +66,17 @@ def test_small_cases_rle(engine, oracle, tmp_path, case):
     _compare(engine, oracle, tmp_path, case, rle=True)
 
 
+@pytest.mark.parametrize("case", cases.small_cases(), ids=lambda c: c[0])
+def test_small_cases_generic_walk(engine, oracle, tmp_path, case):
+    """The generic walk instance on every small case: CMSBWT_PFX_GENERIC=1
+    sends DNA references there too (the specialised instance serves only DNA
+    with every table).  Both instances run the alignment memo (DESIGN.md
+    §3.1); the generic one needed a register barrier at a memo hit, without
+    which the -O2/-O3 build recorded pos = i + K + 1 for the hit's head on
+    every case here (tools/memo_repro.py) -- FN:45-88, FN:1151-1212."""
+    _compare(engine, oracle, tmp_path, case, rle=True, env={"CMSBWT_PFX_GENERIC": "1"})
+
+
 @pytest.mark.parametrize("case", cases.small_cases()[:6], ids=lambda c: c[0])
 def test_small_cases_plain_bwt(engine, oracle, tmp_path, case):
     _compare(engine, oracle, tmp_path, case, rle=False)
