@@ -66,17 +66,25 @@ def cpu_baseline(ref_len, copies, p, seed, rle=True, full_copies=None):
         if rc:
             raise RuntimeError(f"oracle rc={rc}")
     chars = ref_len * copies
-    out = {"value": round(chars / 1e6 / t_coll, 3), "unit": "MB/s", "cores": 1, "kind": "port",
-           "sample": f"{ref_len // 10**6} MB ref + {copies} copies @{p * 100:g}% ({chars / 1e6:.0f} MB collection), "
-                     f"oracle collection stage {t_coll:.2f} s, index {t_idx:.2f} s excluded",
-           "seconds": round(t_coll, 3)}
+    sample = {"value": round(chars / 1e6 / t_coll, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+              "sample": f"{ref_len // 10**6} MB ref + {copies} copies @{p * 100:g}% ({chars / 1e6:.0f} MB "
+                        f"collection), oracle collection stage {t_coll:.2f} s on this host, index {t_idx:.2f} s "
+                        "excluded",
+              "seconds": round(t_coll, 3)}
     full = golden_entry(ref_len, full_copies, p, seed) if full_copies else None
-    if full and full.get("oracle_collection_seconds"):
-        fs = full["oracle_collection_seconds"]
-        out["full_size"] = {"value": round(ref_len * full_copies / 1e6 / fs, 3), "unit": "MB/s", "seconds": fs,
-                            "cores": 1, "sample": f"the whole workload ({full_copies} copies), oracle collection "
-                                                  "stage, timed once in the build container (tests/golden/golden.json)"}
-    return out
+    if not (full and full.get("oracle_collection_seconds")):
+        return sample
+    # The counter phase (FN:1523-1603) grows with the copy count, so the
+    # bounded sample overstates the CPU's rate on the workload itself; the
+    # value is the oracle's own full-size run of this workload (timed once in
+    # the build container), the sample timed here rides beside it.
+    fs = full["oracle_collection_seconds"]
+    return {"value": round(ref_len * full_copies / 1e6 / fs, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+            "sample": f"the whole workload ({full_copies} copies, {ref_len * full_copies / 1e6:.0f} MB), oracle "
+                      f"collection stage {fs:.0f} s on one core of the build container (tests/golden/golden.json); "
+                      f"the bounded sample timed on this host is `bounded_sample`",
+            "seconds": fs, "bounded_sample": sample,
+            "sample_over_full": round(sample["value"] / (ref_len * full_copies / 1e6 / fs), 2)}
 
 
 PMC_FILE = "r04_final_pmc.json"  # tools/gpu_prof_r.sh + tools/pmc_main.py (this round's kernels)

@@ -1797,18 +1797,22 @@ struct Engine {
       mk_win_starts(W.wflag.p, W.wincl.p, n, W.winStart.p, st);
       mk_set_u32(W.winStart.p + W.nw, P1, st);
     }
+    dmt("w.windows");
     // crossing lists: (window, item) pairs sorted by window
     W.crossCnt.alloc(K);
     W.itemOff.alloc(K);
     mk_win_cross(S, K, W.wincl.p, n, W.crossCnt.p, nullptr, nullptr, nullptr, cstatsP + 4, 0, st);
     exscan(W.crossCnt.p, W.itemOff.p, 0u, K);
     W.ncross = K ? (uint32_t)sum2(W.itemOff.p + (K - 1), W.crossCnt.p + (K - 1)) : 0;
+    dmt("w.cross_count");
     W.keyW.alloc(std::max<uint32_t>(W.ncross, 1));
     W.keyW2.alloc(std::max<uint32_t>(W.ncross, 1));
     W.valQ.alloc(std::max<uint32_t>(W.ncross, 1));
     W.crossList.alloc(std::max<uint32_t>(W.ncross, 1));
     mk_win_cross(S, K, W.wincl.p, n, W.crossCnt.p, W.itemOff.p, W.keyW.p, W.valQ.p, cstatsP + 4, 1, st);
+    dmt("w.cross_fill");
     sort_pairs(W.keyW.p, W.keyW2.p, W.valQ.p, W.crossList.p, W.ncross, bits_for(W.nw));
+    dmt("w.cross_sort");
     W.crossOff.alloc((uint64_t)W.nw + 1);
     mk_win_cross_off(W.keyW2.p, W.ncross, W.nw, W.crossOff.p, st);
     if (W.tgt && !env_u32("CMSBWT_NO_IREC", 0)) {
