@@ -208,9 +208,31 @@ def sharded_step(eng, device, rle: bool = True, xfer: Transport = None):
     return sharded_merge(eng, xfer or Transport(device), rle)
 
 
+class _StageClock:
+    """CMSBWT_DM_TIMING=1: host wall time between the marks (stderr)."""
+
+    def __init__(self, rank):
+        import os
+        import time
+        self.on = os.environ.get("CMSBWT_DM_TIMING") == "1"
+        self.rank, self._time, self.t, self.parts = rank, time.perf_counter, time.perf_counter(), []
+
+    def mark(self, what):
+        if self.on:
+            t = self._time()
+            self.parts.append(f"{what} {1e3 * (t - self.t):.2f}")
+            self.t = t
+
+    def flush(self):
+        if self.on:
+            import sys
+            print(f"[py-dm-timing] rank {self.rank}: " + " ".join(self.parts), file=sys.stderr, flush=True)
+
+
 def sharded_merge(eng, x: Transport, rle: bool = True):
     from . import CMSBWT_EINPUT, CmsBwtError
     world, rank = x.world, x.rank
+    clk = _StageClock(rank)
     st = eng.stats()
     H, n = int(st.heads), int(st.n)
     meta = x.allgather_ints([H, int(st.ndocs), int(st.chars), int(st.order_invariant)])
@@ -220,12 +242,14 @@ def sharded_merge(eng, x: Transport, rle: bool = True):
     inv = all(m[3] for m in meta)
     i32, i64 = torch.int32, torch.int64
     eng.dm_begin(world, rank, Htot, E, inv, rle)
+    clk.mark("meta+begin")
     # 1-2. heads to position owners; items; initial group labels
     hc = eng.dm_route_heads(world)
     send = x.empty((H, 5), i32)
     eng.dm_pack_heads(send.data_ptr())
     rc = x.counts(hc)
     recv = x.a2a(send, hc, rc)
+    clk.mark("route+pack+a2a")
     del send
     Hp = sum(rc)
     # per-SA-rank item / head counts and the run difference array, one all-reduce
@@ -233,11 +257,13 @@ def sharded_merge(eng, x: Transport, rle: bool = True):
     eng.dm_group(recv.data_ptr(), Hp, sa.data_ptr())
     del recv
     x.allreduce(sa, "sum")
+    clk.mark("group+allreduce")
     back = x.empty(Hp, i64)  # label | unresolved << 32 (labels use all 32 bits)
     eng.dm_labels(sa.data_ptr(), back.data_ptr())
     del sa
     labels = x.a2a(back, rc, hc)
     U = eng.dm_dbl_init(labels.data_ptr())
+    clk.mark("labels+dbl_init")
     del back, labels
     # 3. prefix doubling of the head string (one count exchange per round
     # also sums the unresolved members over ranks)
@@ -255,11 +281,13 @@ def sharded_merge(eng, x: Transport, rle: bool = True):
         back = x.a2a(res, r, c)
         U = eng.dm_dbl_apply(back.data_ptr())
         h *= 2
+    clk.mark("doubling")
     # 4. head ranks / next-head ranks to the position owners
     ranks = x.empty((H, 3), i32)  # head rank, next-head rank, BWT character
     eng.dm_pack_ranks(ranks.data_ptr())
     rr = x.a2a(ranks, hc, rc)
     eng.dm_load_ranks(rr.data_ptr())
+    clk.mark("ranks")
     del ranks, rr
     # 5. counters with the halo of items reaching in from earlier ranks
     ic, wc = eng.dm_route_halo(world)
@@ -270,6 +298,7 @@ def sharded_merge(eng, x: Transport, rle: bool = True):
     hin = x.a2a(hdr, ic, ric)
     win = x.a2a(words, wc, rwc)
     c6 = eng.dm_counter(hin.data_ptr(), sum(ric), win.data_ptr(), sum(rwc))
+    clk.mark("halo+counter")
     del hdr, words, hin, win
     g = x.allgather_ints(c6)
     bad, good, nothing, viol, errs, keys = [sum(v[k] for v in g) for k in range(6)]
@@ -298,6 +327,7 @@ def sharded_merge(eng, x: Transport, rle: bool = True):
     eng.dm_units(units.data_ptr())
     x.allreduce(units, "sum")
     nloc = eng.dm_emit(units.data_ptr())
+    clk.mark("units+emit")
     del units
     starts = x.empty(nloc, i64)
     chs = x.empty(nloc, torch.uint8)
@@ -312,4 +342,6 @@ def sharded_merge(eng, x: Transport, rle: bool = True):
         sp = [gst.data_ptr() + 8 * int(offs[k]) for k in range(world)]
         cp = [gch.data_ptr() + int(offs[k]) for k in range(world)]
         eng.dm_finish(sp, cp, counts, [Htot, keys, E, chars, bad, good, nothing, viol])
+    clk.mark("gather+finish")
+    clk.flush()
     return Htot, E, chars

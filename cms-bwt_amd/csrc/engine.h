@@ -144,6 +144,7 @@ struct DevAlloc {
       return p;
     }
     void* p = nullptr;
+    mallocs++;
     if (hipMalloc(&p, bytes) != hipSuccess) {
       (void)hipGetLastError();
       trim();
@@ -159,6 +160,7 @@ struct DevAlloc {
     return p;
   }
   uint64_t live = 0, peak = 0;  // bytes handed out by get() and not yet put() back
+  uint64_t mallocs = 0, trims = 0;  // hipMalloc calls (cache misses) and full trims
   void put(void* p) {
     auto s = sizes.find(p);
     if (s == sizes.end()) { (void)hipFree(p); return; }
@@ -168,6 +170,7 @@ struct DevAlloc {
     if (cached > limit) trim();
   }
   void trim() {
+    trims++;
     (void)hipDeviceSynchronize();
     for (auto& kv : freeBlocks) {
       sizes.erase(kv.second);
@@ -357,15 +360,24 @@ struct Engine {
   int dmtOn = -1;
   std::chrono::steady_clock::time_point dmtT;
   std::string dmtLine;
+  uint64_t dmtMallocs = 0, dmtTrims = 0;
   void dmt(const char* what) {
     if (dmtOn < 0) dmtOn = env_u32("CMSBWT_DM_TIMING", 0) ? 1 : 0;
     if (!dmtOn) return;
     sync();
     const auto t = std::chrono::steady_clock::now();
     if (what) {
-      char b[80];
-      snprintf(b, sizeof b, " %s %.2f", what, std::chrono::duration<double, std::milli>(t - dmtT).count());
+      char b[96];
+      const uint64_t m = alloc.mallocs + sideAlloc.mallocs, tr = alloc.trims + sideAlloc.trims;
+      if (m != dmtMallocs || tr != dmtTrims)
+        snprintf(b, sizeof b, " %s %.2f (+%llu malloc, +%llu trim)", what,
+                 std::chrono::duration<double, std::milli>(t - dmtT).count(), (unsigned long long)(m - dmtMallocs),
+                 (unsigned long long)(tr - dmtTrims));
+      else
+        snprintf(b, sizeof b, " %s %.2f", what, std::chrono::duration<double, std::milli>(t - dmtT).count());
       dmtLine += b;
+      dmtMallocs = m;
+      dmtTrims = tr;
     }
     dmtT = t;
   }
