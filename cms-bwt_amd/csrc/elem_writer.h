@@ -1,0 +1,128 @@
+// elem_writer.h — the element writer's per-element segments (FN:1631-1777)
+// and the fused run scan of the one-GPU writer.
+//
+// Writer elements in output order: the E end phrases, then per SA rank r >= 1
+// its heads in head-rank order, or one element when it has none.  Each
+// element emits <= 3 segments (counter refchars, head character, remainder
+// quirk of FN:1761-1770 / the single remainder of FN:1678-1686); runs merge
+// across elements when the character repeats.  Shared by merge.hip (kernels)
+// and engine.h (the fused scan is a rocPRIM lookback scan whose input
+// computes each element's run summary and whose output emits its runs).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <cstddef>
+#include <iterator>
+
+#include "merge_kernels.h"
+
+namespace cmsbwt {
+
+struct ElemArgs {
+  const int32_t* sa;
+  const uint8_t* bwt;
+  const int64_t* bucket;
+  const uint32_t* posBegin;
+  const uint32_t* slot;
+  const uint32_t* itemOfSlot;
+  const uint32_t* headBase;            // per SA rank (n), exclusive head counts
+  const uint32_t* elemBase;            // per SA rank (n), exclusive element counts
+  const uint32_t* rOf;                 // per element: its SA rank
+  const uint8_t* bwtHeads;
+  const unsigned long long* counter;   // by slot
+  const unsigned long long* cum;       // by slot: inclusive sum of counter + 1
+  const uint4* info1;                  // per SA rank: element base, heads, slot base, head base
+  const unsigned long long* info2;     // per SA rank: bucket (56-bit two's complement) | BWT char << 56
+  uint32_t n, E, H;
+  int rle;
+  // position-sharded merge: head characters by local slot (one GPU: null,
+  // characters by head rank from bwtHeads)
+  const uint8_t* bwtSlot;
+};
+
+template <class F>
+__device__ __forceinline__ void d_elem_segments(const ElemArgs& A, uint32_t e, F&& f) {
+  const uint32_t r = A.rOf[e];
+  const uint4 I = A.info1[r];  // the rank's fields, read once per element (k_el_info)
+  const uint32_t k = e - I.x;
+  if (r == 0) { f(A.bwtSlot ? A.bwtSlot[I.z + k] : A.bwtHeads[k], 1ull); return; }  // end phrases (units u < E)
+  const unsigned long long J = A.info2[r];
+  const uint8_t c = (uint8_t)(J >> 56);
+  const int64_t b = ((int64_t)(J << 8)) >> 8;
+  if (b > 0) { if (k == 0) f(c, (unsigned long long)b); return; }
+  if (b == 0) return;
+  const uint32_t nh = I.y;
+  if (nh == 0) {  // no items: the item loop is empty (FN:1761-1770 / 1678-1686)
+    if (!A.rle) f(c, (unsigned long long)(-b));
+    return;
+  }
+  const uint32_t s0 = I.z, s = s0 + k;
+  const unsigned long long cs = A.counter[s];
+  if (cs) f(c, cs);
+  f(A.bwtSlot ? A.bwtSlot[s] : A.bwtHeads[I.w + k], 1ull);
+  const bool last = A.rle ? (s + 1 >= A.H || A.itemOfSlot[s + 1] != A.itemOfSlot[s]) : k + 1 == nh;
+  if (last) {
+    const int64_t acc = b + (int64_t)(A.cum[s] - (s0 ? A.cum[s0 - 1] : 0ull));
+    if (A.rle ? acc != 0 : acc < 0) f(c, (unsigned long long)(-acc));
+  }
+}
+
+
+inline ElemArgs elem_args(const ElemIn& w) {
+  return ElemArgs{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.itemOfSlot, w.headBase, w.elemBase, w.rOf,
+                  w.bwtHeads, w.counter, w.cum, w.info1, w.info2, w.n, w.E, w.H, w.rle, w.bwtSlot};
+}
+
+// Run summary of a range of elements: runs, symbols and (non-empty, last
+// char, first char).  Combining two ranges merges the run at their seam when
+// the characters agree -- an associative operation with identity {0, 0, 0}.
+struct WrState {
+  unsigned long long runs, sym;
+  uint32_t hl;  // 1 << 16 | last << 8 | first, 0 when empty
+  uint32_t pad;
+};
+struct WrOp {
+  __host__ __device__ WrState operator()(const WrState& a, const WrState& b) const {
+    const bool an = (a.hl >> 16) != 0, bn = (b.hl >> 16) != 0;
+    WrState r;
+    r.runs = a.runs + b.runs - ((an && bn && ((a.hl >> 8) & 0xffu) == (b.hl & 0xffu)) ? 1ull : 0ull);
+    r.sym = a.sym + b.sym;
+    r.hl = !bn ? a.hl : (!an ? b.hl : ((1u << 16) | (b.hl & 0xff00u) | (a.hl & 0xffu)));
+    r.pad = 0;
+    return r;
+  }
+};
+// the segments of element e, kept in registers (<= 3: counter refchars, head
+// character, remainder)
+struct ElemSegs {
+  uint32_t n;
+  uint8_t c[3];
+  unsigned long long cnt[3];
+  __device__ WrState state() const {
+    WrState s{0ull, 0ull, 0u, 0u};
+    int prev = -1;
+    for (uint32_t k = 0; k < 3; k++)
+      if (k < n) {
+        if ((int)c[k] != prev) s.runs++;
+        prev = c[k];
+        s.sym += cnt[k];
+      }
+    if (n) s.hl = (1u << 16) | ((uint32_t)c[n - 1] << 8) | (uint32_t)c[0];
+    return s;
+  }
+};
+__device__ __forceinline__ ElemSegs d_elem_collect(const ElemArgs& A, uint32_t e) {
+  ElemSegs g;
+  g.n = 0;
+  d_elem_segments(A, e, [&](uint8_t c, unsigned long long cnt) {
+    if (g.n < 3) {
+      g.c[g.n] = c;
+      g.cnt[g.n] = cnt;
+    }
+    g.n++;
+  });
+  return g;
+}
+
+}  // namespace cmsbwt

@@ -49,6 +49,7 @@
 #include "kernels.h"
 #include "map_replay.h"
 #include "merge_kernels.h"
+#include "elem_writer.h"
 #include "synth.h"
 
 namespace cmsbwt {
@@ -2336,6 +2337,30 @@ struct Engine {
       ElemIn ei{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, itemOfSlot.p, headBase.p, eBase.p, rOf.p, bwtHeads.p,
                 counter.p, cum.p, info1.p, info2.p, n, E, H, rle};
       ei.bwtSlot = bwtSlot.p;
+      if (!env_u32("CMSBWT_WR_UNFUSED", 0)) {
+        // run scan in tiles of 256 elements (merge.hip k_el_wr_tiles /
+        // k_el_wr_emit_tiles): per-tile run summaries, their scan, then each
+        // tile emits at its elements' prefixes; at most 3 runs per element
+        const uint64_t cap = 3ull * V;
+        runStart.alloc(cap); runChar.alloc(cap);
+        const uint32_t nt = (V + 255) / 256;
+        DBuf<WrState> tsum, tpre;
+        DBuf<unsigned long long> tot;
+        tsum.alloc(nt); tpre.alloc(nt); tot.alloc(2);
+        mk_el_wr_tiles(ei, V, tsum.p, st);
+        const WrState zero{0ull, 0ull, 0u, 0u};
+        size_t b = 0;
+        HIPCHK(rocprim::exclusive_scan(nullptr, b, tsum.p, tpre.p, zero, (size_t)nt, WrOp{}, st));
+        HIPCHK(rocprim::exclusive_scan(scratch(b), b, tsum.p, tpre.p, zero, (size_t)nt, WrOp{}, st));
+        mk_el_wr_emit_tiles(ei, V, tpre.p, runStart.p, runChar.p, tot.p, st);
+        unsigned long long tt[2];
+        HIPCHK(hipMemcpyAsync(tt, tot.p, sizeof(tt), hipMemcpyDeviceToHost, st));
+        sync();
+        Rn = tt[0];
+        symbols = tt[1];
+        if (Rn > cap) throw InputError{CMSBWT_EINTERNAL, "internal: writer emitted more than 3 runs per element"};
+        itemOfSlot.release();
+      } else {
       DBuf<uint32_t> wruns, whl, wprev;
       DBuf<unsigned long long> wsym, wrunOff, wsymOff;
       wruns.alloc(V); whl.alloc(V); wprev.alloc(V); wsym.alloc(V); wrunOff.alloc(V); wsymOff.alloc(V);
@@ -2375,6 +2400,7 @@ struct Engine {
       runStart.alloc(std::max<uint64_t>(Rn, 1)); runChar.alloc(std::max<uint64_t>(Rn, 1));
       mk_el_wr_emit(ei, V, wrunOff.p, packed ? nullptr : wsymOff.p, wprev.p, runStart.p, runChar.p, st);
       itemOfSlot.release();
+      }
     }
     runs.alloc(Rn * 9);
     mk_wr_records(runStart.p, runChar.p, Rn, symbols, runs.p, st);

@@ -6,6 +6,7 @@
 #include "device_common.h"
 #include "kernels.h"
 #include "merge_kernels.h"
+#include "elem_writer.h"
 
 #include <algorithm>
 #include <cstdlib>
@@ -1675,54 +1676,7 @@ __global__ void k_wr_records(const unsigned long long* __restrict__ runStart, co
 // thread reads (counter and cum by slot, bwtHeads by head rank), so a wave
 // reads contiguous memory whatever the head count of its ranks; the per-rank
 // loops of the round-1 writer diverged over 1..1000+ heads per thread.
-struct ElemArgs {
-  const int32_t* sa;
-  const uint8_t* bwt;
-  const int64_t* bucket;
-  const uint32_t* posBegin;
-  const uint32_t* slot;
-  const uint32_t* itemOfSlot;
-  const uint32_t* headBase;            // per SA rank (n), exclusive head counts
-  const uint32_t* elemBase;            // per SA rank (n), exclusive element counts
-  const uint32_t* rOf;                 // per element: its SA rank
-  const uint8_t* bwtHeads;
-  const unsigned long long* counter;   // by slot
-  const unsigned long long* cum;       // by slot: inclusive sum of counter + 1
-  const uint4* info1;                  // per SA rank: element base, heads, slot base, head base
-  const unsigned long long* info2;     // per SA rank: bucket (56-bit two's complement) | BWT char << 56
-  uint32_t n, E, H;
-  int rle;
-  // position-sharded merge: head characters by local slot (one GPU: null,
-  // characters by head rank from bwtHeads)
-  const uint8_t* bwtSlot;
-};
-
-template <class F>
-__device__ __forceinline__ void d_elem_segments(const ElemArgs& A, uint32_t e, F&& f) {
-  const uint32_t r = A.rOf[e];
-  const uint4 I = A.info1[r];  // the rank's fields, read once per element (k_el_info)
-  const uint32_t k = e - I.x;
-  if (r == 0) { f(A.bwtSlot ? A.bwtSlot[I.z + k] : A.bwtHeads[k], 1ull); return; }  // end phrases (units u < E)
-  const unsigned long long J = A.info2[r];
-  const uint8_t c = (uint8_t)(J >> 56);
-  const int64_t b = ((int64_t)(J << 8)) >> 8;
-  if (b > 0) { if (k == 0) f(c, (unsigned long long)b); return; }
-  if (b == 0) return;
-  const uint32_t nh = I.y;
-  if (nh == 0) {  // no items: the item loop is empty (FN:1761-1770 / 1678-1686)
-    if (!A.rle) f(c, (unsigned long long)(-b));
-    return;
-  }
-  const uint32_t s0 = I.z, s = s0 + k;
-  const unsigned long long cs = A.counter[s];
-  if (cs) f(c, cs);
-  f(A.bwtSlot ? A.bwtSlot[s] : A.bwtHeads[I.w + k], 1ull);
-  const bool last = A.rle ? (s + 1 >= A.H || A.itemOfSlot[s + 1] != A.itemOfSlot[s]) : k + 1 == nh;
-  if (last) {
-    const int64_t acc = b + (int64_t)(A.cum[s] - (s0 ? A.cum[s0 - 1] : 0ull));
-    if (A.rle ? acc != 0 : acc < 0) f(c, (unsigned long long)(-acc));
-  }
-}
+// ElemArgs, d_elem_segments: elem_writer.h (shared with the fused scan in engine.h)
 
 // per-rank fields of the element writer: element base, head count, slot
 // base of the rank's position, head base; bucket and BWT character
@@ -1764,6 +1718,85 @@ __global__ void k_el_rof(const uint32_t* __restrict__ elemBase, const uint32_t* 
   const uint32_t b = elemBase[r], c = m[r];
   for (uint32_t k = 0; k < c; k++) rOf[b + k] = r;
 }
+// ---- the writer's run scan in tiles of 256 elements (one block each): the
+// tile kernel reduces its elements' run summaries (WrOp, elem_writer.h) to one
+// per tile, a scan of the tile summaries gives every tile its prefix, and the
+// emit kernel scans its tile's summaries again and emits each element's runs
+// at its prefix -- two passes over the elements, no per-element arrays (the
+// unfused writer wrote and scanned five of them, CMSBWT_WR_UNFUSED=1)
+__device__ __forceinline__ WrState wr_shfl_up(const WrState& v, int d) {
+  WrState r;
+  r.runs = __shfl_up(v.runs, d);
+  r.sym = __shfl_up(v.sym, d);
+  r.hl = __shfl_up(v.hl, d);
+  r.pad = 0;
+  return r;
+}
+// block-wide exclusive scan (256 threads) of x; *total = the block's summary
+__device__ __forceinline__ WrState wr_block_exscan(WrState x, WrState* total) {
+  __shared__ WrState wt[4];
+  const uint32_t lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const WrOp op;
+  WrState inc = x;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    const WrState y = wr_shfl_up(inc, d);
+    if ((int)lane >= d) inc = op(y, inc);
+  }
+  if (lane == 63) wt[w] = inc;
+  __syncthreads();
+  const WrState zero{0ull, 0ull, 0u, 0u};
+  WrState pre = zero;
+  for (uint32_t k = 0; k < w; k++) pre = op(pre, wt[k]);
+  WrState ex = wr_shfl_up(inc, 1);
+  if (lane == 0) ex = zero;
+  if (total) *total = op(op(wt[0], wt[1]), op(wt[2], wt[3]));
+  return op(pre, ex);
+}
+__global__ void __launch_bounds__(256) k_el_wr_tiles(ElemArgs A, uint32_t V, WrState* __restrict__ tileSum) {
+  const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+  WrState s{0ull, 0ull, 0u, 0u};
+  if (e < V) s = d_elem_collect(A, e).state();
+  WrState tot;
+  (void)wr_block_exscan(s, &tot);
+  if (threadIdx.x == 0) tileSum[blockIdx.x] = tot;
+}
+__global__ void __launch_bounds__(256) k_el_wr_emit_tiles(ElemArgs A, uint32_t V, const WrState* __restrict__ tilePre,
+                                                         unsigned long long* __restrict__ runStart,
+                                                         uint8_t* __restrict__ runChar,
+                                                         unsigned long long* __restrict__ total) {
+  const uint32_t e = blockIdx.x * 256 + threadIdx.x;
+  ElemSegs g;
+  g.n = 0;
+  if (e < V) g = d_elem_collect(A, e);
+  const WrState ex = WrOp{}(tilePre[blockIdx.x], wr_block_exscan(g.state(), nullptr));
+  int prev = (ex.hl >> 16) ? (int)((ex.hl >> 8) & 0xffu) : -1;
+  unsigned long long j = ex.runs, pos = ex.sym;
+  for (uint32_t k = 0; k < 3; k++)
+    if (k < g.n) {
+      if ((int)g.c[k] != prev) {
+        runStart[j] = pos;
+        runChar[j] = g.c[k];
+        j++;
+      }
+      prev = g.c[k];
+      pos += g.cnt[k];
+    }
+  if (e + 1 == V) {
+    total[0] = j;
+    total[1] = pos;
+  }
+}
+void mk_el_wr_tiles(const ElemIn& w, uint32_t V, WrState* tileSum, hipStream_t st) {
+  if (V) hipLaunchKernelGGL(k_el_wr_tiles, dim3((V + 255) / 256), dim3(256), 0, st, elem_args(w), V, tileSum);
+}
+void mk_el_wr_emit_tiles(const ElemIn& w, uint32_t V, const WrState* tilePre, unsigned long long* runStart,
+                         uint8_t* runChar, unsigned long long* total, hipStream_t st) {
+  if (V)
+    hipLaunchKernelGGL(k_el_wr_emit_tiles, dim3((V + 255) / 256), dim3(256), 0, st, elem_args(w), V, tilePre,
+                       runStart, runChar, total);
+}
+
 __global__ void k_el_wr_count(ElemArgs A, uint32_t V, uint32_t* __restrict__ runs, unsigned long long* __restrict__ sym,
                               uint32_t* __restrict__ hl) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2368,10 +2401,6 @@ void mk_bucket(const int32_t* countIncl, const uint8_t* hasHead, uint32_t n, int
 }
 void mk_wr_adjust(const uint32_t* hl, const uint32_t* prevHL, uint32_t U, uint32_t* runs, hipStream_t st) {
   if (U) hipLaunchKernelGGL(k_wr_adjust, g1(U), dim3(256), 0, st, hl, prevHL, U, runs);
-}
-static ElemArgs elem_args(const ElemIn& w) {
-  return ElemArgs{w.sa, w.bwt, w.bucket, w.posBegin, w.slot, w.itemOfSlot, w.headBase, w.elemBase, w.rOf,
-                  w.bwtHeads, w.counter, w.cum, w.info1, w.info2, w.n, w.E, w.H, w.rle, w.bwtSlot};
 }
 void mk_win_fixed(uint32_t n, uint32_t P0, uint32_t P1, uint32_t winPos, uint32_t nw, uint32_t* wincl,
                   uint32_t* winStart, hipStream_t st) {

@@ -221,6 +221,12 @@ void mk_el_wr_count(const ElemIn& w, uint32_t V, uint32_t* runs, unsigned long l
 constexpr uint32_t kPackSymBits = 34;
 void mk_el_wr_emit(const ElemIn& w, uint32_t V, const unsigned long long* runOff, const unsigned long long* symOff,
                    const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st);
+// the writer's run scan in tiles (elem_writer.h WrState / WrOp): per-tile
+// summaries, then emission at each element's prefix; total = {runs, symbols}
+struct WrState;
+void mk_el_wr_tiles(const ElemIn& w, uint32_t V, WrState* tileSum, hipStream_t st);
+void mk_el_wr_emit_tiles(const ElemIn& w, uint32_t V, const WrState* tilePre, unsigned long long* runStart,
+                         uint8_t* runChar, unsigned long long* total, hipStream_t st);
 // element writer of the position-sharded merge (elements of the owned SA
 // ranks, units summarised for the all-reduce, emission per element)
 void mk_dm_el_count(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t E,
