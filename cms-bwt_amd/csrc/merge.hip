@@ -1216,10 +1216,14 @@ constexpr uint32_t kTgtS = 256;     // queries listed per wave for binary search
 constexpr uint32_t kNoSlot = 0xffffffffu;
 // a staged record covering all 64 targets of its wave carries this range word
 // (no window-relative range is 0xffff..ffff) and skips the range test
-#ifndef CMSBWT_TGT_FULL
-#define CMSBWT_TGT_FULL 0  // r04 A/B: 12.56-12.58 ms without, 12.67-12.73 ms with (the uniform branch costs more)
+// full-cover records walked apart from the others (CMSBWT_TGT_SPLIT=0: one
+// walk per class with the range test for every record; round 4's per-record
+// branch between the two forms measured slower, 12.67-12.73 against
+// 12.56-12.58 ms)
+#ifndef CMSBWT_TGT_SPLIT
+#define CMSBWT_TGT_SPLIT 1
 #endif
-constexpr bool kTgtFull = CMSBWT_TGT_FULL != 0;
+constexpr bool kTgtSplit = CMSBWT_TGT_SPLIT != 0;
 // attribution builds only (wrong counters): 1 staging, 2 + record walks and
 // re-tests, 3 (default) + binary searches
 #ifndef CMSBWT_TGT_PHASES
@@ -1229,6 +1233,27 @@ constexpr int kTgtPhases = CMSBWT_TGT_PHASES;
 
 
 constexpr uint32_t kFullRec = 0xffffffffu;
+
+// stable partition of list[b, e) (one wave, in place): records whose range
+// word is kFullRec first; returns their number
+__device__ __forceinline__ uint32_t tgt_partition_full(uint4* list, uint32_t b, uint32_t e, uint32_t lane) {
+  const uint32_t n = e - b;  // <= 128 (kTgtRec)
+  __builtin_amdgcn_wave_barrier();
+  uint4 v0 = make_uint4(0u, 0u, 0u, 0u), v1 = v0;
+  const bool a0 = lane < n, a1 = lane + 64 < n;
+  if (a0) v0 = list[b + lane];
+  if (a1) v1 = list[b + 64 + lane];
+  const bool f0 = a0 && v0.y == kFullRec, f1 = a1 && v1.y == kFullRec;
+  const uint64_t m0 = __ballot(f0), m1 = __ballot(f1), p0 = __ballot(a0 && !f0), p1 = __ballot(a1 && !f1);
+  const uint32_t nf0 = (uint32_t)__popcll(m0), nf = nf0 + (uint32_t)__popcll(m1);
+  const uint32_t np0 = (uint32_t)__popcll(p0);
+  const uint64_t below = (1ull << lane) - 1;
+  __builtin_amdgcn_wave_barrier();
+  if (a0) list[b + (f0 ? (uint32_t)__popcll(m0 & below) : nf + (uint32_t)__popcll(p0 & below))] = v0;
+  if (a1) list[b + (f1 ? nf0 + (uint32_t)__popcll(m1 & below) : nf + np0 + (uint32_t)__popcll(p1 & below))] = v1;
+  __builtin_amdgcn_wave_barrier();
+  return nf;
+}
 
 // v (wave-uniform) in the lanes of mask m, 0 elsewhere: one v_cndmask on the
 // SGPR-pair mask (keeps decision masks out of VGPRs)
@@ -1350,16 +1375,17 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
   // masks (SGPR pairs; the per-target flags are loop-invariant masks) and an
   // add is one v_cndmask on its mask; range tests and statistics stay on the
   // VALU (the scalar unit, one per CU, bounds this loop).
-  auto rec = [&](auto cls, const uint4& my, uint32_t r, uint32_t e, uint32_t& qn) {
+  auto rec = [&](auto cls, auto fullc, const uint4& my, uint32_t r, uint32_t e, uint32_t& qn) {
     constexpr bool S = decltype(cls)::value;
-    const uint32_t ab = __builtin_amdgcn_readlane(my.y, e);
+    constexpr bool FULL = decltype(fullc)::value;
     const uint32_t cqv = __builtin_amdgcn_readfirstlane(__builtin_amdgcn_readlane(my.z, e));
     const uint32_t L = __builtin_amdgcn_readlane(my.x, e) - t;
     uint64_t mIn, mInF;
-    if (kTgtFull && ab == kFullRec) {  // the record reaches all 64 targets of the wave: no range test
+    if (FULL) {  // the record reaches all 64 targets of the wave: no range test
       mIn = hasM;
       mInF = hasF0M;
     } else {
+      const uint32_t ab = __builtin_amdgcn_readlane(my.y, e);
       const uint32_t aO = ab & 0xffffu, span = ab >> 16;
       mIn = ucmp<kULE>(tofH - aO, span);  // targets with items
       mInF = mIn & hasF0M;                // ... and a smaller=false item
@@ -1443,7 +1469,7 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
   };
   // one walk over a wave's records of one class (smaller=true records from
   // the front of its list, smaller=false ones from the back)
-  auto walk = [&](auto cls, uint32_t rb, uint32_t re) {
+  auto walk = [&](auto cls, auto fullc, uint32_t rb, uint32_t re) {
     uint32_t r = rb;
     while (r < re) {
       uint32_t qn = 0;  // listed undecided queries (wave-uniform)
@@ -1456,10 +1482,10 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
           const uint32_t lim = min(nb, e + ((kTgtQ - qn) >> 6));
           // (unrolled by two: the loop control is scalar work too)
           for (; e + 1 < lim; e += 2) {
-            rec(cls, my, r, e, qn);
-            rec(cls, my, r, e + 1, qn);
+            rec(cls, fullc, my, r, e, qn);
+            rec(cls, fullc, my, r, e + 1, qn);
           }
-          if (e < lim) rec(cls, my, r, e++, qn);
+          if (e < lim) rec(cls, fullc, my, r, e++, qn);
         }
         r += e;
       }
@@ -1504,7 +1530,7 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
             const uint32_t a = k == (aO >> 6) ? (aO & 63u) : 0u, b = k == (bO >> 6) ? (bO & 63u) : 63u;
             nNothing += (uint32_t)__popcll(noItL[k] & (~0ull >> (63u - b)) & (~0ull << a));
             const uint32_t o = atomicAdd(&nG[2 * k + (sm ? 0 : 1)], 1u);
-            const bool full = kTgtFull && aO <= 64 * k && bO >= 64 * k + 63;
+            const bool full = kTgtSplit && aO <= 64 * k && bO >= 64 * k + 63;
             recG[k][sm ? o : kTgtRec - 1 - o] = full ? make_uint4(rec.x, kFullRec, rec.z, rec.w) : rec;
           }
         }
@@ -1512,9 +1538,21 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
     }
     __syncthreads();
     const uint32_t nS = nG[2 * wv], nF = nG[2 * wv + 1];
-    if (kTgtPhases >= 2) {
-      walk(std::true_type{}, 0u, nS);
-      walk(std::false_type{}, kTgtRec - nF, kTgtRec);
+    if (kTgtSplit) {
+      // full-cover records first in each class's list (a stable partition by
+      // the wave, <= 2 x 64 records per class), so the walks over them skip
+      // the range test and its decode (80 % of the records, 94 % of the pairs)
+      const uint32_t nSf = tgt_partition_full(recG[wv], 0u, nS, lane);
+      const uint32_t nFf = tgt_partition_full(recG[wv], kTgtRec - nF, kTgtRec, lane);
+      if (kTgtPhases >= 2) {
+        walk(std::true_type{}, std::true_type{}, 0u, nSf);
+        walk(std::true_type{}, std::false_type{}, nSf, nS);
+        walk(std::false_type{}, std::true_type{}, kTgtRec - nF, kTgtRec - nF + nFf);
+        walk(std::false_type{}, std::false_type{}, kTgtRec - nF + nFf, kTgtRec);
+      }
+    } else if (kTgtPhases >= 2) {
+      walk(std::true_type{}, std::false_type{}, 0u, nS);
+      walk(std::false_type{}, std::false_type{}, kTgtRec - nF, kTgtRec);
     }
     if (kTgtPhases < 3) nSearch = 0;
     if (nSearch) search();  // before the next chunk replaces the records
