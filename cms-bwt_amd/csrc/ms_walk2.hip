@@ -82,6 +82,7 @@ enum : uint32_t {
   PH_LCE_COOP,  // served by the whole wave (no lane load)
   // compute phases
   PC_ADJ0,
+  PC_PFX,   // (prefetch) a position whose probe entry is in registers
   PC_ADV,
   PC_POST,
   PC_CHAR,
@@ -132,6 +133,7 @@ enum : uint32_t {
   U0E = 1024, // 8 B at A
   U2E = 2048, // 8 B at B
   UREG = 4096, // (no load) the probe's next window comes from the skip's 32 text bytes
+  U3E = 8192,  // 8 B of the prefix tables at entry u8 (the prefetched probe of i + 1)
 };
 // First differing byte of two 16-byte strings: 16 if equal.
 __device__ __forceinline__ uint32_t diff16(const uint4& x, const uint4& t, uint8_t& xc, uint8_t& tc) {
@@ -325,6 +327,19 @@ constexpr bool kAlignMemo = CMSBWT_ALIGN_MEMO != 0;
 #define CMSBWT_MEMO_CHECK 0
 #endif
 constexpr bool kMemoCheck = CMSBWT_MEMO_CHECK != 0;
+// probe prefetch (specialised instance): a probe step at position i whose
+// window holds K + 1 symbols also loads the table entry of position i + 1
+// (its code is known from the same window); when the walk reaches i + 1 by
+// the next-position route, that entry is used in a second pass of the compute
+// phases of the same iteration (PC_PFX), so a mismatch region's heads (one
+// probe each) take one load step per two positions.  Measured (round 5,
+// config 3): probe lane-steps 131.9 M -> 69.3 M, wave steps 4.04 M -> 2.45 M,
+// walk kernel unchanged (12.0 ms either way, 5 VGPRs spilled with it): the
+// walk is bound by its random-line traffic, not by its dependent round
+// trips.  Off by default; CMSBWT_PFX_PREFETCH=1 builds it (bit-exact).
+#ifndef CMSBWT_PFX_PREFETCH
+#define CMSBWT_PFX_PREFETCH 0
+#endif
 // the register barrier after a memo hit in the specialised instance too
 // (the generic instance always has it; A/B: +0.15 ms of walk kernel with
 // (pos, i, len) opaque)
@@ -387,6 +402,11 @@ k_ms_walk2(Walk2Args A) {
   // code of its first wm <= K symbols in wcode
   uint4 tw = make_uint4(0, 0, 0, 0);
   uint32_t twAt = 0xffffffffu, wcode = 0, wm = 0;
+  // (prefetch) the window's 2-bit codes of all 16 bytes and its first
+  // non-symbol index; the prefetched entry (pfE) is that of position pfAt
+  constexpr bool kPrefetch = FAST && CMSBWT_PFX_PREFETCH != 0;
+  uint32_t wfull = 0, wbad = 0, pfAt = 0xffffffffu;
+  uint2 pfE = make_uint2(0u, 0u);
   // the 32 text bytes t[t32At ..) the last skip step loaded around the match
   // end: the probes of the next positions (a mismatch region) take their
   // windows from them instead of loading the text again
@@ -443,6 +463,10 @@ k_ms_walk2(Walk2Args A) {
       }
       wm = bad < K ? bad : K;
       wcode = wm ? full >> (32 - 2 * wm) : 0u;
+      if (kPrefetch) {
+        wfull = full;
+        wbad = bad;
+      }
       return;
     }
     uint32_t code = 0, m = 0;
@@ -476,6 +500,13 @@ k_ms_walk2(Walk2Args A) {
     u7 = (int32_t)m;
     ad0 = (uintptr_t)(R.pfx + pfxL[m] + 2 * code);
     use = U0E;
+    if (kPrefetch && m == R.kmerK && R.kmerK <= 15 && wbad > R.kmerK) {
+      // the entry of i + 1: symbols 1 .. K of this window
+      const uint32_t K = R.kmerK;
+      const uint32_t code1 = (wfull >> (32 - 2 * (K + 1))) & ((1u << (2 * K)) - 1u);
+      u8 = (int32_t)(pfxL[K] + 2 * code1);
+      use |= U3E;
+    }
     if (pfxExact) {
       if (i + 1 - t32At <= 16u) {
         use |= UREG;
@@ -490,6 +521,12 @@ k_ms_walk2(Walk2Args A) {
   };
   auto begin_pfx = [&]() {
     if (twAt == i) {
+      if (kPrefetch && pfAt == i && wm == R.kmerK && wm > len && !(len == 0 && !(lb == 0 && rb == (int32_t)n - 1))) {
+        phase = PC_PFX;  // (pfx_probe's load, served by the prefetched entry)
+        use = 0;
+        pfAt = 0xffffffffu;
+        return;
+      }
       pfx_probe();
     } else {
       phase = PH_PFX_TEXT;
@@ -626,6 +663,49 @@ k_ms_walk2(Walk2Args A) {
     }
   };
 
+  // the probe entry (ex, ey) of t[i..i+m) (m = u7, code = u6): FN:45-88's
+  // outcome as the binary searches would find it (PH_PFX_PROBE, and PC_PFX for
+  // a prefetched entry)
+  auto pfx_entry = [&](uint32_t ex, uint32_t ey) {
+    const uint32_t m = (uint32_t)u7, code = (uint32_t)u6, Bb = R.kmerB;
+    if (ey == (kPfxOne | 1u)) {  // t[i..i+m) occurs once, at ex: extend there (FN:52-62)
+      lb = rb = 0;
+      len = m;
+      pos = ex;
+      start_lce();
+      return;
+    }
+    if (!(ey & kPfxAns)) {  // t[i..i+m) occurs: its interval, depth m
+      lb = (int32_t)ex;
+      rb = (int32_t)(ex + ey) - 1;
+      len = m;
+      phase = PC_CHAR;
+      use = 0;
+      return;
+    }
+    // answer entry: the longest occurring prefix t[i..i+l), the insertion
+    // point's SA value and `smaller` of FN:65-76, as the binary searches
+    // from the (exact) carried interval would find them
+    len = ey & 0xffu;
+    pos = ex;
+    smaller = (ey & kPfxSmaller) != 0;
+    use = 0;
+    phase = PC_POST;
+    if (ey & kPfxSingle) {
+      lb = rb = 0;  // a one-suffix interval: the skip of FN:1175-1189 follows
+    } else if (pfxExact && wm == R.kmerK) {
+      lb = -1;  // the next position resolves by its own probe
+      rb = -2;
+    } else if (len == 0) {
+      lb = 0;
+      rb = (int32_t)n - 1;
+    } else {  // contractLeft needs the interval of t[i..i+l)
+      phase = PH_IVL;
+      ad0 = (uintptr_t)(R.pfx + pfxL[len] + 2 * (code >> (Bb * (m - len))));
+      use = U0E;
+    }
+  };
+
   while (true) {
     // ---- refill lanes from the chunk queues (one atomic per wave and band).
     // Chunks are banded by their offset inside the document; blocks that
@@ -664,6 +744,7 @@ k_ms_walk2(Walk2Args A) {
           twAt = 0xffffffffu;
           t32At = 0xfffffff0u;  // (another document's bytes)
           amLo = 0xffffffffu;
+          pfAt = 0xffffffffu;
           if (hasPfx) {
             phase = PH_PFX_TEXT;
             ad0 = T + i;
@@ -679,8 +760,11 @@ k_ms_walk2(Walk2Args A) {
       use = 0;
     }
 
-    // ---- compute phases, in chain order (ADJ0 -> POST -> ADV -> CHAR; POST reaches ADV
-    // when the contraction is dropped)
+    // ---- compute phases, in chain order (ADJ0 -> PFX -> POST -> ADV -> CHAR;
+    // POST reaches ADV when the contraction is dropped).  A second pass runs
+    // when a lane's CHAR found its probe entry prefetched (PC_PFX), so that
+    // position is settled in this iteration too.
+    for (uint32_t pass = 0;; pass++) {
     if (phase == PC_ADJ0) {  // adjustInterval(lo = u0, hi = u5, len) (FN:11-25)
       const int32_t lo = u0, hi = u5;
       uint32_t ls0;
@@ -688,6 +772,17 @@ k_ms_walk2(Walk2Args A) {
       scan_start<true>(V, hi + 1, u5, u6, u7, u8, u9);
       u4 = (int32_t)ls0;
       adj_or_finish();
+    }
+    if (kPrefetch && phase == PC_PFX) {  // pfx_probe at i with the prefetched entry
+      // the window at i + 1 from this one (15 bytes: K <= 14 symbols and the
+      // prefetch's symbol K, as the text load at i + 1 would give them)
+      const uint32_t K = R.kmerK;
+      u6 = (int32_t)wcode;
+      u7 = (int32_t)K;
+      const uint4 sh = make_uint4(__builtin_amdgcn_alignbyte(tw.y, tw.x, 1), __builtin_amdgcn_alignbyte(tw.z, tw.y, 1),
+                                  __builtin_amdgcn_alignbyte(tw.w, tw.z, 1), tw.w >> 8);
+      set_window(sh, i + 1);
+      pfx_entry(pfE.x, pfE.y);
     }
     if (phase == PC_POST) {  // head test and record (FN:1154-1171), then contraction
       if (kMemoCheck && chkOn) {  // the LCE's result against the memo's prediction
@@ -798,6 +893,8 @@ k_ms_walk2(Walk2Args A) {
         begin_search();
       }
     }
+    if (!kPrefetch || pass == 1 || !__ballot(phase == PC_PFX)) break;
+    }
 
     if (!__ballot(phase != PH_DONE)) break;
     if (STATS) {
@@ -822,6 +919,7 @@ k_ms_walk2(Walk2Args A) {
     if (use & U5Q) v5 = ldu16(ad0 + 48);
     if (use & U0E) { const uint2 w = ld8_nt(ad0); v0.x = w.x; v0.y = w.y; }
     if (use & U2E) { const uint2 w = ld8(ad2); v2.x = w.x; v2.y = w.y; }
+    if (kPrefetch && (use & U3E)) { const uint2 w = ld8_nt((uintptr_t)(R.pfx + (uint32_t)u8)); v3.x = w.x; v3.y = w.y; }
     // PLCP skip (FN:1176-1185): the exit inside the 16-entry window below
     // the match end, if it is there (skS = the skip, or ~0u)
     uint32_t skS = 0xffffffffu;
@@ -1107,47 +1205,15 @@ k_ms_walk2(Walk2Args A) {
         break;
       }
       case PH_PFX_PROBE: {  // (wm/wcode already describe the window at i + 1)
-        const uint32_t m = (uint32_t)u7, code = (uint32_t)u6, Bb = R.kmerB;
+        if (kPrefetch && (use & U3E)) {  // the entry of i + 1 rode along
+          pfE = make_uint2(v3.x, v3.y);
+          pfAt = i + 1;
+        }
         if (!pfxExact && len > 0 && (v2.x != (uint32_t)lb || v2.y != (uint32_t)(rb - lb) + 1)) {
           begin_bs();
           break;
         }
-        if (v0.y == (kPfxOne | 1u)) {  // t[i..i+m) occurs once, at v0.x: extend there (FN:52-62)
-          lb = rb = 0;
-          len = m;
-          pos = v0.x;
-          start_lce();
-          break;
-        }
-        if (!(v0.y & kPfxAns)) {  // t[i..i+m) occurs: its interval, depth m
-          lb = (int32_t)v0.x;
-          rb = (int32_t)(v0.x + v0.y) - 1;
-          len = m;
-          phase = PC_CHAR;
-          use = 0;
-          break;
-        }
-        // answer entry: the longest occurring prefix t[i..i+l), the insertion
-        // point's SA value and `smaller` of FN:65-76, as the binary searches
-        // from the (exact) carried interval would find them
-        len = v0.y & 0xffu;
-        pos = v0.x;
-        smaller = (v0.y & kPfxSmaller) != 0;
-        use = 0;
-        phase = PC_POST;
-        if (v0.y & kPfxSingle) {
-          lb = rb = 0;  // a one-suffix interval: the skip of FN:1175-1189 follows
-        } else if (pfxExact && wm == R.kmerK) {
-          lb = -1;  // the next position resolves by its own probe
-          rb = -2;
-        } else if (len == 0) {
-          lb = 0;
-          rb = (int32_t)n - 1;
-        } else {  // contractLeft needs the interval of t[i..i+l)
-          phase = PH_IVL;
-          ad0 = (uintptr_t)(R.pfx + pfxL[len] + 2 * (code >> (Bb * (m - len))));
-          use = U0E;
-        }
+        pfx_entry(v0.x, v0.y);
         break;
       }
       case PH_IVL: {
