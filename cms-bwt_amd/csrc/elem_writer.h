@@ -74,21 +74,27 @@ inline ElemArgs elem_args(const ElemIn& w) {
                   w.bwtHeads, w.counter, w.cum, w.info1, w.info2, w.n, w.E, w.H, w.rle, w.bwtSlot};
 }
 
-// Run summary of a range of elements: runs, symbols and (non-empty, last
-// char, first char).  Combining two ranges merges the run at their seam when
-// the characters agree -- an associative operation with identity {0, 0, 0}.
+// Run summary of a range of elements: runs, symbols, where its last (open)
+// run starts, and (non-empty, last char, first char).  Combining two ranges
+// merges the run at their seam when the characters agree -- an associative
+// operation with identity {0, 0, 0, 0}.
 struct WrState {
   unsigned long long runs, sym;
-  uint32_t hl;  // 1 << 16 | last << 8 | first, 0 when empty
+  unsigned long long lastStart;  // symbol offset of the last run's start in the range
+  uint32_t hl;                   // 1 << 16 | last << 8 | first, 0 when empty
   uint32_t pad;
 };
 struct WrOp {
   __host__ __device__ WrState operator()(const WrState& a, const WrState& b) const {
     const bool an = (a.hl >> 16) != 0, bn = (b.hl >> 16) != 0;
+    if (!bn) return a;
+    if (!an) return b;
+    const bool seam = ((a.hl >> 8) & 0xffu) == (b.hl & 0xffu);
     WrState r;
-    r.runs = a.runs + b.runs - ((an && bn && ((a.hl >> 8) & 0xffu) == (b.hl & 0xffu)) ? 1ull : 0ull);
+    r.runs = a.runs + b.runs - (seam ? 1ull : 0ull);
     r.sym = a.sym + b.sym;
-    r.hl = !bn ? a.hl : (!an ? b.hl : ((1u << 16) | (b.hl & 0xff00u) | (a.hl & 0xffu)));
+    r.lastStart = (seam && b.runs == 1) ? a.lastStart : a.sym + b.lastStart;
+    r.hl = (1u << 16) | (b.hl & 0xff00u) | (a.hl & 0xffu);
     r.pad = 0;
     return r;
   }
@@ -100,11 +106,14 @@ struct ElemSegs {
   uint8_t c[3];
   unsigned long long cnt[3];
   __device__ WrState state() const {
-    WrState s{0ull, 0ull, 0u, 0u};
+    WrState s{0ull, 0ull, 0ull, 0u, 0u};
     int prev = -1;
     for (uint32_t k = 0; k < 3; k++)
       if (k < n) {
-        if ((int)c[k] != prev) s.runs++;
+        if ((int)c[k] != prev) {
+          s.runs++;
+          s.lastStart = s.sym;
+        }
         prev = c[k];
         s.sym += cnt[k];
       }

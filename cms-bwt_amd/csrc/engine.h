@@ -2330,6 +2330,7 @@ struct Engine {
     uint64_t Rn = 0, symbols = 0;
     DBuf<unsigned long long> runStart;
     DBuf<uint8_t> runChar;
+    bool recordsWritten = false;
     {
       DBuf<unsigned long long> cum;
       cum.alloc(H);
@@ -2340,19 +2341,21 @@ struct Engine {
       if (!env_u32("CMSBWT_WR_UNFUSED", 0)) {
         // run scan in tiles of 256 elements (merge.hip k_el_wr_tiles /
         // k_el_wr_emit_tiles): per-tile run summaries, their scan, then each
-        // tile emits at its elements' prefixes; at most 3 runs per element
+        // tile emits at its elements' prefixes, straight into the 9-byte
+        // records; at most 3 runs per element
         const uint64_t cap = 3ull * V;
-        runStart.alloc(cap); runChar.alloc(cap);
+        runs.alloc(cap * 9);
         const uint32_t nt = (V + 255) / 256;
         DBuf<WrState> tsum, tpre;
         DBuf<unsigned long long> tot;
         tsum.alloc(nt); tpre.alloc(nt); tot.alloc(2);
         mk_el_wr_tiles(ei, V, tsum.p, st);
-        const WrState zero{0ull, 0ull, 0u, 0u};
+        const WrState zero{0ull, 0ull, 0ull, 0u, 0u};
         size_t b = 0;
         HIPCHK(rocprim::exclusive_scan(nullptr, b, tsum.p, tpre.p, zero, (size_t)nt, WrOp{}, st));
         HIPCHK(rocprim::exclusive_scan(scratch(b), b, tsum.p, tpre.p, zero, (size_t)nt, WrOp{}, st));
-        mk_el_wr_emit_tiles(ei, V, tpre.p, runStart.p, runChar.p, tot.p, st);
+        mk_el_wr_emit_tiles(ei, V, tpre.p, runs.p, tot.p, st);
+        recordsWritten = true;
         unsigned long long tt[2];
         HIPCHK(hipMemcpyAsync(tt, tot.p, sizeof(tt), hipMemcpyDeviceToHost, st));
         sync();
@@ -2402,8 +2405,10 @@ struct Engine {
       itemOfSlot.release();
       }
     }
-    runs.alloc(Rn * 9);
-    mk_wr_records(runStart.p, runChar.p, Rn, symbols, runs.p, st);
+    if (!recordsWritten) {
+      runs.alloc(Rn * 9);
+      mk_wr_records(runStart.p, runChar.p, Rn, symbols, runs.p, st);
+    }
     HIPCHK(hipGetLastError());
     sync();
     nruns = Rn;

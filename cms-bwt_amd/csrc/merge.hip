@@ -1766,6 +1766,7 @@ __device__ __forceinline__ WrState wr_shfl_up(const WrState& v, int d) {
   WrState r;
   r.runs = __shfl_up(v.runs, d);
   r.sym = __shfl_up(v.sym, d);
+  r.lastStart = __shfl_up(v.lastStart, d);
   r.hl = __shfl_up(v.hl, d);
   r.pad = 0;
   return r;
@@ -1783,7 +1784,7 @@ __device__ __forceinline__ WrState wr_block_exscan(WrState x, WrState* total) {
   }
   if (lane == 63) wt[w] = inc;
   __syncthreads();
-  const WrState zero{0ull, 0ull, 0u, 0u};
+  const WrState zero{0ull, 0ull, 0ull, 0u, 0u};
   WrState pre = zero;
   for (uint32_t k = 0; k < w; k++) pre = op(pre, wt[k]);
   WrState ex = wr_shfl_up(inc, 1);
@@ -1793,15 +1794,23 @@ __device__ __forceinline__ WrState wr_block_exscan(WrState x, WrState* total) {
 }
 __global__ void __launch_bounds__(256) k_el_wr_tiles(ElemArgs A, uint32_t V, WrState* __restrict__ tileSum) {
   const uint32_t e = blockIdx.x * 256 + threadIdx.x;
-  WrState s{0ull, 0ull, 0u, 0u};
+  WrState s{0ull, 0ull, 0ull, 0u, 0u};
   if (e < V) s = d_elem_collect(A, e).state();
   WrState tot;
   (void)wr_block_exscan(s, &tot);
   if (threadIdx.x == 0) tileSum[blockIdx.x] = tot;
 }
+// a 9-byte little-endian record (length u64, char), FN:1708-1709
+__device__ __forceinline__ void wr_record(uint8_t* o, unsigned long long len, uint8_t c) {
+#pragma unroll
+  for (int b = 0; b < 8; b++) o[b] = (uint8_t)(len >> (8 * b));
+  o[8] = c;
+}
+// each element emits its runs at its prefix; a run's record is written by the
+// element that starts the next run (its length is then known) or, for the
+// last run, by the last element
 __global__ void __launch_bounds__(256) k_el_wr_emit_tiles(ElemArgs A, uint32_t V, const WrState* __restrict__ tilePre,
-                                                         unsigned long long* __restrict__ runStart,
-                                                         uint8_t* __restrict__ runChar,
+                                                         uint8_t* __restrict__ rec,
                                                          unsigned long long* __restrict__ total) {
   const uint32_t e = blockIdx.x * 256 + threadIdx.x;
   ElemSegs g;
@@ -1809,18 +1818,19 @@ __global__ void __launch_bounds__(256) k_el_wr_emit_tiles(ElemArgs A, uint32_t V
   if (e < V) g = d_elem_collect(A, e);
   const WrState ex = WrOp{}(tilePre[blockIdx.x], wr_block_exscan(g.state(), nullptr));
   int prev = (ex.hl >> 16) ? (int)((ex.hl >> 8) & 0xffu) : -1;
-  unsigned long long j = ex.runs, pos = ex.sym;
+  unsigned long long j = ex.runs, pos = ex.sym, start = ex.lastStart;
   for (uint32_t k = 0; k < 3; k++)
     if (k < g.n) {
       if ((int)g.c[k] != prev) {
-        runStart[j] = pos;
-        runChar[j] = g.c[k];
+        if (j) wr_record(rec + 9 * (j - 1), pos - start, (uint8_t)prev);
+        start = pos;
         j++;
       }
       prev = g.c[k];
       pos += g.cnt[k];
     }
   if (e + 1 == V) {
+    if (j) wr_record(rec + 9 * (j - 1), pos - start, (uint8_t)prev);
     total[0] = j;
     total[1] = pos;
   }
@@ -1828,11 +1838,11 @@ __global__ void __launch_bounds__(256) k_el_wr_emit_tiles(ElemArgs A, uint32_t V
 void mk_el_wr_tiles(const ElemIn& w, uint32_t V, WrState* tileSum, hipStream_t st) {
   if (V) hipLaunchKernelGGL(k_el_wr_tiles, dim3((V + 255) / 256), dim3(256), 0, st, elem_args(w), V, tileSum);
 }
-void mk_el_wr_emit_tiles(const ElemIn& w, uint32_t V, const WrState* tilePre, unsigned long long* runStart,
-                         uint8_t* runChar, unsigned long long* total, hipStream_t st) {
+void mk_el_wr_emit_tiles(const ElemIn& w, uint32_t V, const WrState* tilePre, uint8_t* rec,
+                         unsigned long long* total, hipStream_t st) {
   if (V)
-    hipLaunchKernelGGL(k_el_wr_emit_tiles, dim3((V + 255) / 256), dim3(256), 0, st, elem_args(w), V, tilePre,
-                       runStart, runChar, total);
+    hipLaunchKernelGGL(k_el_wr_emit_tiles, dim3((V + 255) / 256), dim3(256), 0, st, elem_args(w), V, tilePre, rec,
+                       total);
 }
 
 __global__ void k_el_wr_count(ElemArgs A, uint32_t V, uint32_t* __restrict__ runs, unsigned long long* __restrict__ sym,
