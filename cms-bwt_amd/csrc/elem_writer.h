@@ -100,35 +100,37 @@ struct WrOp {
   }
 };
 // the segments of element e, kept in registers (<= 3: counter refchars, head
-// character, remainder)
+// character, remainder); fixed fields, never indexed at run time (an array
+// indexed by the segment count went to scratch memory)
 struct ElemSegs {
   uint32_t n;
-  uint8_t c[3];
-  unsigned long long cnt[3];
+  uint32_t c0, c1, c2;
+  unsigned long long n0, n1, n2;
+  __device__ __forceinline__ uint32_t ch(uint32_t k) const { return k == 0 ? c0 : (k == 1 ? c1 : c2); }
+  __device__ __forceinline__ unsigned long long cnt(uint32_t k) const { return k == 0 ? n0 : (k == 1 ? n1 : n2); }
   __device__ WrState state() const {
     WrState s{0ull, 0ull, 0ull, 0u, 0u};
     int prev = -1;
+#pragma unroll
     for (uint32_t k = 0; k < 3; k++)
       if (k < n) {
-        if ((int)c[k] != prev) {
+        if ((int)ch(k) != prev) {
           s.runs++;
           s.lastStart = s.sym;
         }
-        prev = c[k];
-        s.sym += cnt[k];
+        prev = (int)ch(k);
+        s.sym += cnt(k);
       }
-    if (n) s.hl = (1u << 16) | ((uint32_t)c[n - 1] << 8) | (uint32_t)c[0];
+    if (n) s.hl = (1u << 16) | (ch(n - 1) << 8) | c0;
     return s;
   }
 };
 __device__ __forceinline__ ElemSegs d_elem_collect(const ElemArgs& A, uint32_t e) {
-  ElemSegs g;
-  g.n = 0;
+  ElemSegs g{0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};
   d_elem_segments(A, e, [&](uint8_t c, unsigned long long cnt) {
-    if (g.n < 3) {
-      g.c[g.n] = c;
-      g.cnt[g.n] = cnt;
-    }
+    if (g.n == 0) { g.c0 = c; g.n0 = cnt; }
+    else if (g.n == 1) { g.c1 = c; g.n1 = cnt; }
+    else { g.c2 = c; g.n2 = cnt; }
     g.n++;
   });
   return g;

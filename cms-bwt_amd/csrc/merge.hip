@@ -1813,21 +1813,22 @@ __global__ void __launch_bounds__(256) k_el_wr_emit_tiles(ElemArgs A, uint32_t V
                                                          uint8_t* __restrict__ rec,
                                                          unsigned long long* __restrict__ total) {
   const uint32_t e = blockIdx.x * 256 + threadIdx.x;
-  ElemSegs g;
-  g.n = 0;
+  ElemSegs g{0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};
   if (e < V) g = d_elem_collect(A, e);
   const WrState ex = WrOp{}(tilePre[blockIdx.x], wr_block_exscan(g.state(), nullptr));
   int prev = (ex.hl >> 16) ? (int)((ex.hl >> 8) & 0xffu) : -1;
   unsigned long long j = ex.runs, pos = ex.sym, start = ex.lastStart;
+#pragma unroll
   for (uint32_t k = 0; k < 3; k++)
     if (k < g.n) {
-      if ((int)g.c[k] != prev) {
+      const uint32_t c = g.ch(k);
+      if ((int)c != prev) {
         if (j) wr_record(rec + 9 * (j - 1), pos - start, (uint8_t)prev);
         start = pos;
         j++;
       }
-      prev = g.c[k];
-      pos += g.cnt[k];
+      prev = (int)c;
+      pos += g.cnt(k);
     }
   if (e + 1 == V) {
     if (j) wr_record(rec + 9 * (j - 1), pos - start, (uint8_t)prev);
