@@ -204,7 +204,7 @@ def e2e_leg(args, rle):
             walls.append(time.perf_counter() - t0)
             if r.returncode:
                 return {"error": f"cmsbwt exit {r.returncode}: {r.stderr[-400:]}"}
-            stages = (r.stderr.strip().splitlines() or [""])[-1]
+            stages = " ".join(ln for ln in r.stderr.strip().splitlines() if ln.startswith(("context", "cli:")))
         out = pre + "_out" + (".rl_bwt" if rle else ".bwt")
         sha = _sha256_file(out)
         want = golden_for(args, rle)

@@ -37,6 +37,7 @@ static void print_help(char** argv) {  // main.cpp:14-24
 }
 
 int main(int argc, char** argv) {
+  const auto t0 = std::chrono::steady_clock::now();
   std::string filename, outname;
   unsigned long long prefix = UINT64_MAX;
   unsigned buffer = 2;
@@ -103,5 +104,8 @@ int main(int argc, char** argv) {
   auto t2 = std::chrono::steady_clock::now();
   std::cout << "==== Time elapsed: " << std::chrono::duration_cast<std::chrono::milliseconds>(t2 - t1).count()
             << " ms" << std::endl;
+  if (verbose)
+    fprintf(stderr, "cli: main to run %.3fs, run %.3fs\n", std::chrono::duration<double>(t1 - t0).count(),
+            std::chrono::duration<double>(t2 - t1).count());
   return 0;
 }
