@@ -2068,8 +2068,12 @@ struct Engine {
     // first sa position of each item (the BWT characters' slot base)
     DBuf<uint32_t> gItem;
     gItem.alloc(K);
-    DBuf<uint8_t> unres;  // per sa position: member of an item with >= 2 heads
-    unres.alloc((uint64_t)H + 1);
+    // per sa position: member of an item with >= 2 heads, in bit 31 of the sa
+    // entry when head indices fit 31 bits (one random store per head fewer
+    // than a byte array; CMSBWT_UNRES_BYTES=1 keeps the byte array)
+    const bool flag31 = H < 0x80000000u && !env_u32("CMSBWT_UNRES_BYTES", 0);
+    DBuf<uint8_t> unres;
+    if (!flag31) unres.alloc((uint64_t)H + 1);
     {
       DBuf<uint32_t> rankBase, gBase;
       rankBase.alloc(n);
@@ -2077,7 +2081,7 @@ struct Engine {
       mk_pos_rank_base(posBegin.p, sSlot.p, disa.p, itemRankBase.p, headBase.p, n, E, keepT ? rankBase.p : nullptr,
                        gBase.p, st);
       mk_ranks_slot(S, itemOfSlot.p, PmP, H, rankBase.p, gBase.p, n, keepT ? T.p : nullptr, saT.p, grp.p, nullptr,
-                    st, gItem.p, unres.p);
+                    st, gItem.p, flag31 ? nullptr : unres.p, flag31 ? 0x80000000u : 0u);
     }
     // (enqueued after the ranks: the host waits for the side stream's
     // crossing count while the main stream ranks)
@@ -2168,11 +2172,13 @@ struct Engine {
         DBuf<uint32_t> tc, to;
         tc.alloc(nt);
         to.alloc(nt);
-        mk_sel_count8(unres.p, nf, tc.p, st);
+        if (flag31) mk_sel_count31(saT.p, nf, tc.p, st);
+        else mk_sel_count8(unres.p, nf, tc.p, st);
         exscan(tc.p, to.p, 0u, nt);
         U = (uint32_t)sum2(to.p + (nt - 1), tc.p + (nt - 1));
         act.alloc(std::max<uint32_t>(U, 1)); act2.alloc(std::max<uint32_t>(U, 1));
-        mk_sel_write_idx8(unres.p, nf, to.p, act.p, st);
+        if (flag31) mk_sel_write_idx31(saT.p, nf, to.p, act.p, st);
+        else mk_sel_write_idx8(unres.p, nf, to.p, act.p, st);
         unres.release();
       }
       DBuf<uint64_t> k64, k64b;
@@ -2188,7 +2194,7 @@ struct Engine {
       gflag.alloc(U); bigList.alloc((uint64_t)U + 1);
       for (uint64_t hstep = 1; U > 0; hstep <<= 1) {
         if (hstep > H) throw InputError{CMSBWT_EINPUT, "internal: head-string suffix sort did not converge"};
-        mk_dbl_keys(act.p, saT.p, grp.p, (uint32_t)hstep, U, k64.p, val.p, st);
+        mk_dbl_keys(act.p, saT.p, grp.p, (uint32_t)hstep, U, k64.p, val.p, st, flag31 ? 0x7fffffffu : 0xffffffffu);
         HIPCHK(hipMemsetAsync(bigList.p, 0, 4, st));
         if (rankPath) {
           mk_dbl_rank(U, act.p, k64.p, val.p, saT.p, grp.p, keep.p, bigList.p, maxSmall, st);
@@ -2218,6 +2224,10 @@ struct Engine {
     // Every group is a single head now, and a group's label is its first sa
     // position: grp[idx] = 1 + rank of head idx (FN:1468-1471's rankToHead),
     // so the inverse permutation needs no scatter.
+    // (members never moved by the sort keep the flag: cleared for the
+    // parity copies and the BWTheads gather, the only later readers of sa)
+    if (flag31 && keepT) mk_and_u32(saT.p, (uint64_t)H + 1, 0x7fffffffu, st);
+    saFlagged = flag31 && !keepT;
     HIPCHK(hipEventRecord(evm[2], st));
     rthFL.alloc(2);
     HIPCHK(hipMemcpyAsync(rthFL.p, grp.p, 4, hipMemcpyDeviceToDevice, st));
@@ -2482,6 +2492,7 @@ struct Engine {
   }
   float counter_kernel_ms = 0;
   bool keptT = false;  // rank2head written by the last merge
+  bool saFlagged = false;  // saT may hold k_ranks_slot's bit-31 flags (cleared before a copy)
   uint32_t windows = 0, crossings = 0;
   uint64_t eqListed = 0;  // equal-key counter queries answered after the ranks (last merge)
   bool orderInvariant = false;  // set by ms_walk (k_finalize), false for imported shards
@@ -2723,7 +2734,13 @@ struct Engine {
       if (!keptT) throw InputError{CMSBWT_EARG, "rank2head is kept only with CMSBWT_KEEP_STAGES=1"};
       return cp(T.p, ((uint64_t)H + 1) * 4);
     }
-    if (name == "head2rank") return cp(saT.p, ((uint64_t)H + 1) * 4);
+    if (name == "head2rank") {
+      if (out && saFlagged) {  // unresolved flags left in bit 31 (merge: flag31)
+        mk_and_u32(saT.p, (uint64_t)H + 1, 0x7fffffffu, st);
+        saFlagged = false;
+      }
+      return cp(saT.p, ((uint64_t)H + 1) * 4);
+    }
     if (name == "bwtheads") return cp(bwtHeads.p, H);
     if (name == "counters") return cp(counter.p, ((uint64_t)H + 1) * 8);
     throw InputError{CMSBWT_EARG, "unknown array " + name};

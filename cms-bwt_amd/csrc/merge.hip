@@ -404,10 +404,10 @@ __global__ void k_sa_counts(const int32_t* __restrict__ sa, const uint32_t* __re
 // prefix doubling: key = (group of suffix, group of suffix + h)
 __global__ void k_dbl_keys(const uint32_t* __restrict__ act, const uint32_t* __restrict__ sa,
                            const uint32_t* __restrict__ grp, uint32_t h, uint32_t U,
-                           uint64_t* __restrict__ key, uint32_t* __restrict__ val) {
+                           uint64_t* __restrict__ key, uint32_t* __restrict__ val, uint32_t saMask) {
   uint32_t u = blockIdx.x * blockDim.x + threadIdx.x;
   if (u >= U) return;
-  uint32_t idx = sa[act[u]];
+  uint32_t idx = sa[act[u]] & saMask;  // (k_ranks_slot's unresolved flag cleared)
   key[u] = ((uint64_t)grp[idx] << 32) | grp[idx + h];
   val[u] = idx;
 }
@@ -650,7 +650,7 @@ __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ ite
                              const uint32_t* __restrict__ Pm, uint32_t H, const uint32_t* __restrict__ rankBase,
                              const uint32_t* __restrict__ gBase, uint32_t n, int32_t* __restrict__ T,
                              uint32_t* __restrict__ sa, uint32_t* __restrict__ grp, uint32_t* __restrict__ actv,
-                             uint32_t* __restrict__ gItem, uint8_t* __restrict__ unres) {
+                             uint32_t* __restrict__ gItem, uint8_t* __restrict__ unres, uint32_t saFlag) {
   uint32_t s = blockIdx.x * blockDim.x + threadIdx.x;
   if (s >= H) return;
   if (unres && s == 0) unres[0] = 0;  // sa position 0: the sentinel
@@ -670,11 +670,13 @@ __global__ void k_ranks_slot(const ItemsSoA it, const uint32_t* __restrict__ ite
   // head rank is g - 1 whatever the suffix sort does inside it
   if (gItem && m == 0) gItem[q] = g;
   if (T) T[idx] = (int32_t)(rankBase[p] + q);  // rank2head: kept for parity copies only
-  sa[g + m] = idx;
+  // unresolved members (items with >= 2 heads): their sa positions, flagged
+  // in bit 31 of the sa entry (saFlag, H < 2^31) or in a byte per position
+  const bool ur = it.count[q] >= 2;
+  sa[g + m] = idx | (ur ? saFlag : 0u);
   grp[idx] = g;
-  // unresolved members (items with >= 2 heads): their sa positions
-  if (actv) actv[s] = it.count[q] >= 2 ? g + m : 0xffffffffu;
-  if (unres) unres[g + m] = it.count[q] >= 2 ? 1 : 0;
+  if (actv) actv[s] = ur ? g + m : 0xffffffffu;
+  if (unres) unres[g + m] = ur ? 1 : 0;
 }
 // next-head rank of each member, in slot order (FN:1480-1494): first per head
 // in document order (nexthead is small, so headRank[idx + nexthead] is read
@@ -2189,6 +2191,27 @@ void mk_sel_write(const uint32_t* in, const uint32_t* flags, uint32_t n, const u
                   hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_sel_write<uint32_t>, dim3(sel_tiles(n)), dim3(256), 0, st, in, flags, n, tileOff, out);
 }
+// flags in bit 31 of u32 words (k_ranks_slot's sa entries)
+struct Bit31 {
+  uint32_t v;
+  __device__ bool operator!=(int) const { return (v >> 31) != 0; }
+};
+void mk_sel_count31(const uint32_t* words, uint32_t n, uint32_t* tileCnt, hipStream_t st) {
+  if (n)
+    hipLaunchKernelGGL(k_sel_count<Bit31>, dim3(sel_tiles(n)), dim3(256), 0, st, (const Bit31*)words, n, tileCnt);
+}
+void mk_sel_write_idx31(const uint32_t* words, uint32_t n, const uint32_t* tileOff, uint32_t* out, hipStream_t st) {
+  if (n)
+    hipLaunchKernelGGL(k_sel_write<Bit31>, dim3(sel_tiles(n)), dim3(256), 0, st, nullptr, (const Bit31*)words, n,
+                       tileOff, out);
+}
+__global__ void k_and_u32(uint32_t* __restrict__ p, uint64_t n, uint32_t m) {
+  const uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) p[i] &= m;
+}
+void mk_and_u32(uint32_t* p, uint64_t n, uint32_t m, hipStream_t st) {
+  if (n) hipLaunchKernelGGL(k_and_u32, g1(n), dim3(256), 0, st, p, n, m);
+}
 void mk_sel_count8(const uint8_t* flags, uint32_t n, uint32_t* tileCnt, hipStream_t st) {
   if (n) hipLaunchKernelGGL(k_sel_count<uint8_t>, dim3(sel_tiles(n)), dim3(256), 0, st, flags, n, tileCnt);
 }
@@ -2236,10 +2259,10 @@ void mk_pos_rank_base(const uint32_t* posBegin, const uint32_t* slot, const uint
 }
 void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
                    const uint32_t* rankBase, const uint32_t* gBase, uint32_t n, int32_t* T, uint32_t* sa,
-                   uint32_t* grp, uint32_t* actv, hipStream_t st, uint32_t* gItem, uint8_t* unres) {
+                   uint32_t* grp, uint32_t* actv, hipStream_t st, uint32_t* gItem, uint8_t* unres, uint32_t saFlag) {
   if (H)
     hipLaunchKernelGGL(k_ranks_slot, g1(H), dim3(256), 0, st, it, itemOfSlot, Pm, H, rankBase, gBase, n, T, sa, grp,
-                       actv, gItem, unres);
+                       actv, gItem, unres, saFlag);
 }
 void mk_head_chars_slot(const uint32_t* Pm, const uint32_t* grp, const uint8_t* lchar, const ItemsSoA& it,
                         const uint32_t* itemOfSlot, const uint32_t* gItem, uint32_t H, uint8_t* bwtSlot,
@@ -2314,8 +2337,8 @@ void mk_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t* s
   hipLaunchKernelGGL(k_sa_counts, g1(n), dim3(256), 0, st, sa, posBegin, slot, n, E, itemsSA, headsSA);
 }
 void mk_dbl_keys(const uint32_t* act, const uint32_t* sa, const uint32_t* grp, uint32_t h, uint32_t U,
-                 uint64_t* key, uint32_t* val, hipStream_t st) {
-  if (U) hipLaunchKernelGGL(k_dbl_keys, g1(U), dim3(256), 0, st, act, sa, grp, h, U, key, val);
+                 uint64_t* key, uint32_t* val, hipStream_t st, uint32_t saMask) {
+  if (U) hipLaunchKernelGGL(k_dbl_keys, g1(U), dim3(256), 0, st, act, sa, grp, h, U, key, val, saMask);
 }
 void mk_dbl_apply(const uint32_t* act, const uint64_t* key, const uint32_t* val, uint32_t U, uint32_t* sa,
                   uint32_t* lab, hipStream_t st) {

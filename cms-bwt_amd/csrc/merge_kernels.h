@@ -50,9 +50,13 @@ void mk_pos_rank_base(const uint32_t* posBegin, const uint32_t* slot, const uint
 void mk_ranks_slot(const ItemsSoA& it, const uint32_t* itemOfSlot, const uint32_t* Pm, uint32_t H,
                    const uint32_t* rankBase, const uint32_t* gBase, uint32_t n, int32_t* T, uint32_t* sa,
                    uint32_t* grp, uint32_t* actv, hipStream_t st, uint32_t* gItem = nullptr,
-                   uint8_t* unres = nullptr);
+                   uint8_t* unres = nullptr, uint32_t saFlag = 0u);
 // byte-flag compaction into the kept indices (k_sel_count / k_sel_write)
 void mk_sel_count8(const uint8_t* flags, uint32_t n, uint32_t* tileCnt, hipStream_t st);
+// the same over bit 31 of u32 words; p[i] &= m
+void mk_sel_count31(const uint32_t* words, uint32_t n, uint32_t* tileCnt, hipStream_t st);
+void mk_sel_write_idx31(const uint32_t* words, uint32_t n, const uint32_t* tileOff, uint32_t* out, hipStream_t st);
+void mk_and_u32(uint32_t* p, uint64_t n, uint32_t m, hipStream_t st);
 void mk_sel_write_idx8(const uint8_t* flags, uint32_t n, const uint32_t* tileOff, uint32_t* out, hipStream_t st);
 // the character before each head at slot[q] + rank - (gItem[q] - 1)
 void mk_head_chars_slot(const uint32_t* Pm, const uint32_t* grp, const uint8_t* lchar, const ItemsSoA& it,
@@ -101,7 +105,7 @@ void mk_check_items(const ItemsSoA& it, const uint32_t* posBegin, const uint32_t
 void mk_sa_counts(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t E,
                   uint32_t* itemsSA, uint32_t* headsSA, hipStream_t st);
 void mk_dbl_keys(const uint32_t* act, const uint32_t* sa, const uint32_t* grp, uint32_t h, uint32_t U,
-                 uint64_t* key, uint32_t* val, hipStream_t st);
+                 uint64_t* key, uint32_t* val, hipStream_t st, uint32_t saMask = 0xffffffffu);
 void mk_dbl_apply(const uint32_t* act, const uint64_t* key, const uint32_t* val, uint32_t U, uint32_t* sa,
                   uint32_t* lab, hipStream_t st);
 void mk_dbl_groups(const uint32_t* act, const uint64_t* key, const uint32_t* val, const uint32_t* labMax,

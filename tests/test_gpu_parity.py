@@ -165,14 +165,16 @@ def test_grouping_position_first(engine, oracle, tmp_path, case, env):
 
 @pytest.mark.parametrize("env", [{"CMSBWT_DBL_SMALL": "2"}, {"CMSBWT_DBL_SMALL": "1000000"},
                                  {"CMSBWT_DBL_LEADERS": "1"}, {"CMSBWT_DBL_LEADERS": "1", "CMSBWT_DBL_SMALL": "2"},
-                                 {"CMSBWT_NHR_SORT": "1"}],
-                         ids=["radix_groups", "member_ranks", "leader_sorts", "leader_radix", "nhr_item_sorts"])
+                                 {"CMSBWT_NHR_SORT": "1"}, {"CMSBWT_UNRES_BYTES": "1"}],
+                         ids=["radix_groups", "member_ranks", "leader_sorts", "leader_radix", "nhr_item_sorts",
+                              "unresolved_byte_flags"])
 @pytest.mark.parametrize("case", cases.small_cases()[:4], ids=lambda c: c[0])
 def test_doubling_group_paths(engine, oracle, tmp_path, case, env):
     """Head-string suffix sort: groups above CMSBWT_DBL_SMALL members go through
     the radix path, smaller ones are ranked per member (default) or sorted by
     their leader thread; all give the oracle's SA.  Next-head ranks (FN:1480-
-    1494) ranked per slot (default) or sorted per item."""
+    1494) ranked per slot (default) or sorted per item.  Unresolved members
+    flagged in bit 31 of their sa entry (default) or in a byte per position."""
     _compare(engine, oracle, tmp_path, case, env=env)
 
 
