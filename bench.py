@@ -87,7 +87,7 @@ def cpu_baseline(ref_len, copies, p, seed, rle=True, full_copies=None):
             "sample_over_full": round(sample["value"] / (ref_len * full_copies / 1e6 / fs), 2)}
 
 
-PMC_FILE = "r05_pmc.json"  # tools/gpu_round_prof.sh: tools/gpu_prof_r.sh + tools/pmc_main.py (this round's kernels)
+PMC_FILE = "r05_final_pmc.json"  # tools/gpu_round_prof.sh: tools/gpu_prof_r.sh + tools/pmc_main.py (this round's kernels)
 
 # Algorithmic bytes of the MS walk (k_ms_walk2) -- what THIS algorithm must
 # move, each byte counted once (DESIGN.md §3.1 "Roofline"):
