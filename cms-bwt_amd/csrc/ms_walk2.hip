@@ -353,6 +353,14 @@ __device__ uint32_t g_memo_bad = 0;
 #ifndef CMSBWT_W2_WAVES
 #define CMSBWT_W2_WAVES 4
 #endif
+// head records staged per lane in LDS and stored four at a time (one 64-byte
+// piece of the lane's pool block) instead of one 16-byte store per head,
+// which left every head's record a partial line of its own on the fabric
+#ifndef CMSBWT_HEAD_BUF
+#define CMSBWT_HEAD_BUF 1
+#endif
+constexpr bool kHeadBuf = CMSBWT_HEAD_BUF != 0;
+static_assert(sizeof(HeadRec) == sizeof(uint4), "head records are stored as uint4");
 template <bool STATS, bool FAST>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CMSBWT_W2_WAVES, 8)))
 k_ms_walk2(Walk2Args A) {
@@ -360,6 +368,7 @@ k_ms_walk2(Walk2Args A) {
   __shared__ uint8_t kmapL[256];
   __shared__ uint32_t lvlL[2 * kMaxLevels];
   __shared__ uint32_t pfxL[17];
+  __shared__ uint4 hbuf[kHeadBuf ? 4 : 1][256];  // 16 KB: four records per lane (slot-major: no bank conflicts)
   if (STATS && threadIdx.x < 32) sc[threadIdx.x] = 0;
   if (A.R.pfx) kmapL[threadIdx.x] = A.R.kmap[threadIdx.x];  // blockDim == 256
   if (threadIdx.x < 17) pfxL[threadIdx.x] = A.R.pfxOff[threadIdx.x];
@@ -821,7 +830,14 @@ k_ms_walk2(Walk2Args A) {
           if (blk < A.pool.capBlocks) { A.pool.blkChunk[blk] = cid; A.pool.blkSeq[blk] = seq; }
           seq++;
         }
-        if (blk < A.pool.capBlocks) {
+        if (kHeadBuf) {
+          hbuf[fill & 3][threadIdx.x] = make_uint4(i, pos, len, smaller ? 1u : 0u);
+          if ((fill & 3) == 3 && blk < A.pool.capBlocks) {  // a full 64-byte piece of the block
+            uint4* dst = (uint4*)(A.pool.rec + (uint64_t)blk * kPoolB + (fill - 3));
+#pragma unroll
+            for (uint32_t k = 0; k < 4; k++) dst[k] = hbuf[k][threadIdx.x];
+          }
+        } else if (blk < A.pool.capBlocks) {
           HeadRec r;
           r.start = i;
           r.pos = pos;
@@ -873,6 +889,10 @@ k_ms_walk2(Walk2Args A) {
         A.chunkCount[cid] = count;
         phase = PH_NEXT;
         use = 0;
+        if (kHeadBuf && fill != kPoolB && (fill & 3) && blk < A.pool.capBlocks) {  // the chunk's last records
+          uint4* dst = (uint4*)(A.pool.rec + (uint64_t)blk * kPoolB + (fill & ~3u));
+          for (uint32_t k = 0; k < (fill & 3); k++) dst[k] = hbuf[k][threadIdx.x];
+        }
       } else {
         phase = PC_CHAR;
       }
