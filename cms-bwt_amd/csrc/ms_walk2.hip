@@ -353,13 +353,17 @@ __device__ uint32_t g_memo_bad = 0;
 #ifndef CMSBWT_W2_WAVES
 #define CMSBWT_W2_WAVES 4
 #endif
-// head records staged per lane in LDS and stored four at a time (one 64-byte
-// piece of the lane's pool block) instead of one 16-byte store per head,
-// which left every head's record a partial line of its own on the fabric
+// head records staged per lane in LDS and stored kHeadBufN at a time (one
+// 64- or 128-byte piece of the lane's pool block) instead of one 16-byte
+// store per head, which left every record a partial line of its own on the
+// fabric (A/B: walk kernel 11.24-11.38 -> 10.73-10.79 ms with 4 records;
+// 8, a whole line: 10.96-11.02 -> 10.74-10.87 ms on another box)
 #ifndef CMSBWT_HEAD_BUF
-#define CMSBWT_HEAD_BUF 1
+#define CMSBWT_HEAD_BUF 8
 #endif
-constexpr bool kHeadBuf = CMSBWT_HEAD_BUF != 0;
+constexpr uint32_t kHeadBufN = CMSBWT_HEAD_BUF;  // records per store (0: none; 4: 64 B; 8: a 128-byte line)
+constexpr bool kHeadBuf = kHeadBufN != 0;
+static_assert(kHeadBufN == 0 || (kHeadBufN <= kPoolB && kPoolB % kHeadBufN == 0), "pieces tile the pool block");
 static_assert(sizeof(HeadRec) == sizeof(uint4), "head records are stored as uint4");
 template <bool STATS, bool FAST>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CMSBWT_W2_WAVES, 8)))
@@ -368,7 +372,7 @@ k_ms_walk2(Walk2Args A) {
   __shared__ uint8_t kmapL[256];
   __shared__ uint32_t lvlL[2 * kMaxLevels];
   __shared__ uint32_t pfxL[17];
-  __shared__ uint4 hbuf[kHeadBuf ? 4 : 1][256];  // 16 KB: four records per lane (slot-major: no bank conflicts)
+  __shared__ uint4 hbuf[kHeadBuf ? kHeadBufN : 1][256];  // 16 B x kHeadBufN per lane (slot-major: no bank conflicts)
   if (STATS && threadIdx.x < 32) sc[threadIdx.x] = 0;
   if (A.R.pfx) kmapL[threadIdx.x] = A.R.kmap[threadIdx.x];  // blockDim == 256
   if (threadIdx.x < 17) pfxL[threadIdx.x] = A.R.pfxOff[threadIdx.x];
@@ -831,11 +835,12 @@ k_ms_walk2(Walk2Args A) {
           seq++;
         }
         if (kHeadBuf) {
-          hbuf[fill & 3][threadIdx.x] = make_uint4(i, pos, len, smaller ? 1u : 0u);
-          if ((fill & 3) == 3 && blk < A.pool.capBlocks) {  // a full 64-byte piece of the block
-            uint4* dst = (uint4*)(A.pool.rec + (uint64_t)blk * kPoolB + (fill - 3));
+          constexpr uint32_t M = kHeadBufN - 1;
+          hbuf[fill & M][threadIdx.x] = make_uint4(i, pos, len, smaller ? 1u : 0u);
+          if ((fill & M) == M && blk < A.pool.capBlocks) {  // a full piece of the block
+            uint4* dst = (uint4*)(A.pool.rec + (uint64_t)blk * kPoolB + (fill - M));
 #pragma unroll
-            for (uint32_t k = 0; k < 4; k++) dst[k] = hbuf[k][threadIdx.x];
+            for (uint32_t k = 0; k < kHeadBufN; k++) dst[k] = hbuf[k][threadIdx.x];
           }
         } else if (blk < A.pool.capBlocks) {
           HeadRec r;
@@ -889,9 +894,10 @@ k_ms_walk2(Walk2Args A) {
         A.chunkCount[cid] = count;
         phase = PH_NEXT;
         use = 0;
-        if (kHeadBuf && fill != kPoolB && (fill & 3) && blk < A.pool.capBlocks) {  // the chunk's last records
-          uint4* dst = (uint4*)(A.pool.rec + (uint64_t)blk * kPoolB + (fill & ~3u));
-          for (uint32_t k = 0; k < (fill & 3); k++) dst[k] = hbuf[k][threadIdx.x];
+        constexpr uint32_t M = kHeadBuf ? kHeadBufN - 1 : 0;
+        if (kHeadBuf && fill != kPoolB && (fill & M) && blk < A.pool.capBlocks) {  // the chunk's last records
+          uint4* dst = (uint4*)(A.pool.rec + (uint64_t)blk * kPoolB + (fill & ~M));
+          for (uint32_t k = 0; k < (fill & M); k++) dst[k] = hbuf[k][threadIdx.x];
         }
       } else {
         phase = PC_CHAR;
