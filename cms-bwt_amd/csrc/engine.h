@@ -2093,6 +2093,14 @@ struct Engine {
     DBuf<uint4> info1;
     DBuf<unsigned long long> info2;
     uint32_t V = 0;
+    bool Vread = false;
+    auto read_V = [&]() {  // writer elements (stream-ordered after writer_inputs' exscan)
+      if (Vread) return;
+      const uint64_t V64 = sum2(eBase.p + (n - 1), wm.p + (n - 1));
+      if (V64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer elements"};
+      V = (uint32_t)V64;
+      Vread = true;
+    };
     auto writer_inputs = [&]() {
       bucket.alloc(n);
       bcnt.alloc(n);
@@ -2101,10 +2109,14 @@ struct Engine {
       wm.alloc(n); eBase.alloc(n);
       mk_el_count(headBase.p, n, E, H, wm.p, st);
       exscan(wm.p, eBase.p, 0u, n);
-      const uint64_t V64 = sum2(eBase.p + (n - 1), wm.p + (n - 1));
-      if (V64 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer elements"};
-      V = (uint32_t)V64;
-      rOf.alloc(V);
+      // the element count V is read when the writer needs it (read_V): a
+      // host read here would hold the host until the side stream had sorted
+      // the crossing lists, with the main stream's doubling not yet enqueued
+      // (~1.2 ms idle).  rOf is sized by the bound E + sum over SA ranks of
+      // max(1, heads) <= E + n + H.
+      const uint64_t Vmax = (uint64_t)E + n + H;
+      if (Vmax >= 0xffffffffull) read_V();
+      rOf.alloc(Vread ? V : Vmax);
       mk_el_rof(eBase.p, wm.p, n, rOf.p, st);
       info1.alloc(n); info2.alloc(n);
       ElemIn ei{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, itemOfSlot.p, headBase.p, eBase.p, rOf.p, nullptr,
@@ -2335,6 +2347,7 @@ struct Engine {
     stats.counter_work = W;
 
     if (check) writer_inputs();
+    read_V();
 
     // ---- writer (FN:1631-1777) as segments + run-length merge
     uint64_t Rn = 0, symbols = 0;
