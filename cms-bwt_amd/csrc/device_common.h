@@ -8,7 +8,7 @@ namespace cmsbwt {
 constexpr int kMaxLevels = 6;   // block-minima levels over LCP (64^6 > 2^32)
 constexpr uint32_t kPoolB = 16; // head records per pool block
 // pool blocks a lane of the uniform-step walk reserves per atomic (it keeps
-// unused ones for its next chunk; blocks never started keep blkChunk = ~0)
+// unused ones for its next chunk; blocks never started keep blkMeta.x = ~0)
 constexpr uint32_t kPoolBatch = 16;
 constexpr uint8_t kSep = 2;     // CMS-BWT.h:28
 // Readable tail after x and after the collection text: the cooperative LCE
@@ -97,8 +97,7 @@ struct HeadRec {
 
 struct Pool {
   HeadRec* rec;
-  uint32_t* blkChunk;
-  uint32_t* blkSeq;
+  uint2* blkMeta;      // (chunk, block sequence in the chunk) per block; chunk ~0: reserved, never started
   uint32_t* used;      // atomic block counter
   uint32_t capBlocks;
 };

@@ -1365,17 +1365,16 @@ struct Engine {
     const uint64_t slack = (uint64_t)lanes * (kPoolBatch - 1);
     uint64_t cap = (uint64_t)nch + slack + (uint64_t)((double)chars * poolDensity * 1.1) / kPoolB + 1024;
     DBuf<HeadRec> rec;
-    DBuf<uint32_t> blkChunk, blkSeq;
+    DBuf<uint2> blkMeta;
     uint32_t usedBlocks = 0;
     while (true) {
       if (cap > 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "head pool exceeds 2^32 blocks"};
       rec.alloc(cap * kPoolB);
-      blkChunk.alloc(cap);
-      blkSeq.alloc(cap);
+      blkMeta.alloc(cap);
       used.zero(st);
       nextChunk.zero(st);
-      HIPCHK(hipMemsetAsync(blkChunk.p, 0xff, cap * 4, st));
-      Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
+      HIPCHK(hipMemsetAsync(blkMeta.p, 0xff, cap * 8, st));
+      Pool pool{rec.p, blkMeta.p, used.p, (uint32_t)cap};
       HIPCHK(hipEventRecord(ev0, st));
       launch_ms_walk2(R, dtext.p, ddoc.p, plan.dch.p, nch, plan.bandOrder.p, plan.bandStart.p, plan.nbands,
                       nextChunk.p, pool, chunkCount.p, lanes, w2stats.p, st);
@@ -1419,7 +1418,7 @@ struct Engine {
     hStart.alloc(H); hPos.alloc(H); hLen.alloc(H); hIsa.alloc(H); hTonext.alloc(H);
     hSmall.alloc(H); hChar.alloc(H); hNext.alloc(H);
     HeadsSoA h = heads();
-    Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
+    Pool pool{rec.p, blkMeta.p, used.p, (uint32_t)cap};
     DBuf<uint32_t> hDoc;  // document of each head (finalize)
     hDoc.alloc(H);
     launch_scatter_heads(pool, usedBlocks, chunkCount.p, chunkBase.p, h, plan.dch.p, dtext.p, ddoc.p, hDoc.p, st);
@@ -2486,12 +2485,11 @@ struct Engine {
     const uint32_t sampleLanes = std::min<uint32_t>(kWalkLanes, ns);
     const uint64_t cap = ns + (uint64_t)sampleLanes * (kPoolBatch - 1) + sampleChars / 2 / kPoolB + 1024;  // up to 50 % heads
     DBuf<HeadRec> rec;
-    DBuf<uint32_t> blkChunk, blkSeq;
+    DBuf<uint2> blkMeta;
     rec.alloc(cap * kPoolB);
-    blkChunk.alloc(cap);
-    blkSeq.alloc(cap);
-    HIPCHK(hipMemsetAsync(blkChunk.p, 0xff, cap * 4, st));
-    Pool pool{rec.p, blkChunk.p, blkSeq.p, used.p, (uint32_t)cap};
+    blkMeta.alloc(cap);
+    HIPCHK(hipMemsetAsync(blkMeta.p, 0xff, cap * 8, st));
+    Pool pool{rec.p, blkMeta.p, used.p, (uint32_t)cap};
     launch_ms_walk2(R, dtext.p, ddoc.p, plan.dch.p, nch, order.p, bstart.p, 1, next.p, pool, cnt.p,
                     sampleLanes, nullptr, st);
     HIPCHK(hipGetLastError());

@@ -26,9 +26,10 @@ __global__ void k_scatter_heads(Pool pool, uint32_t blocksUsed, const uint32_t* 
   uint64_t slot = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
   uint64_t blk = slot / kPoolB;
   if (blk >= blocksUsed) return;
-  uint32_t cid = pool.blkChunk[blk];
+  const uint2 bm = pool.blkMeta[blk];
+  const uint32_t cid = bm.x;
   if (cid == 0xffffffffu) return;  // reserved by a lane, never started
-  uint32_t local = pool.blkSeq[blk] * kPoolB + (uint32_t)(slot % kPoolB);
+  uint32_t local = bm.y * kPoolB + (uint32_t)(slot % kPoolB);
   if (local >= chunkCount[cid]) return;
   uint32_t idx = (uint32_t)chunkBase[cid] + local;
   HeadRec r = pool.rec[slot];

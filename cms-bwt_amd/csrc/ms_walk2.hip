@@ -433,7 +433,7 @@ k_ms_walk2(Walk2Args A) {
   uint32_t chkOn = 0, chkLen = 0, chkC = 0, chkLo = 0, chkLen0 = 0;
   // emission
   // pool blocks are reserved kPoolBatch at a time (blk .. blkEnd) and kept
-  // across this lane's chunks; blocks never started keep blkChunk = ~0
+  // across this lane's chunks; blocks never started keep blkMeta.x = ~0
   uint32_t count = 0, blk = 0xffffffffu, blkEnd = 0, fill = kPoolB, seq = 0;
   uint32_t phase = PH_NEXT, use = 0;
   uintptr_t ad0 = X, ad2 = X;
@@ -831,7 +831,7 @@ k_ms_walk2(Walk2Args A) {
         if (fill == kPoolB) {
           blk++;
           fill = 0;
-          if (blk < A.pool.capBlocks) { A.pool.blkChunk[blk] = cid; A.pool.blkSeq[blk] = seq; }
+          if (blk < A.pool.capBlocks) A.pool.blkMeta[blk] = make_uint2(cid, seq);  // (one 8-byte store)
           seq++;
         }
         if (kHeadBuf) {

@@ -457,3 +457,33 @@ def test_collection_without_documents(engine, tmp_path, case, host_reader):
     engine.load_collection_file(cp2)
     engine.step(rle=True)
     assert engine.stats().heads > 0
+
+
+@pytest.mark.parametrize("case", cases.small_cases(), ids=lambda c: c[0])
+def test_small_cases_without_stage_copies(engine, oracle, tmp_path, case):
+    """The production merge keeps no parity copies (CMSBWT_KEEP_STAGES=0, as
+    bench.py and the CLI run it; the unresolved flags then stay in bit 31 of
+    the sa entries, cleared before a head2rank copy).  The runs and the
+    statistics equal the oracle's."""
+    d, rp, cp, prefix = cases.materialise(tmp_path, case)
+    rc, ost, _ = oracle.run(rp, cp, os.path.join(d, "oracle"), rle=True, prefix=prefix)
+    assert rc == 0
+    want = open(os.path.join(d, "oracle") + ".rl_bwt", "rb").read()
+    old = os.environ.get("CMSBWT_KEEP_STAGES")
+    os.environ["CMSBWT_KEEP_STAGES"] = "0"
+    try:
+        engine.initialize_reference(rp)
+        engine.load_collection_file(cp, prefix)
+        engine.ms_walk()
+        engine.merge(True)
+    finally:
+        if old is None:
+            del os.environ["CMSBWT_KEEP_STAGES"]
+        else:
+            os.environ["CMSBWT_KEEP_STAGES"] = old
+    assert engine.runs_bytes() == want
+    st = engine.stats()
+    assert (st.heads, st.keys, st.rank) == (ost["heads"], ost["keys"], ost["rank"])
+    assert (st.counter_bad, st.counter_good, st.counter_nothing) == (ost["bad"], ost["good"], ost["nothing"])
+    h2r = engine.array("head2rank")  # (int32: a flag left in bit 31 would read negative)
+    assert int(h2r.min()) >= 0
