@@ -125,6 +125,26 @@ struct ElemSegs {
     return s;
   }
 };
+// an element's segments in 16 bytes (k_el_wr_tiles stores them in element
+// order, k_el_wr_emit_tiles reads them back sequentially instead of
+// re-gathering the per-slot inputs): x = n | c0 << 8 | c1 << 16 | c2 << 24,
+// the first and the last segment's counts in 48 bits each (<= the collection
+// length); a middle segment (n == 3: the head character between the counter
+// refchars and the remainder, d_elem_segments) always counts 1
+__device__ __forceinline__ uint4 segs_pack(const ElemSegs& g) {
+  const unsigned long long a = g.n0, b = g.n == 3 ? g.n2 : (g.n == 2 ? g.n1 : 0ull);
+  return make_uint4(g.n | (g.c0 << 8) | (g.c1 << 16) | (g.c2 << 24), (uint32_t)a,
+                    ((uint32_t)(a >> 32) & 0xffffu) | (((uint32_t)b & 0xffffu) << 16), (uint32_t)(b >> 16));
+}
+__device__ __forceinline__ ElemSegs segs_unpack(const uint4 v) {
+  ElemSegs g{v.x & 3u, (v.x >> 8) & 0xffu, (v.x >> 16) & 0xffu, (v.x >> 24) & 0xffu, 0ull, 0ull, 0ull};
+  const unsigned long long a = v.y | ((unsigned long long)(v.z & 0xffffu) << 32);
+  const unsigned long long b = (v.z >> 16) | ((unsigned long long)v.w << 16);
+  g.n0 = a;
+  g.n1 = g.n == 3 ? 1ull : b;
+  g.n2 = b;
+  return g;
+}
 __device__ __forceinline__ ElemSegs d_elem_collect(const ElemArgs& A, uint32_t e) {
   ElemSegs g{0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};
   d_elem_segments(A, e, [&](uint8_t c, unsigned long long cnt) {

@@ -2371,12 +2371,18 @@ struct Engine {
         DBuf<WrState> tsum, tpre;
         DBuf<unsigned long long> tot;
         tsum.alloc(nt); tpre.alloc(nt); tot.alloc(2);
-        mk_el_wr_tiles(ei, V, tsum.p, st);
+        // the elements' segments kept between the passes (16 B each, element
+        // order): the second pass reads them sequentially instead of
+        // gathering the per-slot counters, sums and characters again
+        // (CMSBWT_WR_SEGBUF=0: recomputed)
+        DBuf<uint4> segs;
+        if (env_u32("CMSBWT_WR_SEGBUF", 1)) segs.alloc(V);
+        mk_el_wr_tiles(ei, V, tsum.p, st, segs.p);
         const WrState zero{0ull, 0ull, 0ull, 0u, 0u};
         size_t b = 0;
         HIPCHK(rocprim::exclusive_scan(nullptr, b, tsum.p, tpre.p, zero, (size_t)nt, WrOp{}, st));
         HIPCHK(rocprim::exclusive_scan(scratch(b), b, tsum.p, tpre.p, zero, (size_t)nt, WrOp{}, st));
-        mk_el_wr_emit_tiles(ei, V, tpre.p, runs.p, tot.p, st);
+        mk_el_wr_emit_tiles(ei, V, tpre.p, runs.p, tot.p, st, segs.p);
         recordsWritten = true;
         unsigned long long tt[2];
         HIPCHK(hipMemcpyAsync(tt, tot.p, sizeof(tt), hipMemcpyDeviceToHost, st));

@@ -1794,10 +1794,15 @@ __device__ __forceinline__ WrState wr_block_exscan(WrState x, WrState* total) {
   if (total) *total = op(op(wt[0], wt[1]), op(wt[2], wt[3]));
   return op(pre, ex);
 }
-__global__ void __launch_bounds__(256) k_el_wr_tiles(ElemArgs A, uint32_t V, WrState* __restrict__ tileSum) {
+__global__ void __launch_bounds__(256) k_el_wr_tiles(ElemArgs A, uint32_t V, WrState* __restrict__ tileSum,
+                                                     uint4* __restrict__ segOut) {
   const uint32_t e = blockIdx.x * 256 + threadIdx.x;
   WrState s{0ull, 0ull, 0ull, 0u, 0u};
-  if (e < V) s = d_elem_collect(A, e).state();
+  if (e < V) {
+    const ElemSegs g = d_elem_collect(A, e);
+    if (segOut) segOut[e] = segs_pack(g);  // (element order: coalesced)
+    s = g.state();
+  }
   WrState tot;
   (void)wr_block_exscan(s, &tot);
   if (threadIdx.x == 0) tileSum[blockIdx.x] = tot;
@@ -1813,10 +1818,11 @@ __device__ __forceinline__ void wr_record(uint8_t* o, unsigned long long len, ui
 // last run, by the last element
 __global__ void __launch_bounds__(256) k_el_wr_emit_tiles(ElemArgs A, uint32_t V, const WrState* __restrict__ tilePre,
                                                          uint8_t* __restrict__ rec,
-                                                         unsigned long long* __restrict__ total) {
+                                                         unsigned long long* __restrict__ total,
+                                                         const uint4* __restrict__ segIn) {
   const uint32_t e = blockIdx.x * 256 + threadIdx.x;
   ElemSegs g{0u, 0u, 0u, 0u, 0ull, 0ull, 0ull};
-  if (e < V) g = d_elem_collect(A, e);
+  if (e < V) g = segIn ? segs_unpack(segIn[e]) : d_elem_collect(A, e);
   const WrState ex = WrOp{}(tilePre[blockIdx.x], wr_block_exscan(g.state(), nullptr));
   int prev = (ex.hl >> 16) ? (int)((ex.hl >> 8) & 0xffu) : -1;
   unsigned long long j = ex.runs, pos = ex.sym, start = ex.lastStart;
@@ -1838,14 +1844,15 @@ __global__ void __launch_bounds__(256) k_el_wr_emit_tiles(ElemArgs A, uint32_t V
     total[1] = pos;
   }
 }
-void mk_el_wr_tiles(const ElemIn& w, uint32_t V, WrState* tileSum, hipStream_t st) {
-  if (V) hipLaunchKernelGGL(k_el_wr_tiles, dim3((V + 255) / 256), dim3(256), 0, st, elem_args(w), V, tileSum);
+void mk_el_wr_tiles(const ElemIn& w, uint32_t V, WrState* tileSum, hipStream_t st, uint4* segOut) {
+  if (V)
+    hipLaunchKernelGGL(k_el_wr_tiles, dim3((V + 255) / 256), dim3(256), 0, st, elem_args(w), V, tileSum, segOut);
 }
 void mk_el_wr_emit_tiles(const ElemIn& w, uint32_t V, const WrState* tilePre, uint8_t* rec,
-                         unsigned long long* total, hipStream_t st) {
+                         unsigned long long* total, hipStream_t st, const uint4* segIn) {
   if (V)
     hipLaunchKernelGGL(k_el_wr_emit_tiles, dim3((V + 255) / 256), dim3(256), 0, st, elem_args(w), V, tilePre, rec,
-                       total);
+                       total, segIn);
 }
 
 __global__ void k_el_wr_count(ElemArgs A, uint32_t V, uint32_t* __restrict__ runs, unsigned long long* __restrict__ sym,

@@ -228,10 +228,12 @@ void mk_el_wr_emit(const ElemIn& w, uint32_t V, const unsigned long long* runOff
 // the writer's run scan in tiles (elem_writer.h WrState / WrOp): per-tile
 // summaries, then emission at each element's prefix; total = {runs, symbols}
 struct WrState;
-void mk_el_wr_tiles(const ElemIn& w, uint32_t V, WrState* tileSum, hipStream_t st);
+// segOut / segIn (optional, V x 16 B): the elements' segments stored by the
+// first pass and read back by the second (elem_writer.h segs_pack)
+void mk_el_wr_tiles(const ElemIn& w, uint32_t V, WrState* tileSum, hipStream_t st, uint4* segOut = nullptr);
 // (rec: the 9-byte run records, FN:1708-1709, written directly)
 void mk_el_wr_emit_tiles(const ElemIn& w, uint32_t V, const WrState* tilePre, uint8_t* rec,
-                         unsigned long long* total, hipStream_t st);
+                         unsigned long long* total, hipStream_t st, const uint4* segIn = nullptr);
 // element writer of the position-sharded merge (elements of the owned SA
 // ranks, units summarised for the all-reduce, emission per element)
 void mk_dm_el_count(const int32_t* sa, const uint32_t* posBegin, const uint32_t* slot, uint32_t n, uint32_t E,

@@ -82,6 +82,18 @@ def test_small_cases_plain_bwt(engine, oracle, tmp_path, case):
     _compare(engine, oracle, tmp_path, case, rle=False)
 
 
+@pytest.mark.parametrize("env", [{"CMSBWT_WR_SEGBUF": "0"}, {"CMSBWT_WR_UNFUSED": "1"}],
+                         ids=["segments_recomputed", "unfused_writer"])
+@pytest.mark.parametrize("rle", [True, False], ids=["rl_bwt", "bwt"])
+@pytest.mark.parametrize("case", cases.small_cases()[:5], ids=lambda c: c[0])
+def test_writer_variants(engine, oracle, tmp_path, case, rle, env):
+    """The tile writer (default) keeps each element's segments between its
+    two passes (16-byte packed form, elem_writer.h segs_pack); recomputing
+    them in the second pass, and the element-scan writer of rounds 2-4,
+    give the same bytes."""
+    _compare(engine, oracle, tmp_path, case, rle=rle, env=env)
+
+
 @pytest.mark.parametrize("rle", [True, False], ids=["rl_bwt", "bwt"])
 @pytest.mark.parametrize("case", cases.small_cases()[:5], ids=lambda c: c[0])
 def test_writer_two_scans(engine, oracle, tmp_path, case, rle):
