@@ -450,8 +450,7 @@ void Engine::dm_units(int64_t* out) {
   const uint32_t Hp = dm.Hp;
   dm.cum.alloc(std::max<uint32_t>(Hp, 1));
   if (Hp)
-    inscan(rocprim::make_transform_iterator(dm.counter.p, PlusOneU64()), dm.cum.p, Hp,
-           rocprim::plus<unsigned long long>());
+    inscan_plus1_u64(dm.counter.p, dm.cum.p, Hp);
   dm.info1.alloc(n);
   dm.info2.alloc(n);
   const ElemIn ei = dm_elem_in();

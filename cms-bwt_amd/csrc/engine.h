@@ -21,6 +21,26 @@
 #include <cstring>
 
 #include <hip/hip_runtime.h>
+#include <rocprim/iterator/counting_iterator.hpp>
+#include <rocprim/iterator/transform_iterator.hpp>
+
+// rocPRIM's radix sort assumes any non-pointer input may alias its output and,
+// with an odd number of digit passes, first copies keys and values into its
+// temporary buffers (a 16-B HeadKV per head for the position sort: ~0.5 ms
+// at 1e8 heads).  The grouping's value input is computed from the head SoA
+// (MakeHeadKV over a counting iterator) and never aliases a sort buffer, so
+// tell it so; the first pass then reads the input directly.  Declared before
+// the rocPRIM device headers: their qualified call is looked up there.
+namespace cmsbwt { struct MakeHeadKV; }
+BEGIN_ROCPRIM_NAMESPACE
+namespace detail {
+template <class V, class D, class O>
+inline bool can_iterators_alias(transform_iterator<counting_iterator<unsigned int, D>, cmsbwt::MakeHeadKV, V>, O*,
+                                const size_t) {
+  return false;
+}
+}  // namespace detail
+END_ROCPRIM_NAMESPACE
 #include <rocprim/rocprim.hpp>
 
 #include <fcntl.h>
@@ -432,6 +452,25 @@ struct Engine {
     mk_scan_tiles(in, out, n, off.p, init, inclusive, st);
   }
   static bool rocprim_scan() { return env_u32("CMSBWT_ROCPRIM_SCAN", 0) != 0; }
+  // inclusive u64 scan of (in[i] + 1): the writer's cumulative counters
+  void inscan_plus1_u64(const unsigned long long* in, unsigned long long* out, uint64_t n) {
+    if (!n) return;
+    if (rocprim_scan()) {
+      inscan(rocprim::make_transform_iterator(in, PlusOneU64()), out, n, rocprim::plus<unsigned long long>());
+      return;
+    }
+    const uint64_t nt = scan_tiles(n);
+    DBuf<unsigned long long> sums, off;
+    sums.alloc(nt);
+    off.alloc(nt);
+    mk_scan64_sums(in, n, 1u, sums.p, st);
+    size_t b = 0;
+    HIPCHK(rocprim::exclusive_scan(nullptr, b, sums.p, off.p, 0ull, (size_t)nt, rocprim::plus<unsigned long long>(),
+                                   st));
+    HIPCHK(rocprim::exclusive_scan(scratch(b), b, sums.p, off.p, 0ull, (size_t)nt,
+                                   rocprim::plus<unsigned long long>(), st));
+    mk_scan64_tiles(in, out, n, off.p, 1u, true, st);
+  }
   template <class In, class Out, class Init>
   void exscan(In in, Out out, Init init, uint64_t n) {
     if (!n) return;
@@ -2356,7 +2395,7 @@ struct Engine {
     {
       DBuf<unsigned long long> cum;
       cum.alloc(H);
-      inscan(rocprim::make_transform_iterator(counter.p, PlusOneU64()), cum.p, H, rocprim::plus<unsigned long long>());
+      inscan_plus1_u64(counter.p, cum.p, H);
       ElemIn ei{dsa.p, dbwt.p, bucket.p, posBegin.p, sSlot.p, itemOfSlot.p, headBase.p, eBase.p, rOf.p, bwtHeads.p,
                 counter.p, cum.p, info1.p, info2.p, n, E, H, rle};
       ei.bwtSlot = bwtSlot.p;

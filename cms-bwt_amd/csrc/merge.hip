@@ -2176,8 +2176,87 @@ __global__ void __launch_bounds__(256) k_scan_tiles(const uint32_t* in, uint32_t
       if (e + k < n) out[e + k] = r[k];
   }
 }
+// the same two passes over u64 values plus a constant: the writer's
+// cumulative counters (FN:1504-1515's prefix sums over counter + 1)
+__device__ __forceinline__ void scan_load8_u64(const unsigned long long* __restrict__ in, uint64_t e, uint64_t n,
+                                               bool vec, uint32_t add, unsigned long long v[kScanIpt]) {
+  if (vec && e + kScanIpt <= n) {
+    const ulonglong2* i2 = reinterpret_cast<const ulonglong2*>(in + e);
+#pragma unroll
+    for (uint32_t k = 0; k < kScanIpt / 2; k++) {
+      const ulonglong2 a = i2[k];
+      v[2 * k] = a.x + add;
+      v[2 * k + 1] = a.y + add;
+    }
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kScanIpt; k++) v[k] = e + k < n ? in[e + k] + add : 0ull;
+  }
+}
+__global__ void __launch_bounds__(256) k_scan64_sums(const unsigned long long* __restrict__ in, uint64_t n, int vec,
+                                                     uint32_t add, unsigned long long* __restrict__ sums) {
+  __shared__ unsigned long long wsum[4];
+  const uint64_t e = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanIpt;
+  unsigned long long v[kScanIpt];
+  scan_load8_u64(in, e, n, vec != 0, add, v);
+  unsigned long long c = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanIpt; k++) c += v[k];
+  for (uint32_t d = 32; d >= 1; d >>= 1) c += __shfl_xor(c, (int)d);
+  if ((threadIdx.x & 63) == 0) wsum[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) sums[blockIdx.x] = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+}
+__global__ void __launch_bounds__(256) k_scan64_tiles(const unsigned long long* in, unsigned long long* out,
+                                                      uint64_t n, int vec,
+                                                      const unsigned long long* __restrict__ tileOff, uint32_t add,
+                                                      int inclusive) {
+  __shared__ unsigned long long wsum[4];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const uint64_t e = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanIpt;
+  unsigned long long v[kScanIpt];
+  scan_load8_u64(in, e, n, vec != 0, add, v);
+  unsigned long long tot = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < kScanIpt; k++) tot += v[k];
+  unsigned long long inc = tot;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const unsigned long long o = __shfl_up(inc, d);
+    if (lane >= d) inc += o;
+  }
+  if (lane == 63) wsum[wv] = inc;
+  __syncthreads();
+  unsigned long long base = tileOff[blockIdx.x] + (inc - tot);
+  for (uint32_t w = 0; w < wv; w++) base += wsum[w];
+  unsigned long long r[kScanIpt];
+#pragma unroll
+  for (uint32_t k = 0; k < kScanIpt; k++) {
+    if (inclusive) { base += v[k]; r[k] = base; }
+    else { r[k] = base; base += v[k]; }
+  }
+  if (vec != 0 && e + kScanIpt <= n) {
+    ulonglong2* o2 = reinterpret_cast<ulonglong2*>(out + e);
+#pragma unroll
+    for (uint32_t k = 0; k < kScanIpt / 2; k++) o2[k] = make_ulonglong2(r[2 * k], r[2 * k + 1]);
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < kScanIpt; k++)
+      if (e + k < n) out[e + k] = r[k];
+  }
+}
 static inline dim3 g1(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 uint64_t scan_tiles(uint64_t n) { return (n + kScanTile - 1) / kScanTile; }
+void mk_scan64_sums(const unsigned long long* in, uint64_t n, uint32_t add, unsigned long long* sums, hipStream_t st) {
+  const int vec = (((uintptr_t)in) & 15) == 0;
+  if (n) hipLaunchKernelGGL(k_scan64_sums, dim3((unsigned)scan_tiles(n)), dim3(256), 0, st, in, n, vec, add, sums);
+}
+void mk_scan64_tiles(const unsigned long long* in, unsigned long long* out, uint64_t n, const unsigned long long* tileOff,
+                     uint32_t add, bool inclusive, hipStream_t st) {
+  const int vec = ((((uintptr_t)in) | ((uintptr_t)out)) & 15) == 0;
+  if (n)
+    hipLaunchKernelGGL(k_scan64_tiles, dim3((unsigned)scan_tiles(n)), dim3(256), 0, st, in, out, n, vec, tileOff,
+                       add, inclusive ? 1 : 0);
+}
 void mk_scan_sums(const uint32_t* in, uint64_t n, uint32_t* sums, hipStream_t st) {
   const int vec = (((uintptr_t)in) & 15) == 0;
   if (n) hipLaunchKernelGGL(k_scan_sums, dim3((unsigned)scan_tiles(n)), dim3(256), 0, st, in, n, vec, sums);

@@ -115,6 +115,10 @@ uint64_t scan_tiles(uint64_t n);
 void mk_scan_sums(const uint32_t* in, uint64_t n, uint32_t* sums, hipStream_t st);
 void mk_scan_tiles(const uint32_t* in, uint32_t* out, uint64_t n, const uint32_t* tileOff, uint32_t init,
                    bool inclusive, hipStream_t st);
+// the same over u64 values plus a constant
+void mk_scan64_sums(const unsigned long long* in, uint64_t n, uint32_t add, unsigned long long* sums, hipStream_t st);
+void mk_scan64_tiles(const unsigned long long* in, unsigned long long* out, uint64_t n, const unsigned long long* tileOff,
+                     uint32_t add, bool inclusive, hipStream_t st);
 // order-preserving compaction of flagged u32 values (tiles of 2048); `out`
 // must not alias `in` (k_sel_write reads in[] after other blocks may have
 // written their compacted values)
