@@ -1650,7 +1650,8 @@ struct Engine {
         mk_pos_begin(posS.p, H, n, hb.p, st);
         // run buckets from the sorted heads: starts per position from hb,
         // ends counted in k_grp_seg (LDS histogram near the block's positions)
-        const bool runsHere = !runsValid;
+        // (CMSBWT_GRP_RUNS=0: the position-bin path of ensure_runs instead)
+        const bool runsHere = !runsValid && env_u32("CMSBWT_GRP_RUNS", 1) != 0;
         if (runsHere) {
           diff.alloc((uint64_t)n + 1);
           hasHead.alloc(n);
