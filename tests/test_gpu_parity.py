@@ -203,15 +203,16 @@ def test_counter_stream_paths(engine, oracle, tmp_path, case, env):
     _compare(engine, oracle, tmp_path, case, env=env)
 
 
-@pytest.mark.parametrize("geom", [{"CMSBWT_RUN_BIN_SHIFT": "3"},
-                                  {"CMSBWT_RUN_BIN_SHIFT": "5", "CMSBWT_RUN_BIN_GLOBAL": "1"},
-                                  {"CMSBWT_RUN_BIN_GLOBAL": "1"}],
+@pytest.mark.parametrize("geom", [{"CMSBWT_RUN_BIN_SHIFT": "3", "CMSBWT_GRP_RUNS": "0"},
+                                  {"CMSBWT_RUN_BIN_SHIFT": "5", "CMSBWT_RUN_BIN_GLOBAL": "1", "CMSBWT_GRP_RUNS": "0"},
+                                  {"CMSBWT_RUN_BIN_GLOBAL": "1", "CMSBWT_GRP_RUNS": "0"}],
                          ids=["bins8_lds", "bins32_global", "bins8192_global"])
 @pytest.mark.parametrize("case", cases.small_cases(), ids=lambda c: c[0])
 def test_run_bucket_bins(engine, oracle, tmp_path, case, geom):
     """Run buckets (FN:1162-1171, 1203) through position bins: many small bins
     (runs crossing bin edges, endpoints at n) and the global-counter path used
-    above kRunBinLdsMax bins give the oracle's bucket array and output."""
+    above kRunBinLdsMax bins give the oracle's bucket array and output
+    (CMSBWT_GRP_RUNS=0: the grouping leaves the run ends to this path)."""
     _compare(engine, oracle, tmp_path, case, env=geom)
 
 
