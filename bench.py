@@ -254,12 +254,29 @@ def main():
     if in_process:
         world = args.gpus
     import torch
+    # n_gpus is the number of distinct devices the ranks ran on: ranks that
+    # would share a device (more in-process ranks than devices, or torchrun
+    # ranks rehearsed on one GPU) are refused unless the rehearsal is asked
+    # for explicitly, and then reported as ranks beside n_gpus (main.cpp:85-132
+    # has no such mode)
+    rehearsal = os.environ.get("CMSBWT_BENCH_REHEARSAL", "0") == "1"
+    ndev = torch.cuda.device_count()  # (does not initialise the GPU on this image)
+    if in_process and world > ndev and not rehearsal:
+        print(json.dumps({"error": f"--gpus {world} in one process but {ndev} device(s): ranks would share a "
+                                   "device; set CMSBWT_BENCH_REHEARSAL=1 to run them as a rehearsal "
+                                   "(reported as n_gpus = distinct devices, ranks = N)"}), flush=True)
+        sys.exit(2)
     dist = None
     # Rehearsal of the N>1 path on a one-GPU box (never set by the driver):
     # CMSBWT_BENCH_SAME_GPU=1 puts every rank on device 0 and uses gloo (host
     # staging) instead of RCCL, which allows one rank per device.
     same_gpu = os.environ.get("CMSBWT_BENCH_SAME_GPU", "0") == "1"
     if same_gpu:
+        if world > 1 and not rehearsal:
+            print(json.dumps({"error": "CMSBWT_BENCH_SAME_GPU=1 puts every rank on device 0; set "
+                                       "CMSBWT_BENCH_REHEARSAL=1 as well (reported as n_gpus = 1, ranks = N)"}),
+                  flush=True)
+            sys.exit(2)
         local = 0
     if world > 1 and not in_process:
         import torch.distributed as dist
@@ -376,10 +393,12 @@ def main():
     traffic, traffic_src = pmc_traffic(args) if world == 1 else (None, None)
     ctraffic, _ = pmc_traffic(args, "k_counter_tgt") if world == 1 else (None, None)
     c_ms = st.counter_kernel_ms
+    # distinct devices the ranks ran on (the rehearsals share device 0)
+    n_devices = 1 if same_gpu else min(world, ndev) if in_process else world
     out = {
         "metric": ("collection MB/s to .bwt" if args.plain else
                    "collection MB/s to .rl_bwt (10 MB ref + 1000 copies @0.1% SNP)"),
-        "value": round(value, 3), "unit": "MB/s", "n_gpus": world, "steps": args.steps,
+        "value": round(value, 3), "unit": "MB/s", "n_gpus": n_devices, "ranks": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(ms_step, 3), "higher_is_better": True,
         "scaling": "strong", "vs_baseline": None, "dtype": "u8",
         "data": "synthetic (counter-based generator in HBM, SURVEY.md §8d)",
@@ -435,8 +454,12 @@ def main():
             out["parity"] = parity_check(eng, args, rle)
         except Exception as e:  # reported, never fatal for the GPU number
             out["parity"] = {"error": str(e)[-400:]}
+    if world > n_devices:
+        out["rehearsal"] = f"{world} ranks on {n_devices} device(s): not a {world}-GPU measurement"
     if grp is not None:
         out["per_rank_devices"] = [int(r.device) for r in group_rows[-1]] if group_rows else None
+        if group_rows:
+            out["n_gpus"] = len(set(out["per_rank_devices"]))
         grp.close()
     else:
         eng.close()

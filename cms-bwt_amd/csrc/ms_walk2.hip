@@ -347,6 +347,12 @@ constexpr bool kMemoCheck = CMSBWT_MEMO_CHECK != 0;
 #define CMSBWT_MEMO_BARRIER 0
 #endif
 constexpr bool kMemoBarrier = CMSBWT_MEMO_BARRIER != 0;
+// (tools/memo_isa.sh) CMSBWT_MEMO_GENERIC_BARRIER=0 drops the barrier from the
+// generic instance too: the build that reproduces the code-generation fault
+#ifndef CMSBWT_MEMO_GENERIC_BARRIER
+#define CMSBWT_MEMO_GENERIC_BARRIER 1
+#endif
+constexpr bool kMemoGenBarrier = CMSBWT_MEMO_GENERIC_BARRIER != 0;
 __device__ uint32_t g_memo_bad = 0;
 // waves per SIMD of the walk (Makefile W2WAVES; measured 3 -> 16.50 ms,
 // 4 -> 16.44-16.68, 5 -> 16.9, 6 -> 31.3 with register spills)
@@ -645,7 +651,7 @@ k_ms_walk2(Walk2Args A) {
       // register barrier: the head recorded after a hit carries pos = i + K
       // + 1 (tools/memo_repro.py); pos made opaque (or i;
       // not len) or -O1 keep every case bit-exact
-      if (!FAST || kMemoBarrier) asm volatile("" : "+v"(pos));
+      if ((!FAST && kMemoGenBarrier) || kMemoBarrier) asm volatile("" : "+v"(pos));
       if (amC & 0x10000u) {  // the mismatch at amFront (FN:55)
         smaller = (int8_t)(uint8_t)amC > (int8_t)(uint8_t)(amC >> 8);
         phase = PC_POST;

@@ -38,6 +38,7 @@
 #include <fstream>
 #include <functional>
 #include <mutex>
+#include <shared_mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -106,6 +107,13 @@ void launch_red(Red op, void* a, const void* b, uint64_t n, hipStream_t st) {
 
 struct Aborted {};  // another rank failed: leave quietly
 
+// test hook: CMSBWT_MULTI_FAIL_RANK=k makes rank k fail after its walk, while
+// the other ranks enter the merge's exchanges (tests/test_gpu_cli_multi.py)
+void inject_failure(int rank) {
+  const char* e = getenv("CMSBWT_MULTI_FAIL_RANK");
+  if (e && *e && atoi(e) == rank) throw CtxError{CMSBWT_EINTERNAL, "injected failure (CMSBWT_MULTI_FAIL_RANK)"};
+}
+
 // Rank threads of one run: barrier, failure flag, host exchange table.
 class Group {
  public:
@@ -137,12 +145,31 @@ class Group {
       std::lock_guard<std::mutex> lk(mu);
       if (!failed && onFail) ab = onFail;
       failed = true;
+      failedFlag = true;
       cv.notify_all();
     }
-    // ranks blocked inside an RCCL call (or a stream synchronisation behind
-    // one) wait on a peer that never posts its side: abort the communicators
-    // so those calls return an error and the ranks reach their latch
-    if (ab) ab();
+    // ranks blocked in a stream synchronisation behind an RCCL kernel wait on
+    // a peer that never posts its side: abort the communicators so those
+    // waits return an error and the ranks reach their latch.  The abort frees
+    // the communicators, so it waits until no rank is inside an enqueue
+    // (rccl() below: a rank checks the flag and enqueues under the shared
+    // gate); a rank blocked inside an enqueue itself (a connection to the dead
+    // peer) would hold the gate forever, and that call is what the abort
+    // exists to end, so after kGateWait the abort proceeds regardless.
+    if (ab) {
+      std::unique_lock<std::shared_timed_mutex> lk(gate, std::defer_lock);
+      (void)lk.try_lock_for(kGateWait);
+      ab();
+    }
+  }
+  bool has_failed() const { return failedFlag; }
+  // RCCL enqueue section of one rank: refused once the group has failed, and
+  // never concurrent with the abort of the communicators
+  template <class F>
+  void rccl(F&& f) {
+    std::shared_lock<std::shared_timed_mutex> lk(gate);
+    if (failedFlag) throw Aborted{};
+    f();
   }
   std::function<void()> onFail;  // set before the rank threads start
   // every rank, failed or not, passes here once before its context goes away
@@ -153,11 +180,14 @@ class Group {
   }
 
  private:
+  static constexpr std::chrono::seconds kGateWait{2};
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0, done = 0;
   uint64_t gen = 0;
   bool failed = false;
+  std::atomic<bool> failedFlag{false};
+  std::shared_timed_mutex gate;
 };
 
 // librccl entry points, resolved at run time (the PEER transport needs none)
@@ -220,15 +250,24 @@ class Xfer {
   void a2a(const void* send, uint64_t elem, const std::vector<uint64_t>& sc, const std::vector<uint64_t>& rc,
            void* recv) {
     if (nccl) {
-      nccl->check(nccl->groupStart(), "group start");
-      uint64_t so = 0, ro = 0;
-      for (int s = 0; s < W; s++) {
-        if (sc[s]) nccl->check(nccl->send((const char*)send + so, sc[s] * elem, ncclUint8, s, comm, st), "send");
-        if (rc[s]) nccl->check(nccl->recv((char*)recv + ro, rc[s] * elem, ncclUint8, s, comm, st), "recv");
-        so += sc[s] * elem;
-        ro += rc[s] * elem;
-      }
-      nccl->check(nccl->groupEnd(), "group end");
+      g.rccl([&] {
+        nccl->check(nccl->groupStart(), "group start");
+        uint64_t so = 0, ro = 0;
+        bool open = true;
+        try {
+          for (int s = 0; s < W; s++) {
+            if (sc[s]) nccl->check(nccl->send((const char*)send + so, sc[s] * elem, ncclUint8, s, comm, st), "send");
+            if (rc[s]) nccl->check(nccl->recv((char*)recv + ro, rc[s] * elem, ncclUint8, s, comm, st), "recv");
+            so += sc[s] * elem;
+            ro += rc[s] * elem;
+          }
+          open = false;
+          nccl->check(nccl->groupEnd(), "group end");
+        } catch (...) {
+          if (open) (void)nccl->groupEnd();  // (a group left open would swallow the next calls)
+          throw;
+        }
+      });
       sync();
       return;
     }
@@ -252,7 +291,9 @@ class Xfer {
   void allreduce(void* buf, uint64_t n, Red op) {
     if (nccl) {
       const ncclDataType_t t = op == Red::SumU32 ? ncclUint32 : op == Red::SumI64 ? ncclInt64 : ncclUint8;
-      nccl->check(nccl->allReduce(buf, buf, n, t, op == Red::MaxU8 ? ncclMax : ncclSum, comm, st), "all-reduce");
+      g.rccl([&] {
+        nccl->check(nccl->allReduce(buf, buf, n, t, op == Red::MaxU8 ? ncclMax : ncclSum, comm, st), "all-reduce");
+      });
       sync();
       return;
     }
@@ -283,7 +324,13 @@ class Xfer {
     g.barrier();
   }
 
-  void sync() { MCHK(hipStreamSynchronize(st)); }
+  // a wait that fails because the group failed (aborted communicators) is
+  // that failure's consequence, not a second error
+  void sync() {
+    const hipError_t e = hipStreamSynchronize(st);
+    if (e != hipSuccess && g.has_failed()) throw Aborted{};
+    MCHK(e);
+  }
 
   Group& g;
   const int rank, W;
@@ -767,6 +814,7 @@ int run_multi(const cmsbwt_args* a, const char* ref_path, const char* coll_path,
           const CtxView vw = ctx_view(ctx);
           r.heads = vw.H;
           r.walkKernelMs = vw.stats.ms_walk_kernel_ms;
+          inject_failure(k);
           auto tm = Clock::now();
           if (small || hostRead || forceGather) {
             gather_merge(xf, ctx, a->rle ? 1 : 0, r);
@@ -989,6 +1037,7 @@ extern "C" int cmsbwt_group_step(cmsbwt_group* G, int rle, cmsbwt_rank_times* pe
           r.heads = vw.H;
           r.chars = vw.chars;
           r.walkKernelMs = vw.stats.ms_walk_kernel_ms;
+          inject_failure(k);
           auto tm = Clock::now();
           if (W == 1) {
             chk(cmsbwt_merge(ctx, rle), ctx);

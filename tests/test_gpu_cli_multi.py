@@ -169,3 +169,22 @@ def test_cli_multi_labels_past_2_31(built, tmp_path):
     assert r1.returncode == 0 and r2.returncode == 0, r2.stdout + r2.stderr
     assert sha(pre + "_2.rl_bwt") == g["rl_bwt_sha256"]
     assert _values(pre + "_2.log", KEYS_LARGE) == _values(pre + "_1.log", KEYS_LARGE)
+
+
+@pytest.mark.parametrize("backend", ["peer", "rccl"])
+def test_cli_multi_injected_rank_failure(built, tmp_path, backend):
+    """One rank fails after its walk (test hook CMSBWT_MULTI_FAIL_RANK) while
+    the others enter the sharded merge's exchanges: the process ends with that
+    rank's error code and log line, no crash and no hang.  With RCCL the
+    failure aborts the communicators; the enqueue gate keeps every rank out of
+    RCCL calls on them from then on.  RCCL needs one GPU per rank."""
+    import torch
+    if backend == "rccl" and torch.cuda.device_count() < 2:
+        pytest.skip("RCCL needs two distinct GPUs")
+    pre = str(tmp_path / "c1")
+    _gen_np().gen(1_000_000, 10, 0.001, 11, pre)
+    for fail_rank in ("1", "0"):
+        r = run_cli(["-r", "-n", "2", "-t", backend, "-o", pre + "_f" + fail_rank, pre + ".list"],
+                    env={"CMSBWT_MULTI_FAIL_RANK": fail_rank})
+        assert r.returncode == 2 + 7, (r.returncode, r.stdout[-500:], r.stderr[-500:])  # CMSBWT_EINTERNAL
+        assert f"rank {fail_rank}: injected failure" in open(pre + "_f" + fail_rank + ".log").read()

@@ -188,3 +188,24 @@ def test_bench_refuses_rank_mismatch():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2
     assert "refusing" in json.loads(r.stdout.strip().splitlines()[-1])["error"]
+
+
+def test_bench_refuses_shared_devices_cpu():
+    """In-process --gpus N with fewer devices than ranks (none here), or
+    torchrun ranks all put on device 0, exit 2 without the explicit rehearsal
+    variable, before touching a GPU."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items()
+           if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "CMSBWT_BENCH_REHEARSAL", "CMSBWT_BENCH_SAME_GPU")}
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2, r.stderr[-1000:]
+    assert "share a device" in json.loads(r.stdout.strip().splitlines()[-1])["error"]
+    env2 = dict(env, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0", CMSBWT_BENCH_SAME_GPU="1")
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2"], cwd=root, env=env2,
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode == 2, r.stderr[-1000:]
+    assert "REHEARSAL" in json.loads(r.stdout.strip().splitlines()[-1])["error"]

@@ -9,7 +9,7 @@ cd /tmp && export TMPDIR=/tmp && cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 lib() { case $1 in new) echo cms-bwt_amd/build/libcmsbwt.so;; *) echo exp/$1/libcmsbwt.so;; esac; }
 for v in "$@"; do
-  CMSBWT_LIB=$(lib $v) timeout -k 10 300 python -u tools/memo_repro.py > gpurun_out/memo_$v.log 2>&1
+  CMSBWT_LIB=$(lib $v) timeout -k 10 ${MEMO_TIMEOUT:-300} python -u tools/memo_repro.py $MEMO_CASES > gpurun_out/memo_$v.log 2>&1
   rc=$?
   echo "$v rc=$rc"; grep -E "DIFF|\[memo\]|ALL OK|SOME|Error|error" gpurun_out/memo_$v.log | head -30
   [ $rc -le 1 ] || exit 1
