@@ -27,10 +27,14 @@ $(OUT)/%.o: $(SRC)/%.hip $(HDRS) | $(OUT)
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 # the uniform-step walk keeps its addresses in registers only without
-# SimplifyCFG store sinking (which otherwise moves them to scratch)
+# SimplifyCFG store sinking (which otherwise moves them to scratch), and is
+# built without the backend's SIOptimizeVGPRLiveRange pass, which miscompiles
+# it (DESIGN.md §3.1 "Round 6": the pass marks the walk's `pos` undefined on a
+# path that still reads it; found by tools/memo_isa.sh + opt-bisect)
 W2WAVES ?= 4
+W2FLAGS := -mllvm -simplifycfg-sink-common=false -mllvm -amdgpu-opt-vgpr-liverange=false
 $(OUT)/ms_walk2.o: $(SRC)/ms_walk2.hip $(HDRS) | $(OUT)
-	$(HIPCC) $(HIPFLAGS) -mllvm -simplifycfg-sink-common=false -DCMSBWT_W2_WAVES=$(W2WAVES) -c -o $@ $<
+	$(HIPCC) $(HIPFLAGS) $(W2FLAGS) -DCMSBWT_W2_WAVES=$(W2WAVES) -c -o $@ $<
 
 $(OUT)/host_%.o: $(SRC)/host_%.cpp $(HDRS) | $(OUT)
 	g++ $(HOSTFLAGS) -c -o $@ $<

@@ -340,11 +340,14 @@ constexpr bool kMemoCheck = CMSBWT_MEMO_CHECK != 0;
 #ifndef CMSBWT_PFX_PREFETCH
 #define CMSBWT_PFX_PREFETCH 0
 #endif
-// the register barrier after a memo hit in the specialised instance too
-// (the generic instance always has it; A/B: +0.15 ms of walk kernel with
-// (pos, i, len) opaque)
+// the register barrier after a memo hit in the specialised instance too (the
+// generic instance has it unless CMSBWT_MEMO_GENERIC_BARRIER=0).  Round 6:
+// the fault it guarded against is the backend pass SIOptimizeVGPRLiveRange,
+// now disabled for this file (Makefile W2FLAGS); the barrier
+// stays in both instances as a second guard (A/B on one box: walk kernel
+// 10.83-10.87 ms without, 10.80-10.87 ms with it)
 #ifndef CMSBWT_MEMO_BARRIER
-#define CMSBWT_MEMO_BARRIER 0
+#define CMSBWT_MEMO_BARRIER 1
 #endif
 constexpr bool kMemoBarrier = CMSBWT_MEMO_BARRIER != 0;
 // (tools/memo_isa.sh) CMSBWT_MEMO_GENERIC_BARRIER=0 drops the barrier from the
@@ -647,10 +650,12 @@ k_ms_walk2(Walk2Args A) {
         chkLen0 = len;
       } else {
       len = amFront - i;
-      // the generic instance is miscompiled here at -O2/-O3 without this
-      // register barrier: the head recorded after a hit carries pos = i + K
-      // + 1 (tools/memo_repro.py); pos made opaque (or i;
-      // not len) or -O1 keep every case bit-exact
+      // with the backend's SIOptimizeVGPRLiveRange pass on, the generic
+      // instance was miscompiled here without this register barrier: the
+      // head recorded after a hit carried pos = i + K + 1 (the pass gave
+      // `pos` an undefined value on the path of the lanes that took the
+      // branch before; DESIGN.md §3.1, tools/memo_isa.sh).  The pass is off
+      // for this file; the barrier stays as a second guard
       if ((!FAST && kMemoGenBarrier) || kMemoBarrier) asm volatile("" : "+v"(pos));
       if (amC & 0x10000u) {  // the mismatch at amFront (FN:55)
         smaller = (int8_t)(uint8_t)amC > (int8_t)(uint8_t)(amC >> 8);

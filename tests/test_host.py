@@ -209,3 +209,13 @@ def test_bench_refuses_shared_devices_cpu():
                        capture_output=True, text=True, timeout=120)
     assert r.returncode == 2, r.stderr[-1000:]
     assert "REHEARSAL" in json.loads(r.stdout.strip().splitlines()[-1])["error"]
+
+
+def test_walk_built_without_vgpr_liverange_pass():
+    """ms_walk2.o must be built with SIOptimizeVGPRLiveRange off: that backend
+    pass miscompiles the walk (DESIGN.md §3.1 round 6,
+    profiles/r06_memo_miscompile.txt)."""
+    mk = open(os.path.join(ROOT, "Makefile")).read()
+    assert "-amdgpu-opt-vgpr-liverange=false" in mk
+    rule = mk[mk.index("$(OUT)/ms_walk2.o:"):]
+    assert "$(W2FLAGS)" in rule.splitlines()[1]
