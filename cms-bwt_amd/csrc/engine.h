@@ -270,7 +270,7 @@ struct Engine {
   DBuf<int32_t> dsa, dlcp, dplcp;
   DBuf<uint8_t> dplcp8;  // min(PLCP, 255), the walk's first skip window
   DBuf<uint32_t> disa;
-  DBuf<uint32_t> dpfx;
+  DBuf<uint32_t> dpfx, dpfk;
   DBuf<uint32_t> dld;
   DBuf<uint4> dpr, dir;
   DBuf<uint8_t> dkmap;
@@ -835,7 +835,19 @@ struct Engine {
   // and its successor code, so the interval end is Start + Count, not the
   // next Start).  Only ASCII references: there the walk's signed (FN:55) and
   // unsigned orders agree.
+  // the paired level-K table (DevRef::pfk) of a DNA reference, from pfx's
+  // level K (CMSBWT_PFX_PAIR=0: none; the walk then probes pfx alone)
+  void build_pfx_pair() {
+    R.pfk = nullptr;
+    dpfk.release();
+    if (!R.pfx || !R.pfxDna || R.kmerB != 2 || R.kmerK < 2 || R.kmerK > 14 || !env_u32("CMSBWT_PFX_PAIR", 1)) return;
+    dpfk.alloc(16ull << (2 * (R.kmerK - 1)));
+    launch_ix_pfx_pair(R.pfx + R.pfxOff[R.kmerK], R.kmerK, dpfk.p, st);
+    HIPCHK(hipGetLastError());
+    R.pfk = dpfk.p;
+  }
   void build_prefix_tables(bool device) {
+    R.pfk = nullptr;
     R.pfx = nullptr;
     R.kmap = nullptr;
     R.kmerK = R.kmerB = 0;
@@ -908,6 +920,7 @@ struct Engine {
       R.kmerB = B;
       R.pfxExact = (cnt[0] == 0 && cnt[1] == 0) ? 1u : 0u;
       R.pfxDna = (sigma == 4 && cnt['A'] && cnt['C'] && cnt['G'] && cnt['T'] && !env_u32("CMSBWT_PFX_GENERIC", 0)) ? 1u : 0u;
+      build_pfx_pair();
       return;
     }
     std::vector<uint32_t> tab(total + 4, 0);
@@ -976,6 +989,7 @@ struct Engine {
     R.kmerB = B;
     R.pfxExact = (cnt[0] == 0 && cnt[1] == 0) ? 1u : 0u;
       R.pfxDna = (sigma == 4 && cnt['A'] && cnt['C'] && cnt['G'] && cnt['T'] && !env_u32("CMSBWT_PFX_GENERIC", 0)) ? 1u : 0u;
+    build_pfx_pair();
   }
 
   // Child table of the uniform-step walk: ld[k] packs LCP[k] (clipped to 16
@@ -1852,8 +1866,11 @@ struct Engine {
     dmt("w.windows");
     // crossing lists: (window, item) pairs sorted by window
     W.crossCnt.alloc(K);
-    W.itemOff.alloc(K);
     mk_win_cross(S, K, W.wincl.p, n, W.crossCnt.p, nullptr, nullptr, nullptr, cstatsP + 4, 0, st);
+    // fixed windows: the lists placed by distance without a sort (merge.hip
+    // k_xw_*; CMSBWT_XW_SORT=1 keeps the sort of the (window, item) pairs)
+    if (W.tgt && K && W.nw && !env_u32("CMSBWT_XW_SORT", 0) && cross_place(S, K, posBegin, P0, W)) return;
+    W.itemOff.alloc(K);
     exscan(W.crossCnt.p, W.itemOff.p, 0u, K);
     W.ncross = K ? (uint32_t)sum2(W.itemOff.p + (K - 1), W.crossCnt.p + (K - 1)) : 0;
     dmt("w.cross_count");
@@ -1871,6 +1888,48 @@ struct Engine {
       W.irec.alloc(std::max<uint32_t>(K, 1));
       mk_item_rec(S, K, W.irec.p, st);
     }
+  }
+  // crossing lists of the fixed windows by distance (merge.hip k_xw_*):
+  // sources sv = 0 .. nw (0: items before P0, else window sv - 1); false when
+  // a source is deeper than kXwMaxDepth windows (the sort path then runs)
+  bool cross_place(const ItemsSoA& S, uint32_t K, const uint32_t* posBegin, uint32_t P0, WinPlan& W) {
+    const uint32_t nw = W.nw, nsv = nw + 1;
+    DBuf<uint32_t> depth, toff, mx;
+    depth.alloc(nsv);
+    toff.alloc(nsv);
+    mk_xw_depth(posBegin, W.winStart.p, P0, nsv, W.crossCnt.p, depth.p, st);
+    exscan(depth.p, toff.p, 0u, nsv);
+    uint32_t maxDepth = 0;
+    {
+      mx.alloc(1);
+      size_t b = 0;
+      HIPCHK(rocprim::reduce(nullptr, b, depth.p, mx.p, 0u, (size_t)nsv, rocprim::maximum<uint32_t>(), st));
+      HIPCHK(rocprim::reduce(scratch(b), b, depth.p, mx.p, 0u, (size_t)nsv, rocprim::maximum<uint32_t>(), st));
+      maxDepth = read1(mx.p);
+    }
+    if (maxDepth > kXwMaxDepth) return false;
+    const uint64_t nT = sum2(toff.p + (nsv - 1), depth.p + (nsv - 1));
+    DBuf<uint32_t> T, segOff, count;
+    T.alloc(std::max<uint64_t>(nT, 1));
+    segOff.alloc(std::max<uint64_t>(nT, 1));
+    count.alloc((uint64_t)nw + 1);
+    mk_xw_hist(posBegin, W.winStart.p, P0, nsv, W.crossCnt.p, depth.p, toff.p, T.p, st);
+    mk_xw_count(depth.p, toff.p, T.p, nw, maxDepth, segOff.p, count.p, st);
+    HIPCHK(hipMemsetAsync(count.p + nw, 0, 4, st));
+    W.crossOff.alloc((uint64_t)nw + 1);
+    exscan(count.p, W.crossOff.p, 0u, (uint64_t)nw + 1);
+    const uint64_t nc = read1(W.crossOff.p + nw);
+    if (nc >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "crossing list longer than 2^32"};
+    W.ncross = (uint32_t)nc;
+    W.crossList.alloc(std::max<uint32_t>(W.ncross, 1));
+    mk_xw_place(posBegin, W.winStart.p, P0, nsv, W.crossCnt.p, depth.p, toff.p, segOff.p, W.crossOff.p,
+                W.crossList.p, st);
+    dmt("w.cross_place");
+    if (W.tgt && !env_u32("CMSBWT_NO_IREC", 0)) {
+      W.irec.alloc(std::max<uint32_t>(K, 1));
+      mk_item_rec(S, K, W.irec.p, st);
+    }
+    return true;
   }
   // the counter kernel between ev0 and ev1 (no synchronisation; counter_time
   // reads the duration once the stream has passed ev1)

@@ -1232,6 +1232,24 @@ constexpr bool kTgtSplit = CMSBWT_TGT_SPLIT != 0;
 #define CMSBWT_TGT_PHASES 3
 #endif
 constexpr int kTgtPhases = CMSBWT_TGT_PHASES;
+// attribution builds only (wrong counters): CMSBWT_TGT_SKIP bit 1 drops the
+// re-tests (the listed queries are discarded), bit 2 the full-cover walks,
+// bit 4 the partial-record walks
+#ifndef CMSBWT_TGT_SKIP
+#define CMSBWT_TGT_SKIP 0
+#endif
+constexpr int kTgtSkip = CMSBWT_TGT_SKIP;
+// CMSBWT_TGT_L3=1: the record walk settles the third level in registers too
+// (round 6): a query landing on the second-longest S item / third F item, or
+// past the shortest item of a class with exactly three, is added without
+// being listed.  The attribution builds (CMSBWT_TGT_SKIP) put the re-tests
+// and searches at 5.65 of 12.4 ms, and ~300 M of their 357 M queries land
+// there; but the extra compares on every record cost more (A/B one box,
+// bit-exact: counter 12.37-12.43 -> 13.23-13.34 ms), so it stays off
+#ifndef CMSBWT_TGT_L3
+#define CMSBWT_TGT_L3 0
+#endif
+constexpr bool kTgtL3 = CMSBWT_TGT_L3 != 0;
 
 
 constexpr uint32_t kFullRec = 0xffffffffu;
@@ -1321,6 +1339,7 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
   const uint64_t hasF1M = __ballot(hasF1);  // per wave
   const uint64_t hasF0M = __ballot(hasF0);  // (an F item implies items: in-range F lanes = in-range lanes & hasF0M)
   const uint64_t hasM = __ballot(has);
+  const uint64_t hasF2M = __ballot(hasF2), nS3M = __ballot(nS3), nF3M = __ballot(nF3);
   const uint32_t flags = (hasF0 ? 1u : 0u) | (hasF1 ? 2u : 0u) | (hasF2 ? 4u : 0u) | (nS3 ? 8u : 0u) |
                          (nF3 ? 16u : 0u) | (nS8 << 8) | (nF8 << 16);
   for (uint32_t k = 0; k < 6; k++) accL[k][tid] = 0;
@@ -1392,24 +1411,46 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
       mIn = ucmp<kULE>(tofH - aO, span);  // targets with items
       mInF = mIn & hasF0M;                // ... and a smaller=false item
     }
-    uint64_t mF0, mX, msl;
+    uint64_t mF0, mX, msl, mX3 = 0;
     if (S) {  // smaller=true: S items ascending, then F items
       const uint64_t m1 = ucmp<kUGT>(L, sl0) & ucmp<kNE>(L, fl0);  // past every S item: f (or end)
       const uint64_t m2 = ucmp<kULT>(L, sl0) & ucmp<kUGT>(L, sl1);   // the longest S item
       mF0 = mInF & m1;
       mX = mIn & m2;
       aS0 += sel_u32(cqv, mX);
-      msl = mIn & ~(m1 | m2);
+      if (kTgtL3) {
+        // the second-longest S item (the shortest when there are two), or
+        // below the shortest of exactly three S items: the third (FN:1534)
+        const uint64_t lt1 = ucmp<kULT>(L, sl1);
+        const uint64_t m3 = lt1 & ucmp<kUGT>(L, sl2);
+        const uint64_t m4 = ucmp<kULT>(L, sl2) & nS3M;
+        mX3 = mIn & (m3 | m4);
+        aS1 += sel_u32(cqv, mIn & m3);
+        aS2 += sel_u32(cqv, mIn & m4);
+        msl = mIn & ~(m1 | m2 | m3 | m4);
+      } else {
+        msl = mIn & ~(m1 | m2);
+      }
     } else {  // smaller=false: F items descending
       const uint64_t m1 = ucmp<kUGT>(L, fl0);                       // f
       const uint64_t m2 = ucmp<kULT>(L, fl0) & ucmp<kUGT>(L, fl1);   // the second F item (or end)
       mF0 = mInF & m1;
       mX = mIn & m2 & hasF1M;
       aF1 += sel_u32(cqv, mX);
-      msl = mIn & ~(m1 | m2);
+      if (kTgtL3) {
+        // the third F item (or end), or below the shortest of exactly three
+        // F items: end (nothing added, FN:1535-1536)
+        const uint64_t m3 = ucmp<kULT>(L, fl1) & ucmp<kUGT>(L, fl2);
+        const uint64_t m4 = ucmp<kULT>(L, fl2) & nF3M;
+        mX3 = mIn & m3 & hasF2M;
+        aF2 += sel_u32(cqv, mX3);
+        msl = mIn & ~(m1 | m2 | m3 | m4);
+      } else {
+        msl = mIn & ~(m1 | m2);
+      }
     }
     aF0 += sel_u32(cqv, mF0);
-    nGood = addc_mask(nGood, mF0 | mX);  // (disjoint masks)
+    nGood = addc_mask(nGood, mF0 | mX | mX3);  // (disjoint masks)
     if (msl) {
       if ((msl >> lane) & 1) {
         const uint32_t rk =
@@ -1491,7 +1532,7 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
         }
         r += e;
       }
-      if (qn) retest(cls, qn);
+      if (qn && !(kTgtSkip & 1)) retest(cls, qn);
     }
   };
   for (uint32_t ch = 0; ch < nList; ch += kTgtRec) {
@@ -1547,10 +1588,10 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
       const uint32_t nSf = tgt_partition_full(recG[wv], 0u, nS, lane);
       const uint32_t nFf = tgt_partition_full(recG[wv], kTgtRec - nF, kTgtRec, lane);
       if (kTgtPhases >= 2) {
-        walk(std::true_type{}, std::true_type{}, 0u, nSf);
-        walk(std::true_type{}, std::false_type{}, nSf, nS);
-        walk(std::false_type{}, std::true_type{}, kTgtRec - nF, kTgtRec - nF + nFf);
-        walk(std::false_type{}, std::false_type{}, kTgtRec - nF + nFf, kTgtRec);
+        if (!(kTgtSkip & 2)) walk(std::true_type{}, std::true_type{}, 0u, nSf);
+        if (!(kTgtSkip & 4)) walk(std::true_type{}, std::false_type{}, nSf, nS);
+        if (!(kTgtSkip & 2)) walk(std::false_type{}, std::true_type{}, kTgtRec - nF, kTgtRec - nF + nFf);
+        if (!(kTgtSkip & 4)) walk(std::false_type{}, std::false_type{}, kTgtRec - nF + nFf, kTgtRec);
       }
     } else if (kTgtPhases >= 2) {
       walk(std::true_type{}, std::false_type{}, 0u, nS);
@@ -1662,6 +1703,127 @@ __global__ void k_win_cross(const ItemsSoA it, uint32_t K, const uint32_t* __res
   if (!fill) { cnt[q] = c; return; }
   const uint32_t o = off[q];
   for (uint32_t k = 0; k < c; k++) { keyW[o + k] = wf + k; valQ[o + k] = q; }
+}
+
+// ---- crossing lists without a sort (round 6).  Item q crosses the windows
+// wf_q .. wf_q + c_q - 1 (k_win_cross: wf = its own window + 1, 0 for the
+// halo items before P0).  Number the item's "source" sv = wf_q (items of
+// window sv - 1; sv = 0: positions before P0) and the distance d = w - sv:
+// the items of one source that reach distance d are a filtered run of its
+// items, so window w's list is the concatenation over d of the runs of
+// source w - d.  Three passes, no sort (the (window, item) pairs were a
+// rocPRIM radix sort of ~2 x 10^8 keys, 5.7 ms on the side stream at config
+// 3): per source its depth (largest c) and n_sv(d) = #items with c > d; per
+// window the counts and the offsets of its runs; per source the placement.
+// The order inside a window's list (by distance, then item) differs from the
+// sorted order; the counter only sums over it.
+constexpr uint32_t kXwHist = kXwMaxDepth;  // depth handled in LDS (deeper sources: the sort path)
+__device__ __forceinline__ void xw_items(const uint32_t* posBegin, const uint32_t* winStart, uint32_t P0, uint32_t sv,
+                                         uint32_t& ib, uint32_t& ie) {
+  const uint32_t ps = sv == 0 ? 0u : winStart[sv - 1], pe = sv == 0 ? P0 : winStart[sv];
+  ib = posBegin[ps];
+  ie = posBegin[pe];
+}
+__global__ void __launch_bounds__(256) k_xw_depth(const uint32_t* __restrict__ posBegin,
+                                                  const uint32_t* __restrict__ winStart, uint32_t P0,
+                                                  const uint32_t* __restrict__ cnt, uint32_t* __restrict__ depth) {
+  __shared__ uint32_t mx[4];
+  const uint32_t sv = blockIdx.x;
+  uint32_t ib, ie;
+  xw_items(posBegin, winStart, P0, sv, ib, ie);
+  uint32_t m = 0;
+  for (uint32_t q = ib + threadIdx.x; q < ie; q += 256) m = max(m, cnt[q]);
+  for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+  if ((threadIdx.x & 63) == 0) mx[threadIdx.x >> 6] = m;
+  __syncthreads();
+  if (threadIdx.x == 0) depth[sv] = max(max(mx[0], mx[1]), max(mx[2], mx[3]));
+}
+// n_sv(d) for d < depth[sv] at T[toff[sv] + d] (suffix sums of a histogram
+// of c over the source's items)
+__global__ void __launch_bounds__(256) k_xw_hist(const uint32_t* __restrict__ posBegin,
+                                                 const uint32_t* __restrict__ winStart, uint32_t P0,
+                                                 const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ depth,
+                                                 const uint32_t* __restrict__ toff, uint32_t* __restrict__ T) {
+  __shared__ uint32_t h[kXwHist];
+  const uint32_t sv = blockIdx.x, D = depth[sv];
+  if (D == 0) return;
+  uint32_t ib, ie;
+  xw_items(posBegin, winStart, P0, sv, ib, ie);
+  for (uint32_t d = threadIdx.x; d < D; d += 256) h[d] = 0;
+  __syncthreads();
+  for (uint32_t q = ib + threadIdx.x; q < ie; q += 256) {
+    const uint32_t c = cnt[q];
+    if (c) atomicAdd(&h[c - 1], 1u);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint32_t acc = 0;
+    uint32_t* o = T + toff[sv];
+    for (uint32_t d = D; d-- > 0;) {
+      acc += h[d];
+      o[d] = acc;
+    }
+  }
+}
+// per target window w: its list length and the offset of each of its runs
+// inside it (run (sv, d) at segOff[toff[sv] + d]), distance 0 first
+__global__ void k_xw_count(const uint32_t* __restrict__ depth, const uint32_t* __restrict__ toff,
+                           const uint32_t* __restrict__ T, uint32_t nw, uint32_t maxDepth,
+                           uint32_t* __restrict__ segOff, uint32_t* __restrict__ count) {
+  const uint32_t w = blockIdx.x * blockDim.x + threadIdx.x;
+  if (w >= nw) return;
+  uint32_t run = 0;
+  const uint32_t dEnd = min(w + 1, maxDepth);
+  for (uint32_t d = 0; d < dEnd; d++) {
+    const uint32_t sv = w - d;
+    if (d < depth[sv]) {
+      const uint32_t k = toff[sv] + d;
+      segOff[k] = run;
+      run += T[k];
+    }
+  }
+  count[w] = run;
+}
+// per source: each item with c > d goes to window sv + d at its run's offset
+// plus its rank among the source's items with c > d (item order)
+__global__ void __launch_bounds__(256) k_xw_place(const uint32_t* __restrict__ posBegin,
+                                                  const uint32_t* __restrict__ winStart, uint32_t P0,
+                                                  const uint32_t* __restrict__ cnt, const uint32_t* __restrict__ depth,
+                                                  const uint32_t* __restrict__ toff,
+                                                  const uint32_t* __restrict__ segOff,
+                                                  const uint32_t* __restrict__ crossOff,
+                                                  uint32_t* __restrict__ crossList) {
+  __shared__ uint32_t base[kXwHist];
+  __shared__ uint32_t wsum[4], cmaxL[4];
+  const uint32_t sv = blockIdx.x, D = depth[sv];
+  if (D == 0) return;
+  uint32_t ib, ie;
+  xw_items(posBegin, winStart, P0, sv, ib, ie);
+  const uint32_t t0 = toff[sv];
+  for (uint32_t d = threadIdx.x; d < D; d += 256) base[d] = crossOff[sv + d] + segOff[t0 + d];
+  const uint32_t lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (uint32_t cb = ib; cb < ie; cb += 256) {
+    const uint32_t q = cb + threadIdx.x;
+    const uint32_t c = q < ie ? cnt[q] : 0u;
+    uint32_t m = c;
+    for (int o = 32; o > 0; o >>= 1) m = max(m, (uint32_t)__shfl_xor((int)m, o));
+    if (lane == 0) cmaxL[wv] = m;
+    __syncthreads();  // (also orders the base[] initialisation / previous chunk's updates)
+    const uint32_t cm = max(max(cmaxL[0], cmaxL[1]), max(cmaxL[2], cmaxL[3]));
+    for (uint32_t d = 0; d < cm; d++) {
+      const bool f = c > d;
+      const uint64_t b = __ballot(f);
+      if (lane == 0) wsum[wv] = (uint32_t)__popcll(b);
+      __syncthreads();
+      uint32_t before = 0;
+      for (uint32_t k = 0; k < wv; k++) before += wsum[k];
+      const uint32_t tot = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+      if (f) crossList[base[d] + before + (uint32_t)__popcll(b & ((1ull << lane) - 1))] = q;
+      __syncthreads();  // every read of wsum and base[d] is done
+      if (threadIdx.x == 0) base[d] += tot;
+    }
+    __syncthreads();
+  }
 }
 
 __global__ void k_win_cross_off(const uint32_t* __restrict__ keyW, uint32_t ncross, uint32_t nw,
@@ -2470,6 +2632,25 @@ void mk_win_cross(const ItemsSoA& it, uint32_t K, const uint32_t* winIncl, uint3
                   hipStream_t st) {
   if (K) hipLaunchKernelGGL(k_win_cross, g1(K), dim3(256), 0, st, it, K, winIncl, n, cnt, off, keyW, valQ, errs,
                             fill);
+}
+void mk_xw_depth(const uint32_t* posBegin, const uint32_t* winStart, uint32_t P0, uint32_t nsv, const uint32_t* cnt,
+                 uint32_t* depth, hipStream_t st) {
+  if (nsv) hipLaunchKernelGGL(k_xw_depth, dim3(nsv), dim3(256), 0, st, posBegin, winStart, P0, cnt, depth);
+}
+void mk_xw_hist(const uint32_t* posBegin, const uint32_t* winStart, uint32_t P0, uint32_t nsv, const uint32_t* cnt,
+                const uint32_t* depth, const uint32_t* toff, uint32_t* T, hipStream_t st) {
+  if (nsv) hipLaunchKernelGGL(k_xw_hist, dim3(nsv), dim3(256), 0, st, posBegin, winStart, P0, cnt, depth, toff, T);
+}
+void mk_xw_count(const uint32_t* depth, const uint32_t* toff, const uint32_t* T, uint32_t nw, uint32_t maxDepth,
+                 uint32_t* segOff, uint32_t* count, hipStream_t st) {
+  if (nw) hipLaunchKernelGGL(k_xw_count, g1(nw), dim3(256), 0, st, depth, toff, T, nw, maxDepth, segOff, count);
+}
+void mk_xw_place(const uint32_t* posBegin, const uint32_t* winStart, uint32_t P0, uint32_t nsv, const uint32_t* cnt,
+                 const uint32_t* depth, const uint32_t* toff, const uint32_t* segOff, const uint32_t* crossOff,
+                 uint32_t* crossList, hipStream_t st) {
+  if (nsv)
+    hipLaunchKernelGGL(k_xw_place, dim3(nsv), dim3(256), 0, st, posBegin, winStart, P0, cnt, depth, toff, segOff,
+                       crossOff, crossList);
 }
 void mk_win_cross_off(const uint32_t* keyW, uint32_t ncross, uint32_t nw, uint32_t* crossOff, hipStream_t st) {
   hipLaunchKernelGGL(k_win_cross_off, g1((uint64_t)nw + 1), dim3(256), 0, st, keyW, ncross, nw, crossOff);

@@ -146,6 +146,18 @@ void mk_win_cross(const ItemsSoA& it, uint32_t K, const uint32_t* winIncl, uint3
                   const uint32_t* off, uint32_t* keyW, uint32_t* valQ, unsigned long long* errs, int fill,
                   hipStream_t st);
 void mk_win_cross_off(const uint32_t* keyW, uint32_t ncross, uint32_t nw, uint32_t* crossOff, hipStream_t st);
+// crossing lists without a sort (merge.hip k_xw_*): sources sv = 0 .. nw
+// (0: items before P0, sv: window sv - 1); kXwMaxDepth bounds the depth
+constexpr uint32_t kXwMaxDepth = 1024;
+void mk_xw_depth(const uint32_t* posBegin, const uint32_t* winStart, uint32_t P0, uint32_t nsv, const uint32_t* cnt,
+                 uint32_t* depth, hipStream_t st);
+void mk_xw_hist(const uint32_t* posBegin, const uint32_t* winStart, uint32_t P0, uint32_t nsv, const uint32_t* cnt,
+                const uint32_t* depth, const uint32_t* toff, uint32_t* T, hipStream_t st);
+void mk_xw_count(const uint32_t* depth, const uint32_t* toff, const uint32_t* T, uint32_t nw, uint32_t maxDepth,
+                 uint32_t* segOff, uint32_t* count, hipStream_t st);
+void mk_xw_place(const uint32_t* posBegin, const uint32_t* winStart, uint32_t P0, uint32_t nsv, const uint32_t* cnt,
+                 const uint32_t* depth, const uint32_t* toff, const uint32_t* segOff, const uint32_t* crossOff,
+                 uint32_t* crossList, hipStream_t st);
 void mk_item_sk(const ItemsSoA& it, uint32_t K, hipStream_t st);
 // Queries of the checked counter (hr != nullptr) whose target t has mask[t]
 // are not answered on the device: (source slot, t) pairs go to list (cnt
