@@ -48,6 +48,13 @@ struct DevRef {
   // sorts after all of it), kPfxSmaller = smaller, kPfxSingle = that
   // interval holds one suffix.  Occurring entries keep (Start, Count).
   const uint32_t* pfx;
+  // Paired level-K table (DNA only, B = 2; nullptr: absent): line Z, one per
+  // (K-1)-symbol string, holds 8 entries of pfx's level K -- slot j < 4 the
+  // K-mer j.Z (Z its suffix), slot 4 + j the K-mer Z.j (Z its prefix).  The
+  // K-mers of text positions i and i + 1 share their middle K - 1 symbols, so
+  // the walk's probe of i (slot t[i]) and the prefetched probe of i + 1 (slot
+  // 4 + t[i+K]) read one 64-byte line instead of two random lines.
+  const uint32_t* pfk;
   uint32_t pfxOff[17];
   const uint8_t* kmap;  // 256 entries
   uint32_t kmerK, kmerB;

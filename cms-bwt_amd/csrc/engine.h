@@ -31,16 +31,32 @@
 // (MakeHeadKV over a counting iterator) and never aliases a sort buffer, so
 // tell it so; the first pass then reads the input directly.  Declared before
 // the rocPRIM device headers: their qualified call is looked up there.
-namespace cmsbwt { struct MakeHeadKV; }
+// The hook depends on a private rocPRIM detail: it is declared only for the
+// rocPRIM major version it was written against (4.x, ROCm 7.2), and it
+// returns its own type so that a static_assert below proves the overload is
+// the one selected (a rocPRIM change that stops it matching fails the build
+// instead of silently bringing the copy back).
+#include <rocprim/rocprim_version.hpp>
+#if ROCPRIM_VERSION >= 400000 && ROCPRIM_VERSION < 500000
+#define CMSBWT_NOALIAS_HOOK 1
+namespace cmsbwt {
+struct MakeHeadKV;
+struct NoAlias {  // "cannot alias", as the bool rocPRIM stores
+  __host__ __device__ constexpr operator bool() const { return false; }
+};
+}  // namespace cmsbwt
 BEGIN_ROCPRIM_NAMESPACE
 namespace detail {
 template <class V, class D, class O>
-inline bool can_iterators_alias(transform_iterator<counting_iterator<unsigned int, D>, cmsbwt::MakeHeadKV, V>, O*,
-                                const size_t) {
-  return false;
+inline cmsbwt::NoAlias can_iterators_alias(transform_iterator<counting_iterator<unsigned int, D>, cmsbwt::MakeHeadKV, V>,
+                                           O*, const size_t) {
+  return {};
 }
 }  // namespace detail
 END_ROCPRIM_NAMESPACE
+#else
+#define CMSBWT_NOALIAS_HOOK 0
+#endif
 #include <rocprim/rocprim.hpp>
 
 #include <fcntl.h>
@@ -92,6 +108,16 @@ struct MakeHeadKV {  // head idx -> its grouping fields
     return HeadKV{i, len[i] | (smaller[i] ? 0x80000000u : 0u), isa[i], tonext[i]};
   }
 };
+#if CMSBWT_NOALIAS_HOOK
+// the position sort's computed input must select the hook above (else rocPRIM
+// copies it into its buffers first, ~0.5 ms per step at 1e8 heads)
+static_assert(std::is_same<decltype(::rocprim::detail::can_iterators_alias(
+                               rocprim::make_transform_iterator(rocprim::make_counting_iterator<uint32_t>(0u),
+                                                                MakeHeadKV{}),
+                               (HeadKV*)nullptr, size_t{0})),
+                           NoAlias>::value,
+              "rocPRIM no longer selects the no-alias hook for the position sort's input");
+#endif
 struct AdjustedRuns {  // k_wr_adjust's rule, as a scan input
   const uint32_t* runs;
   const uint32_t* hl;
@@ -836,11 +862,12 @@ struct Engine {
   // next Start).  Only ASCII references: there the walk's signed (FN:55) and
   // unsigned orders agree.
   // the paired level-K table (DevRef::pfk) of a DNA reference, from pfx's
-  // level K (CMSBWT_PFX_PAIR=0: none; the walk then probes pfx alone)
+  // level K, with CMSBWT_PFX_PAIR=1 (a walk built with -DCMSBWT_PFX_PAIR=1
+  // probes it; ms_walk2.hip has the measurement)
   void build_pfx_pair() {
     R.pfk = nullptr;
     dpfk.release();
-    if (!R.pfx || !R.pfxDna || R.kmerB != 2 || R.kmerK < 2 || R.kmerK > 14 || !env_u32("CMSBWT_PFX_PAIR", 1)) return;
+    if (!R.pfx || !R.pfxDna || R.kmerB != 2 || R.kmerK < 2 || R.kmerK > 14 || !env_u32("CMSBWT_PFX_PAIR", 0)) return;
     dpfk.alloc(16ull << (2 * (R.kmerK - 1)));
     launch_ix_pfx_pair(R.pfx + R.pfxOff[R.kmerK], R.kmerK, dpfk.p, st);
     HIPCHK(hipGetLastError());

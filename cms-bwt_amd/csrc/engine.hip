@@ -359,6 +359,10 @@ int cmsbwt_run_sized(const cmsbwt_args* a, uint64_t args_size, const char* ref_p
 }
 
 int cmsbwt_run(const cmsbwt_args* a, const char* ref_path, const char* coll_path, cmsbwt_stats* stats_out) {
+  // (version-1 layout: n_gpus and backend are not read, include/cmsbwt.h)
+  const char* v = getenv("CMSBWT_VERBOSE");
+  if (v && *v && *v != '0')
+    fprintf(stderr, "cmsbwt_run: version-1 arguments, one GPU (n_gpus/backend need cmsbwt_run_sized)\n");
   return cmsbwt_run_sized(a, offsetof(cmsbwt_args, n_gpus), ref_path, coll_path, stats_out,
                           offsetof(cmsbwt_stats, device_peak_bytes));
 }

@@ -120,6 +120,8 @@ void launch_ix_pfx_count(const uint8_t* x, uint32_t n, uint32_t l, uint32_t B, c
 void launch_ix_pfx_write(const uint32_t* cfEx, const uint32_t* ctIn, const uint32_t* cf, uint64_t E1, uint32_t* o,
                          hipStream_t st);
 void launch_ix_pfx_one(uint32_t* tab, uint64_t E, const int32_t* sa, hipStream_t st);
+// paired level-K table (DevRef::pfk), 16 words per line of 4^(K-1)
+void launch_ix_pfx_pair(const uint32_t* tabK, uint32_t K, uint32_t* out, hipStream_t st);
 void launch_ix_pfx_answer(uint32_t* tab, const uint32_t* par, uint64_t E, uint32_t B, const int32_t* sa, uint32_t n,
                           uint32_t l, hipStream_t st);
 

@@ -340,6 +340,25 @@ constexpr bool kMemoCheck = CMSBWT_MEMO_CHECK != 0;
 #ifndef CMSBWT_PFX_PREFETCH
 #define CMSBWT_PFX_PREFETCH 0
 #endif
+// paired probe lines (round 6): with the paired level-K table (DevRef::pfk)
+// the probe of i and the prefetched probe of i + 1 read the same 64-byte line
+// (their K-mers share K - 1 symbols), so a mismatch region's heads take one
+// random line per two positions instead of one each.  Turns the prefetch on.
+// Measured (config 3, one box, bit-exact): L2 -> fabric read requests 286 M
+// -> 250 M per launch, walk kernel 10.73-10.86 -> 10.65-10.82 ms (within the
+// box's spread), with non-temporal probe loads 10.95-11.03 ms: the walk is
+// not bound by its random lines.  Off by default
+// (the table costs 4.3 GB); -DCMSBWT_PFX_PAIR=1 builds it, CMSBWT_PFX_PAIR=1
+// builds the table.
+#ifndef CMSBWT_PFX_PAIR
+#define CMSBWT_PFX_PAIR 0
+#endif
+// the paired probes as cached loads (non-temporal loads of one line do not
+// share a fabric request)
+#ifndef CMSBWT_PAIR_CACHED
+#define CMSBWT_PAIR_CACHED 1
+#endif
+constexpr bool kPairCached = CMSBWT_PAIR_CACHED != 0;
 // the register barrier after a memo hit in the specialised instance too (the
 // generic instance has it unless CMSBWT_MEMO_GENERIC_BARRIER=0).  Round 6:
 // the fault it guarded against is the backend pass SIOptimizeVGPRLiveRange,
@@ -426,7 +445,10 @@ k_ms_walk2(Walk2Args A) {
   uint32_t twAt = 0xffffffffu, wcode = 0, wm = 0;
   // (prefetch) the window's 2-bit codes of all 16 bytes and its first
   // non-symbol index; the prefetched entry (pfE) is that of position pfAt
-  constexpr bool kPrefetch = FAST && CMSBWT_PFX_PREFETCH != 0;
+  constexpr bool kPrefetch = FAST && (CMSBWT_PFX_PREFETCH != 0 || CMSBWT_PFX_PAIR != 0);
+  // paired lines when the table is there (a runtime choice: CMSBWT_PFX_PAIR=0)
+  const bool pairOn = kPrefetch && CMSBWT_PFX_PAIR != 0 && R.pfk != nullptr;
+  const uint32_t* const pfxK = pairOn ? R.pfk : R.pfx;  // where the prefetched entries live
   uint32_t wfull = 0, wbad = 0, pfAt = 0xffffffffu;
   uint2 pfE = make_uint2(0u, 0u);
   // the 32 text bytes t[t32At ..) the last skip step loaded around the match
@@ -520,13 +542,20 @@ k_ms_walk2(Walk2Args A) {
     phase = PH_PFX_PROBE;
     u6 = (int32_t)code;  // kept: the probe step replaces the window
     u7 = (int32_t)m;
-    ad0 = (uintptr_t)(R.pfx + pfxL[m] + 2 * code);
+    const bool pairK = pairOn && m == R.kmerK;
+    if (pairK) {  // slot t[i] of line t[i+1 .. i+K) (its K-1 symbol suffix)
+      const uint32_t K1 = 2 * (R.kmerK - 1);
+      ad0 = (uintptr_t)(R.pfk + 2 * (8ull * (code & ((1u << K1) - 1u)) + (code >> K1)));
+    } else {
+      ad0 = (uintptr_t)(R.pfx + pfxL[m] + 2 * code);
+    }
     use = U0E;
     if (kPrefetch && m == R.kmerK && R.kmerK <= 15 && wbad > R.kmerK) {
-      // the entry of i + 1: symbols 1 .. K of this window
+      // the entry of i + 1: symbols 1 .. K of this window (paired: slot
+      // 4 + t[i+K] of the same line t[i+1 .. i+K))
       const uint32_t K = R.kmerK;
       const uint32_t code1 = (wfull >> (32 - 2 * (K + 1))) & ((1u << (2 * K)) - 1u);
-      u8 = (int32_t)(pfxL[K] + 2 * code1);
+      u8 = pairK ? (int32_t)(2 * (8 * (code1 >> 2) + 4 + (code1 & 3))) : (int32_t)(pfxL[K] + 2 * code1);
       use |= U3E;
     }
     if (pfxExact) {
@@ -954,9 +983,14 @@ k_ms_walk2(Walk2Args A) {
     if (use & U3Q) v3 = ldu16(ad2 + 16);
     if (use & U4Q) v4 = ldu16(ad0 + 32);
     if (use & U5Q) v5 = ldu16(ad0 + 48);
-    if (use & U0E) { const uint2 w = ld8_nt(ad0); v0.x = w.x; v0.y = w.y; }
+    if (use & U0E) { const uint2 w = kPairCached && pairOn ? ld8(ad0) : ld8_nt(ad0); v0.x = w.x; v0.y = w.y; }
     if (use & U2E) { const uint2 w = ld8(ad2); v2.x = w.x; v2.y = w.y; }
-    if (kPrefetch && (use & U3E)) { const uint2 w = ld8_nt((uintptr_t)(R.pfx + (uint32_t)u8)); v3.x = w.x; v3.y = w.y; }
+    if (kPrefetch && (use & U3E)) {
+      const uintptr_t a3 = (uintptr_t)(pfxK + (uint32_t)u8);
+      const uint2 w = kPairCached && pairOn ? ld8(a3) : ld8_nt(a3);
+      v3.x = w.x;
+      v3.y = w.y;
+    }
     // PLCP skip (FN:1176-1185): the exit inside the 16-entry window below
     // the match end, if it is there (skS = the skip, or ~0u)
     uint32_t skS = 0xffffffffu;

@@ -328,6 +328,21 @@ __global__ void k_ix_pfx_one(uint32_t* __restrict__ tab, uint64_t E, const int32
 
 static inline dim3 gix(uint64_t n) { return dim3((unsigned)((n + 255) / 256)); }
 
+// paired level-K table (device_common.h DevRef::pfk): entry s of line Z
+__global__ void k_ix_pfx_pair(const uint32_t* __restrict__ tabK, uint32_t K, uint64_t nent,
+                              uint2* __restrict__ out) {
+  const uint64_t e = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= nent) return;
+  const uint64_t Z = e >> 3;
+  const uint32_t s = (uint32_t)e & 7u;
+  const uint64_t code = s < 4 ? ((uint64_t)s << (2 * (K - 1))) | Z : (Z << 2) | (s - 4);
+  out[e] = make_uint2(tabK[2 * code], tabK[2 * code + 1]);
+}
+void launch_ix_pfx_pair(const uint32_t* tabK, uint32_t K, uint32_t* out, hipStream_t st) {
+  const uint64_t nent = 8ull << (2 * (K - 1));
+  hipLaunchKernelGGL(k_ix_pfx_pair, gix(nent), dim3(256), 0, st, tabK, K, nent, (uint2*)out);
+}
+
 __global__ void k_ix_plcp8(const int32_t* __restrict__ plcp, uint32_t n, uint8_t* __restrict__ out) {
   const uint32_t q = blockIdx.x * blockDim.x + threadIdx.x;
   if (q < n) out[q] = (uint8_t)min(max(plcp[q], 0), 255);

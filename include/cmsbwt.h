@@ -105,7 +105,11 @@ typedef struct cmsbwt_ctx cmsbwt_ctx;
  * version-1 header stay safe; cmsbwt_run_sized takes sizeof(cmsbwt_args) and
  * sizeof(cmsbwt_stats) of the caller's header (unknown trailing args fields
  * read as zero) and is what new callers use (n_gpus, backend,
- * device_peak_bytes). */
+ * device_peak_bytes).
+ * NOTE: cmsbwt_run therefore IGNORES args->n_gpus and args->backend (it
+ * cannot know whether the caller's struct holds them) and always runs on one
+ * GPU; a caller that sets n_gpus > 1 must call cmsbwt_run_sized (the CLI and
+ * the Python mirror do).  With CMSBWT_VERBOSE=1 cmsbwt_run says so on stderr. */
 #define CMSBWT_ABI_VERSION 2
 int cmsbwt_abi_version(void);
 int cmsbwt_run(const cmsbwt_args* args, const char* ref_path, const char* coll_path,

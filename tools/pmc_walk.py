@@ -9,5 +9,5 @@ for r in csv.DictReader(open(files[0])):
             d = per.setdefault(k, {}).setdefault(r["Dispatch_Id"], {})
             d[r["Counter_Name"]] = d.get(r["Counter_Name"], 0) + float(r["Counter_Value"])
 for k, ds in per.items():
-    d = max(ds.values(), key=lambda x: x.get("TCC_MISS_sum", 0))
+    d = max(ds.values(), key=lambda x: x.get("TCC_MISS_sum", x.get("SQ_WAVE_CYCLES", 0)))
     print("variant", sys.argv[2], k, {c: f"{v:.3e}" for c, v in sorted(d.items())})
