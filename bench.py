@@ -51,6 +51,23 @@ def synth_reference(L: int, seed: int) -> bytes:
     return np.frombuffer(b"ACGT", dtype=np.uint8)[(h >> np.uint64(62)).astype(np.int64)].tobytes()
 
 
+def host_cpu():
+    """This host's CPU model and hardware threads (the CPU legs use one)."""
+    model = ""
+    try:
+        for ln in open("/proc/cpuinfo"):
+            if ln.startswith("model name"):
+                model = ln.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        avail = None
+    return {"model": model, "threads_total": os.cpu_count(), "threads_available": avail, "threads_used": 1}
+
+
 def cpu_baseline(ref_len, copies, p, seed, rle=True, full_copies=None):
     """Oracle (single-threaded CPU restatement) on a bounded sample of the same
     workload, collection stage only (parse .. .rl_bwt closed).  The counter
@@ -66,7 +83,8 @@ def cpu_baseline(ref_len, copies, p, seed, rle=True, full_copies=None):
         if rc:
             raise RuntimeError(f"oracle rc={rc}")
     chars = ref_len * copies
-    sample = {"value": round(chars / 1e6 / t_coll, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+    host = host_cpu()
+    sample = {"value": round(chars / 1e6 / t_coll, 3), "unit": "MB/s", "cores": 1, "kind": "port", "host": host,
               "sample": f"{ref_len // 10**6} MB ref + {copies} copies @{p * 100:g}% ({chars / 1e6:.0f} MB "
                         f"collection), oracle collection stage {t_coll:.2f} s on this host, index {t_idx:.2f} s "
                         "excluded",
@@ -80,6 +98,8 @@ def cpu_baseline(ref_len, copies, p, seed, rle=True, full_copies=None):
     # the build container), the sample timed here rides beside it.
     fs = full["oracle_collection_seconds"]
     return {"value": round(ref_len * full_copies / 1e6 / fs, 3), "unit": "MB/s", "cores": 1, "kind": "port",
+            "host": host, "value_timed_on": "build container (8-vCPU Xeon), not this host: the full-size oracle "
+                                           "run takes ~28 min; `bounded_sample` is the leg timed on this host",
             "sample": f"the whole workload ({full_copies} copies, {ref_len * full_copies / 1e6:.0f} MB), oracle "
                       f"collection stage {fs:.0f} s on one core of the build container (tests/golden/golden.json); "
                       f"the bounded sample timed on this host is `bounded_sample`",

@@ -429,6 +429,7 @@ void Engine::dm_units(int64_t* out) {
   const uint32_t n = R.n;
   if ((uint64_t)dm.E + n - 1 >= 0xffffffffull) throw InputError{CMSBWT_ELIMIT, "too many writer units"};
   const uint32_t Uw = dm.Uw = dm.E + n - 1;
+  dmt(nullptr);
   dm.bucket.alloc(n);
   {
     DBuf<int32_t> cnt;
@@ -436,6 +437,7 @@ void Engine::dm_units(int64_t* out) {
     inscan(diff.p, cnt.p, n, rocprim::plus<int32_t>());
     mk_bucket(cnt.p, hasHead.p, n, dm.bucket.p, st);
   }
+  dmt("bucket");
   ItemSet& IS = dm.IS;
   DBuf<uint32_t> m;
   m.alloc(n);
@@ -447,6 +449,7 @@ void Engine::dm_units(int64_t* out) {
   const uint32_t V = dm.V = (uint32_t)V64;
   dm.rOf.alloc(std::max<uint32_t>(V, 1));
   mk_el_rof(dm.eBase.p, m.p, n, dm.rOf.p, st);
+  dmt("el_count+rof");
   const uint32_t Hp = dm.Hp;
   dm.cum.alloc(std::max<uint32_t>(Hp, 1));
   if (Hp)
@@ -455,6 +458,7 @@ void Engine::dm_units(int64_t* out) {
   dm.info2.alloc(n);
   const ElemIn ei = dm_elem_in();
   mk_dm_el_info(ei, dm.P0, dm.P1, st);
+  dmt("cum+el_info");
   DBuf<uint32_t> runs, adj;
   DBuf<unsigned long long> sym;
   runs.alloc(std::max<uint32_t>(V, 1)); adj.alloc(std::max<uint32_t>(V, 1)); sym.alloc(std::max<uint32_t>(V, 1));
@@ -464,6 +468,7 @@ void Engine::dm_units(int64_t* out) {
   if (V) {
     mk_el_wr_count(ei, V, runs.p, sym.p, dm.ehl.p, st);
     mk_dm_el_adj(dm.rOf.p, dm.ehl.p, runs.p, V, adj.p, st);
+    dmt("wr_count+adj");
     // runs and symbols in one packed inclusive scan when the totals fit (as
     // the one-GPU writer), else two
     uint64_t symTotal = 0;
@@ -487,9 +492,12 @@ void Engine::dm_units(int64_t* out) {
       inscan(sym.p, dm.symIn.p, V, rocprim::plus<unsigned long long>());
     }
   }
+  dmt("elem_scans");
   mk_dm_el_units(dm.eBase.p, m.p, dm.runIn.p, dm.symPacked ? nullptr : dm.symIn.p, dm.ehl.p, n, dm.E, Uw, out, st);
   HIPCHK(hipGetLastError());
   sync();
+  dmt("el_units");
+  dmtFlush("dm_units");
 }
 
 ElemIn Engine::dm_elem_in() {
@@ -501,6 +509,7 @@ ElemIn Engine::dm_elem_in() {
 
 uint64_t Engine::dm_emit(const int64_t* unitsAll) {
   const uint32_t n = R.n, Uw = dm.Uw;
+  dmt(nullptr);
   DBuf<unsigned long long> sym, own, srcOff;
   dm.uruns.alloc(Uw); dm.uhl.alloc(Uw); sym.alloc(Uw); dm.uprev.alloc(Uw);
   mk_dm_units_unpack(unitsAll, Uw, dm.uruns.p, dm.uhl.p, sym.p, st);
@@ -515,6 +524,7 @@ uint64_t Engine::dm_emit(const int64_t* unitsAll) {
   exscan(sym.p, dm.symOff.p, 0ull, Uw);
   dm.Rn = sum2(dm.runOff.p + (Uw - 1), dm.uruns.p + (Uw - 1));
   dm.symbols = sum2(dm.symOff.p + (Uw - 1), sym.p + (Uw - 1));
+  dmt("unit_scans");
   const ElemIn ei = dm_elem_in();
   if (dm.rank == 0) {
     // rank 0 holds the output: its own runs go straight to their global indices
@@ -537,6 +547,8 @@ uint64_t Engine::dm_emit(const int64_t* unitsAll) {
   }
   HIPCHK(hipGetLastError());
   sync();
+  dmt("emit");
+  dmtFlush("dm_emit");
   return dm.Rloc;
 }
 

@@ -152,15 +152,18 @@ def test_grouping_three_sorts(engine, oracle, tmp_path, case):
 
 
 @pytest.mark.parametrize("env", [{"CMSBWT_TGTWIN": "7"}, {"CMSBWT_TGTWIN": "1"}, {"CMSBWT_TGTWIN": "64"},
-                                 {"CMSBWT_TGTWIN": "200"}, {"CMSBWT_COUNTER_WIN": "1"}],
+                                 {"CMSBWT_TGTWIN": "200"}, {"CMSBWT_COUNTER_WIN": "1"},
+                                 {"CMSBWT_XW_SORT": "1"}, {"CMSBWT_XW_SORT": "1", "CMSBWT_TGTWIN": "7"}],
                          ids=["tiny_windows", "one_target_windows", "one_wave_windows", "ragged_windows",
-                              "slot_windows_kernel"])
+                              "slot_windows_kernel", "sorted_crossing_lists", "sorted_crossing_lists_tiny"])
 @pytest.mark.parametrize("case", cases.small_cases()[:6], ids=lambda c: c[0])
 def test_counter_target_major(engine, oracle, tmp_path, case, env):
     """counterSmallerThanHead (FN:1523-1603) target-major with per-lane
-    accumulators: tiny windows stress the crossing lists, windows of one wave
-    or not a multiple of 64 targets leave waves idle or partly filled; the
-    slot-budget kernel (k_counter_win) stays selectable."""
+    accumulators: tiny windows stress the crossing lists (placed by distance,
+    k_xw_*; one-target windows make sources deeper than kXwMaxDepth, which
+    take the sort), windows of one wave or not a multiple of 64 targets leave
+    waves idle or partly filled; the sorted crossing lists and the slot-budget
+    kernel (k_counter_win) stay selectable."""
     _compare(engine, oracle, tmp_path, case, env=env)
 
 
