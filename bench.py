@@ -70,10 +70,11 @@ def host_cpu():
 
 def cpu_baseline(ref_len, copies, p, seed, rle=True, full_copies=None):
     """Oracle (single-threaded CPU restatement) on a bounded sample of the same
-    workload, collection stage only (parse .. .rl_bwt closed).  The counter
-    phase grows with the copy count, so a short sample overstates the CPU's
-    rate: the oracle's own full-size run of this workload (timed once in the
-    build container, tests/golden/golden.json) is reported beside it."""
+    workload, collection stage only (parse .. .rl_bwt closed), timed on this
+    host: that is `value`.  The counter phase grows with the copy count, so a
+    short sample overstates the CPU's rate on the full workload; the oracle's
+    own full-size run of this workload (timed once in the build container,
+    tests/golden/golden.json) rides beside it as `full_workload`."""
     import oracle_lib
     gen = oracle_lib.GEN
     with tempfile.TemporaryDirectory() as td:
@@ -83,31 +84,24 @@ def cpu_baseline(ref_len, copies, p, seed, rle=True, full_copies=None):
         if rc:
             raise RuntimeError(f"oracle rc={rc}")
     chars = ref_len * copies
-    host = host_cpu()
-    sample = {"value": round(chars / 1e6 / t_coll, 3), "unit": "MB/s", "cores": 1, "kind": "port", "host": host,
-              "sample": f"{ref_len // 10**6} MB ref + {copies} copies @{p * 100:g}% ({chars / 1e6:.0f} MB "
-                        f"collection), oracle collection stage {t_coll:.2f} s on this host, index {t_idx:.2f} s "
-                        "excluded",
-              "seconds": round(t_coll, 3)}
+    out = {"value": round(chars / 1e6 / t_coll, 3), "unit": "MB/s", "cores": 1, "kind": "port", "host": host_cpu(),
+           "sample": f"{ref_len // 10**6} MB ref + {copies} copies @{p * 100:g}% ({chars / 1e6:.0f} MB collection) "
+                     f"of the bench workload's generator, oracle collection stage {t_coll:.2f} s on this host "
+                     f"(one thread), index {t_idx:.2f} s excluded",
+           "seconds": round(t_coll, 3)}
     full = golden_entry(ref_len, full_copies, p, seed) if full_copies else None
-    if not (full and full.get("oracle_collection_seconds")):
-        return sample
-    # The counter phase (FN:1523-1603) grows with the copy count, so the
-    # bounded sample overstates the CPU's rate on the workload itself; the
-    # value is the oracle's own full-size run of this workload (timed once in
-    # the build container), the sample timed here rides beside it.
-    fs = full["oracle_collection_seconds"]
-    return {"value": round(ref_len * full_copies / 1e6 / fs, 3), "unit": "MB/s", "cores": 1, "kind": "port",
-            "host": host, "value_timed_on": "build container (8-vCPU Xeon), not this host: the full-size oracle "
-                                           "run takes ~28 min; `bounded_sample` is the leg timed on this host",
-            "sample": f"the whole workload ({full_copies} copies, {ref_len * full_copies / 1e6:.0f} MB), oracle "
-                      f"collection stage {fs:.0f} s on one core of the build container (tests/golden/golden.json); "
-                      f"the bounded sample timed on this host is `bounded_sample`",
-            "seconds": fs, "bounded_sample": sample,
-            "sample_over_full": round(sample["value"] / (ref_len * full_copies / 1e6 / fs), 2)}
+    if full and full.get("oracle_collection_seconds"):
+        fs = full["oracle_collection_seconds"]
+        fv = ref_len * full_copies / 1e6 / fs
+        out["full_workload"] = {"value": round(fv, 3), "unit": "MB/s", "cores": 1, "seconds": fs,
+                                "timed_on": "build container (8-vCPU Xeon), once (~28 min; tests/golden/golden.json)",
+                                "sample": f"the whole workload ({full_copies} copies, "
+                                          f"{ref_len * full_copies / 1e6:.0f} MB)"}
+        out["sample_over_full"] = round(out["value"] / fv, 2)
+    return out
 
 
-PMC_FILE = "r05_final_pmc.json"  # tools/gpu_round_prof.sh: tools/gpu_prof_r.sh + tools/pmc_main.py (this round's kernels)
+PMC_FILE = "r06_final_pmc.json"  # tools/gpu_round_prof.sh: tools/gpu_prof_r.sh + tools/pmc_main.py (this round's kernels)
 
 # Algorithmic bytes of the MS walk (k_ms_walk2) -- what THIS algorithm must
 # move, each byte counted once (DESIGN.md §3.1 "Roofline"):
