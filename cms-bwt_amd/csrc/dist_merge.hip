@@ -466,7 +466,11 @@ void Engine::dm_units(int64_t* out) {
   dm.runIn.alloc(std::max<uint32_t>(V, 1));
   dm.symPacked = false;
   if (V) {
-    mk_el_wr_count(ei, V, runs.p, sym.p, dm.ehl.p, st);
+    // the elements' segments kept for dm_emit (CMSBWT_WR_SEGBUF=0: recomputed
+    // there, as the round-5 writer did)
+    if (env_u32("CMSBWT_WR_SEGBUF", 1)) dm.segs.alloc(V);
+    else dm.segs.release();
+    mk_el_wr_count(ei, V, runs.p, sym.p, dm.ehl.p, st, dm.segs.p);
     mk_dm_el_adj(dm.rOf.p, dm.ehl.p, runs.p, V, adj.p, st);
     dmt("wr_count+adj");
     // runs and symbols in one packed inclusive scan when the totals fit (as
@@ -531,7 +535,7 @@ uint64_t Engine::dm_emit(const int64_t* unitsAll) {
     dm.gStart.alloc(std::max<uint64_t>(dm.Rn, 1));
     dm.gChar.alloc(std::max<uint64_t>(dm.Rn, 1));
     mk_dm_el_emit(ei, dm.V, dm.runIn.p, dm.symPacked ? nullptr : dm.symIn.p, dm.runOff.p, dm.symOff.p, dm.uprev.p, dm.uhl.p, dm.ehl.p,
-                  dm.gStart.p, dm.gChar.p, st);
+                  dm.gStart.p, dm.gChar.p, st, dm.segs.p);
     dm.Rloc = 0;
   } else {
     // this rank's runs, its units in unit order (rank 0 places them)
@@ -543,10 +547,11 @@ uint64_t Engine::dm_emit(const int64_t* unitsAll) {
     dm.locStart.alloc(std::max<uint64_t>(dm.Rloc, 1));
     dm.locChar.alloc(std::max<uint64_t>(dm.Rloc, 1));
     mk_dm_el_emit(ei, dm.V, dm.runIn.p, dm.symPacked ? nullptr : dm.symIn.p, srcOff.p, dm.symOff.p, dm.uprev.p, dm.uhl.p, dm.ehl.p,
-                  dm.locStart.p, dm.locChar.p, st);
+                  dm.locStart.p, dm.locChar.p, st, dm.segs.p);
   }
   HIPCHK(hipGetLastError());
   sync();
+  dm.segs.release();
   dmt("emit");
   dmtFlush("dm_emit");
   return dm.Rloc;

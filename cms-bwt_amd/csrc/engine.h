@@ -2925,6 +2925,7 @@ struct Engine {
     DBuf<int64_t> bucket;
     DBuf<uint32_t> eBase, rOf, ehl;
     DBuf<uint4> info1;
+    DBuf<uint4> segs;  // each element's segments (segs_pack), dm_units -> dm_emit
     DBuf<unsigned long long> info2, cum, runIn, symIn;  // symPacked: runIn holds both (symIn unused)
     bool symPacked = false;
     DBuf<uint32_t> uruns, uhl, uprev;

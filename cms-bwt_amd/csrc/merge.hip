@@ -2018,9 +2018,18 @@ void mk_el_wr_emit_tiles(const ElemIn& w, uint32_t V, const WrState* tilePre, ui
 }
 
 __global__ void k_el_wr_count(ElemArgs A, uint32_t V, uint32_t* __restrict__ runs, unsigned long long* __restrict__ sym,
-                              uint32_t* __restrict__ hl) {
+                              uint32_t* __restrict__ hl, uint4* __restrict__ segs) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= V) return;
+  if (segs) {  // the segments kept for the emission (sharded writer, round 6)
+    const ElemSegs g = d_elem_collect(A, e);
+    const WrState w = g.state();
+    runs[e] = (uint32_t)w.runs;
+    sym[e] = w.sym;
+    hl[e] = w.hl;
+    segs[e] = segs_pack(g);
+    return;
+  }
   int prev = -1, first = -1;
   uint32_t nr = 0;
   unsigned long long ns = 0;
@@ -2173,7 +2182,8 @@ __global__ void k_dm_el_emit(ElemArgs A, uint32_t V, const uint32_t* __restrict_
                              const unsigned long long* __restrict__ unitRunOff,
                              const unsigned long long* __restrict__ unitSymOff, const uint32_t* __restrict__ prevHL,
                              const uint32_t* __restrict__ unitHL, const uint32_t* __restrict__ hl,
-                             unsigned long long* __restrict__ runStart, uint8_t* __restrict__ runChar) {
+                             unsigned long long* __restrict__ runStart, uint8_t* __restrict__ runChar,
+                             const uint4* __restrict__ segs) {
   const uint32_t e = blockIdx.x * blockDim.x + threadIdx.x;
   if (e >= V) return;
   const uint32_t r = A.rOf[e];
@@ -2191,7 +2201,7 @@ __global__ void k_dm_el_emit(ElemArgs A, uint32_t V, const uint32_t* __restrict_
     j += es.r(e - 1) - (e0 ? es.r(e0 - 1) : 0ull) - (joined ? 1u : 0u);
   }
   unsigned long long pos = unitSymOff[u] + (e ? es.s(e - 1) : 0ull) - (e0 ? es.s(e0 - 1) : 0ull);
-  d_elem_segments(A, e, [&](uint8_t c, unsigned long long cnt) {
+  auto put = [&](uint8_t c, unsigned long long cnt) {
     if ((int)c != prev) {
       runStart[j] = pos;
       runChar[j] = c;
@@ -2199,7 +2209,15 @@ __global__ void k_dm_el_emit(ElemArgs A, uint32_t V, const uint32_t* __restrict_
     }
     prev = c;
     pos += cnt;
-  });
+  };
+  if (segs) {  // read back sequentially instead of re-gathering the per-slot inputs
+    const ElemSegs g = segs_unpack(segs[e]);
+#pragma unroll
+    for (uint32_t k = 0; k < 3; k++)
+      if (k < g.n) put((uint8_t)g.ch(k), g.cnt(k));
+  } else {
+    d_elem_segments(A, e, put);
+  }
 }
 
 
@@ -2759,8 +2777,8 @@ void mk_el_rof(const uint32_t* elemBase, const uint32_t* m, uint32_t n, uint32_t
   if (n) hipLaunchKernelGGL(k_el_rof, g1(n), dim3(256), 0, st, elemBase, m, n, rOf);
 }
 void mk_el_wr_count(const ElemIn& w, uint32_t V, uint32_t* runs, unsigned long long* sym, uint32_t* hl,
-                    hipStream_t st) {
-  if (V) hipLaunchKernelGGL(k_el_wr_count, g1(V), dim3(256), 0, st, elem_args(w), V, runs, sym, hl);
+                    hipStream_t st, uint4* segs) {
+  if (V) hipLaunchKernelGGL(k_el_wr_count, g1(V), dim3(256), 0, st, elem_args(w), V, runs, sym, hl, segs);
 }
 void mk_el_wr_emit(const ElemIn& w, uint32_t V, const unsigned long long* runOff, const unsigned long long* symOff,
                    const uint32_t* prevHL, unsigned long long* runStart, uint8_t* runChar, hipStream_t st) {
@@ -2787,9 +2805,9 @@ void mk_dm_el_units(const uint32_t* elemBase, const uint32_t* m, const unsigned 
 void mk_dm_el_emit(const ElemIn& w, uint32_t V, const unsigned long long* runIn, const unsigned long long* symIn,
                    const unsigned long long* unitRunOff, const unsigned long long* unitSymOff, const uint32_t* prevHL,
                    const uint32_t* unitHL, const uint32_t* hl, unsigned long long* runStart, uint8_t* runChar,
-                   hipStream_t st) {
+                   hipStream_t st, const uint4* segs) {
   if (V) hipLaunchKernelGGL(k_dm_el_emit, g1(V), dim3(256), 0, st, elem_args(w), V, w.elemBase, runIn, symIn,
-                            unitRunOff, unitSymOff, prevHL, unitHL, hl, runStart, runChar);
+                            unitRunOff, unitSymOff, prevHL, unitHL, hl, runStart, runChar, segs);
 }
 void mk_grp_big_maporder(const uint32_t* bpos, uint32_t nb, const uint32_t* hb, const uint32_t* off,
                          unsigned long long* key, uint32_t* perm, uint32_t* ts, uint8_t* sm, unsigned long long* tKey,

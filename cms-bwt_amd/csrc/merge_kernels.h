@@ -234,8 +234,10 @@ struct ElemIn {
 void mk_el_info(const ElemIn& w, hipStream_t st);
 void mk_el_count(const uint32_t* headBase, uint32_t n, uint32_t E, uint32_t H, uint32_t* m, hipStream_t st);
 void mk_el_rof(const uint32_t* elemBase, const uint32_t* m, uint32_t n, uint32_t* rOf, hipStream_t st);
+// segs != null: each element's segments also stored (16 B, segs_pack) for
+// mk_dm_el_emit to read back
 void mk_el_wr_count(const ElemIn& w, uint32_t V, uint32_t* runs, unsigned long long* sym, uint32_t* hl,
-                    hipStream_t st);
+                    hipStream_t st, uint4* segs = nullptr);
 // run and symbol offsets packed into one 64-bit scan (symbol totals < 2^34,
 // run totals < 2^30): k_el_wr_emit takes the packed offsets with symOff == nullptr
 constexpr uint32_t kPackSymBits = 34;
@@ -263,7 +265,7 @@ void mk_dm_el_units(const uint32_t* elemBase, const uint32_t* m, const unsigned 
 void mk_dm_el_emit(const ElemIn& w, uint32_t V, const unsigned long long* runIn, const unsigned long long* symIn,
                    const unsigned long long* unitRunOff, const unsigned long long* unitSymOff, const uint32_t* prevHL,
                    const uint32_t* unitHL, const uint32_t* hl, unsigned long long* runStart, uint8_t* runChar,
-                   hipStream_t st);
+                   hipStream_t st, const uint4* segs = nullptr);
 
 // dist_kernels.hip: position-sharded merge (multi-GPU)
 void mk_dm_owner(const uint32_t* vals, const uint32_t* idx, uint64_t n, const uint32_t* split, uint32_t world,
