@@ -1250,6 +1250,20 @@ constexpr int kTgtSkip = CMSBWT_TGT_SKIP;
 #define CMSBWT_TGT_L3 0
 #endif
 constexpr bool kTgtL3 = CMSBWT_TGT_L3 != 0;
+// CMSBWT_TGT_THR_LDS=1: the re-tests and searches read a listed query's
+// target fields (class lens, flags, first F item) from LDS (two 16-B reads)
+// instead of five / two ds_bpermute from the owning lane.  The 8 KB it adds
+// leave five blocks per CU instead of seven; measured (round 6, A/B one box,
+// bit-exact): counter 12.36-12.39 -> 14.73-14.75 ms, so the shuffles stay
+#ifndef CMSBWT_TGT_THR_LDS
+#define CMSBWT_TGT_THR_LDS 0
+#endif
+constexpr bool kThrLds = CMSBWT_TGT_THR_LDS != 0;
+// (with the LDS fields: 14.95-14.98 ms, no better than one batch)
+#ifndef CMSBWT_TGT_RETEST2
+#define CMSBWT_TGT_RETEST2 0
+#endif
+constexpr bool kRetest2 = CMSBWT_TGT_RETEST2 != 0;
 
 
 constexpr uint32_t kFullRec = 0xffffffffu;
@@ -1304,6 +1318,7 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
   __shared__ uint32_t accL[6][256];      // 6 KB: adds settled in the search passes, per target
   __shared__ uint32_t qS[4][kTgtS];       // 4 KB: queries left for binary searches
   __shared__ uint64_t noItL[4];           // per wave: targets without items
+  __shared__ uint4 thrL[kThrLds ? 2 : 1][kThrLds ? 256 : 1];  // per target: (sl0, sl1, sl2, fl0), (fl1, fl2, flags, fidx)
   const ItemsSoA& it = A.it;
   const uint32_t w = blockIdx.x, tid = threadIdx.x, lane = tid & 63;
   const uint32_t wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1343,6 +1358,10 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
   const uint32_t flags = (hasF0 ? 1u : 0u) | (hasF1 ? 2u : 0u) | (hasF2 ? 4u : 0u) | (nS3 ? 8u : 0u) |
                          (nF3 ? 16u : 0u) | (nS8 << 8) | (nF8 << 16);
   for (uint32_t k = 0; k < 6; k++) accL[k][tid] = 0;
+  if (kThrLds) {
+    thrL[0][tid] = make_uint4(sl0, sl1, sl2, fl0);
+    thrL[1][tid] = make_uint4(fl1, fl2, flags, fidx);
+  }
   // lanes without items never fall in a record's range (their pairs are
   // counted once per staged record: counterDoNothing, FN:1530)
   const uint32_t tofH = has ? toff : 0x40000000u;
@@ -1368,7 +1387,15 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
       const uint32_t en = act ? myS[d + lane] : 0u;
       // the target's item range from its owning lane
       const int own = (int)((en >> 16) & 63u);
-      const uint32_t fo = __shfl(fidx, own), fl = __shfl(flags, own);
+      uint32_t fo, fl;
+      if (kThrLds) {
+        const uint4 b = thrL[1][(wv << 6) + own];
+        fo = b.w;
+        fl = b.z;
+      } else {
+        fo = __shfl(fidx, own);
+        fl = __shfl(flags, own);
+      }
       if (act) {
         const uint4 rc = myR[en & 0xffffu];
         const uint32_t tq = T0 + ((en >> 16) & 0xffu);
@@ -1460,53 +1487,92 @@ __global__ void __launch_bounds__(256, 7) k_counter_tgt(CounterArgs A) {
       qn += (uint32_t)__popcll(msl);
     }
   };
-  // search pass over the listed queries, 64 at a time: first the three
-  // longest items of the class, read from the target's owning lane
-  // (ds_bpermute); what they do not settle goes to the wave's search list,
-  // binary-searched 64 at a time
-  auto retest = [&](auto cls, uint32_t qn) {
+  // search pass over the listed queries: first the three longest items of
+  // the class (the target's fields from LDS, or from the owning lane by
+  // ds_bpermute); what they do not settle goes to the wave's search list,
+  // binary-searched 64 at a time.
+  // A listed query's landing by the three longest items of its class (0 f,
+  // 1..3 S top 0..2, 4..5 F items 1..2; 6 end / none; 7 search), its count
+  auto decide = [&](auto cls, uint32_t en, bool act, uint32_t& cq) -> uint32_t {
     constexpr bool S = decltype(cls)::value;
+    const int own = (int)((en >> 16) & 63u);
+    uint32_t o0, o1, o2, of0, fl;
+    if (kThrLds) {  // (lanes past the list read their wave's target 0: harmless)
+      const uint4 a = thrL[0][(wv << 6) + own], b = thrL[1][(wv << 6) + own];
+      o0 = S ? a.x : a.w;
+      o1 = S ? a.y : b.x;
+      o2 = S ? a.z : b.y;
+      of0 = a.w;
+      fl = b.z;
+    } else {
+      o0 = __shfl(S ? sl0 : fl0, own);
+      o1 = __shfl(S ? sl1 : fl1, own);
+      o2 = __shfl(S ? sl2 : fl2, own);
+      of0 = __shfl(fl0, own);
+      fl = __shfl(flags, own);
+    }
+    uint32_t dst = 6;
+    cq = 0;
+    if (act) {
+      const uint4 rc = myR[en & 0xffffu];
+      const uint32_t L = rc.x - (T0 + (en >> 16));
+      cq = rc.z & 0x7fffffffu;
+      const bool g0 = L < o0, g1 = L < o1, g2 = L < o2;
+      const bool ne = (L != o0) & (L != o1) & (L != o2);
+      dst = 7;
+      if (S) {
+        if (!g0 & ne) dst = (fl & 1u) ? ((L != of0) ? 0u : 7u) : 6u;
+        else if (g0 & !g1 & ne) dst = 1;
+        else if (g1 & !g2 & ne) dst = 2;
+        else if (g2 & ne & ((fl & 8u) != 0)) dst = 3;
+      } else {
+        if (!g0 & ne) dst = (fl & 1u) ? 0u : 6u;
+        else if (g0 & !g1 & ne) dst = (fl & 2u) ? 4u : 6u;
+        else if (g1 & !g2 & ne) dst = (fl & 4u) ? 5u : 6u;
+        else if (g2 & ne & ((fl & 16u) != 0)) dst = 6;
+      }
+    }
+    return dst;
+  };
+  // the add of a settled query, or its place in the wave's search list
+  auto settle = [&](auto cls, uint32_t en, uint32_t dst, uint32_t cq) {
+    constexpr bool S = decltype(cls)::value;
+    if (dst < 6) {
+      atomicAdd(&accL[dst][en >> 16], cq);
+      qs.good++;
+    }
+    const uint64_t smS = __ballot(dst == 7);
+    if (dst == 7) {
+      const uint32_t rk =
+          __builtin_amdgcn_mbcnt_hi((uint32_t)(smS >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)smS, 0u));
+      myS[nSearch + rk] = en | (S ? 0x80000000u : 0u);
+    }
+    nSearch += (uint32_t)__popcll(smS);
+  };
+  // the pass, 64 queries at a time (two batches per iteration with
+  // CMSBWT_TGT_RETEST2, their LDS reads in flight together)
+  auto retest = [&](auto cls, uint32_t qn) {
     __builtin_amdgcn_wave_barrier();
-    for (uint32_t d = 0; d < qn; d += 64) {
-      const bool act = d + lane < qn;
-      const uint32_t en = act ? myQ[d + lane] : 0u;
-      const int own = (int)((en >> 16) & 63u);
-      const uint32_t o0 = __shfl(S ? sl0 : fl0, own), o1 = __shfl(S ? sl1 : fl1, own);
-      const uint32_t o2 = __shfl(S ? sl2 : fl2, own), of0 = __shfl(fl0, own);
-      const uint32_t fl = __shfl(flags, own);
-      uint32_t dst = 6;  // 0 f, 1..3 S top 0..2, 4..5 F items 1..2; 6 end / none; 7 search
-      uint32_t cq = 0;
-      if (act) {
-        const uint4 rc = myR[en & 0xffffu];
-        const uint32_t L = rc.x - (T0 + (en >> 16));
-        cq = rc.z & 0x7fffffffu;
-        const bool g0 = L < o0, g1 = L < o1, g2 = L < o2;
-        const bool ne = (L != o0) & (L != o1) & (L != o2);
-        dst = 7;
-        if (S) {
-          if (!g0 & ne) dst = (fl & 1u) ? ((L != of0) ? 0u : 7u) : 6u;
-          else if (g0 & !g1 & ne) dst = 1;
-          else if (g1 & !g2 & ne) dst = 2;
-          else if (g2 & ne & ((fl & 8u) != 0)) dst = 3;
-        } else {
-          if (!g0 & ne) dst = (fl & 1u) ? 0u : 6u;
-          else if (g0 & !g1 & ne) dst = (fl & 2u) ? 4u : 6u;
-          else if (g1 & !g2 & ne) dst = (fl & 4u) ? 5u : 6u;
-          else if (g2 & ne & ((fl & 16u) != 0)) dst = 6;
-        }
-        if (dst < 6) {
-          atomicAdd(&accL[dst][en >> 16], cq);
-          qs.good++;
-        }
+    if (kRetest2) {
+      for (uint32_t d = 0; d < qn; d += 128) {
+        const bool act0 = d + lane < qn, act1 = d + 64 + lane < qn;
+        const uint32_t en0 = act0 ? myQ[d + lane] : 0u, en1 = act1 ? myQ[d + 64 + lane] : 0u;
+        uint32_t cq0, cq1;
+        const uint32_t dst0 = decide(cls, en0, act0, cq0);
+        const uint32_t dst1 = decide(cls, en1, act1, cq1);
+        settle(cls, en0, dst0, cq0);
+        settle(cls, en1, dst1, cq1);
+        if (nSearch >= kTgtS - 128) search();
       }
-      const uint64_t smS = __ballot(dst == 7);
-      if (dst == 7) {
-        const uint32_t rk =
-            __builtin_amdgcn_mbcnt_hi((uint32_t)(smS >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)smS, 0u));
-        myS[nSearch + rk] = en | (S ? 0x80000000u : 0u);
+    } else {
+      for (uint32_t d = 0; d < qn; d += 64) {
+        const bool act = d + lane < qn;
+        const uint32_t en = act ? myQ[d + lane] : 0u;
+        uint32_t cq;
+        const uint32_t dst = decide(cls, en, act, cq);
+        settle(cls, en, dst, cq);
+        if (nSearch >= kTgtS - 64) search();
       }
-      nSearch += (uint32_t)__popcll(smS);
-      if (nSearch >= kTgtS - 64) search();
     }
     __builtin_amdgcn_wave_barrier();
   };
