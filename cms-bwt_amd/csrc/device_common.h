@@ -6,7 +6,14 @@
 namespace cmsbwt {
 
 constexpr int kMaxLevels = 6;   // block-minima levels over LCP (64^6 > 2^32)
-constexpr uint32_t kPoolB = 16; // head records per pool block
+// head records per pool block: 32 (round 6) = a whole 128-byte line of every
+// u32 array the head scatter writes per block, and half the block
+// transitions of the walk (A/B one box, walk kernel 10.78-10.90 ->
+// 10.51-10.54 ms with 16 -> 32; 64 was no better and costs more step time)
+#ifndef CMSBWT_POOL_B
+#define CMSBWT_POOL_B 32
+#endif
+constexpr uint32_t kPoolB = CMSBWT_POOL_B;
 // pool blocks a lane of the uniform-step walk reserves per atomic (it keeps
 // unused ones for its next chunk; blocks never started keep blkMeta.x = ~0)
 constexpr uint32_t kPoolBatch = 16;

@@ -288,10 +288,23 @@ struct Walk2Args {
   unsigned long long* stats;  // STATS builds: per-phase lane-steps, wave-steps, ...
 };
 
-constexpr uint32_t kCoopJ = 4;  // 16-B pieces per thread per cooperative round
+#ifndef CMSBWT_COOP_J
+#define CMSBWT_COOP_J 4
+#endif
+constexpr uint32_t kCoopJ = CMSBWT_COOP_J;  // 16-B pieces per thread per cooperative round
 // pending long extensions served together (r03 A/B, walk kernel: 1 -> 15.12 ms,
 // 4 -> 14.74 ms: a round trip of the wave serves four slots instead of ~2)
-constexpr uint32_t kCoopMin = 4;  // (3: 14.58 ms, 5: 15.6, 6: 16.1, 8: 17.1: pending lanes idle longer)
+// Round 6, re-measured on the current kernel (slot refill, memo; A/B on one
+// box each, bit-exact, walk kernel): 3 -> 11.25-11.36 ms, 4 -> 10.78-10.90,
+// 5 -> 10.69, 6 -> 10.62-10.67, 8 -> 10.39-10.42, 12 -> 10.35-10.48, 16 ->
+// 10.28-10.43; with 32-record pool blocks 8 -> 10.16-10.30, 12 -> 9.92-10.01.
+// A session of the four refilled slots then serves at least twelve
+// extensions, so the wave enters the cooperative loop a third as often.
+// (Round 3, before the refill: 3: 14.58 ms, 4: 14.74, 5: 15.6, 8: 17.1.)
+#ifndef CMSBWT_COOP_MIN
+#define CMSBWT_COOP_MIN 12
+#endif
+constexpr uint32_t kCoopMin = CMSBWT_COOP_MIN;
 // four slots whose ended extensions are replaced by pending lanes within the
 // round loop (CMSBWT_COOP_REFILL=0 builds the fixed groups of four for A/B)
 #ifndef CMSBWT_COOP_REFILL
