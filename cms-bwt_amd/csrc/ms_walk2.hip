@@ -168,6 +168,44 @@ __device__ __forceinline__ void diff16x2(const uint4& x, const uint4& t, uint32_
   }
 }
 
+// Cooperative LCE, per thread: the pieces with a mismatch (pm), and in the
+// first of them (mj) the first mismatch (mine, its chars cc) and, with
+// `two`, the second (mine2, cc2).  The pieces are tested with xors first and
+// only that piece is decoded (one diff instead of one per piece).
+template <uint32_t J>
+__device__ __forceinline__ void first_piece_diff(const uint4 (&xv)[J], const uint4 (&tv)[J], bool two,
+                                                 uint32_t& mine, uint32_t& mj, uint32_t& cc, uint32_t& pm,
+                                                 uint32_t& mine2, uint32_t& cc2) {
+  uint32_t p = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < J; j++) {
+    const uint32_t d = (xv[j].x ^ tv[j].x) | (xv[j].y ^ tv[j].y) | (xv[j].z ^ tv[j].z) | (xv[j].w ^ tv[j].w);
+    p |= (d != 0 ? 1u : 0u) << j;
+  }
+  pm = p;
+  if (p) {
+    // the lowest piece with a mismatch, by priority (a select per piece, so
+    // that no indexed copy of the arrays goes to scratch)
+    uint32_t x0 = xv[J - 1].x, x1 = xv[J - 1].y, x2 = xv[J - 1].z, x3 = xv[J - 1].w;
+    uint32_t t0 = tv[J - 1].x, t1 = tv[J - 1].y, t2 = tv[J - 1].z, t3 = tv[J - 1].w;
+#pragma unroll
+    for (int j = (int)J - 2; j >= 0; j--) {
+      const bool s = (p >> j) & 1u;
+      x0 = s ? xv[j].x : x0; x1 = s ? xv[j].y : x1; x2 = s ? xv[j].z : x2; x3 = s ? xv[j].w : x3;
+      t0 = s ? tv[j].x : t0; t1 = s ? tv[j].y : t1; t2 = s ? tv[j].z : t2; t3 = s ? tv[j].w : t3;
+    }
+    const uint4 x = make_uint4(x0, x1, x2, x3), t = make_uint4(t0, t1, t2, t3);
+    mj = (uint32_t)__builtin_ctz(p);
+    if (two) {
+      diff16x2(x, t, mine, cc, mine2, cc2);
+    } else {
+      uint8_t xc = 0, tc = 0;
+      mine = diff16(x, t, xc, tc);
+      cc = (uint32_t)xc | ((uint32_t)tc << 8);
+    }
+  }
+}
+
 // Level geometry of the LCP block minima, staged in LDS.
 struct Lv {
   const uint32_t* len;  // lvlLen
@@ -305,6 +343,29 @@ constexpr uint32_t kCoopJ = CMSBWT_COOP_J;  // 16-B pieces per thread per cooper
 #define CMSBWT_COOP_MIN 12
 #endif
 constexpr uint32_t kCoopMin = CMSBWT_COOP_MIN;
+// slots of the refilled session (CMSBWT_COOP_SLOTS: 4 slots of 16 threads,
+// 1 KiB per slot per round with kCoopJ = 4; 8 slots of 8 threads, 512 B)
+#ifndef CMSBWT_COOP_SLOTS
+#define CMSBWT_COOP_SLOTS 4
+#endif
+constexpr uint32_t kSlots = CMSBWT_COOP_SLOTS;
+constexpr uint32_t kSlotW = 64 / kSlots;
+static_assert(kSlots == 4 || kSlots == 8 || kSlots == 16, "slots of 16, 8 or 4 threads");
+// a cooperative round tests its pieces with xors and decodes only the first
+// mismatching one (CMSBWT_PIECE_XOR=0: every piece decoded, for A/B)
+#ifndef CMSBWT_PIECE_XOR
+#define CMSBWT_PIECE_XOR 1
+#endif
+constexpr bool kPieceXor = CMSBWT_PIECE_XOR != 0;
+// fused cooperative LCE (CMSBWT_COOP_FUSED=1): the four slots' loads ride
+// in the wave's memory step beside the lanes' own loads, so an extension is
+// compared while the other lanes keep walking, instead of in a session that
+// stops the wave (pending lanes join a free slot at the end of the step)
+#ifndef CMSBWT_COOP_FUSED
+#define CMSBWT_COOP_FUSED 0
+#endif
+constexpr bool kFused = CMSBWT_COOP_FUSED != 0;
+static_assert(!kFused || kSlots == 4, "the fused slots are four of 16 threads");
 // four slots whose ended extensions are replaced by pending lanes within the
 // round loop (CMSBWT_COOP_REFILL=0 builds the fixed groups of four for A/B)
 #ifndef CMSBWT_COOP_REFILL
@@ -481,6 +542,11 @@ k_ms_walk2(Walk2Args A) {
   uint32_t count = 0, blk = 0xffffffffu, blkEnd = 0, fill = kPoolB, seq = 0;
   uint32_t phase = PH_NEXT, use = 0;
   uintptr_t ad0 = X, ad2 = X;
+  // fused cooperative LCE: the slots' lanes (6 bits each), open slots, lanes
+  // held by a slot; per thread: its slot's offset and x / text addresses
+  uint64_t fLs = 0, fSlotted = 0;
+  uint32_t fOpen = 0, fRun = 0;
+  uintptr_t fXa = X, fTa = X;
   // phase-local slots
   int32_t u0 = 0, u1 = 0, u2 = 0, u3 = 0, u4 = 0, u5 = 0, u6 = 0, u7 = 0, u8 = 0;
   uint32_t u9 = 0;
@@ -1004,6 +1070,86 @@ k_ms_walk2(Walk2Args A) {
       v3.x = w.x;
       v3.y = w.y;
     }
+    if (kFused && fOpen) {  // the open slots' pieces, compared in this same memory step
+      const uint32_t g = lane >> 4, k = lane & 15;
+      uint32_t mine = 16, mj = 0, cc = 0, pm = 0, mine2 = 16, cc2 = 0;
+      if ((fOpen >> g) & 1) {
+        uint4 xv[kCoopJ], tv[kCoopJ];
+#pragma unroll
+        for (uint32_t j = 0; j < kCoopJ; j++) {
+          const uint32_t o = fRun + 16 * (k + 16 * j);
+          xv[j] = ldu16(fXa + o);
+          tv[j] = CMSBWT_COOP_TEXT_NT ? ldu16_nt(fTa + o) : ldu16(fTa + o);
+        }
+        first_piece_diff<kCoopJ>(xv, tv, memo, mine, mj, cc, pm, mine2, cc2);
+      }
+      if (STATS && lane == 0) atomicAdd(&sc[31], 1ull);
+      uint64_t mask[kCoopJ], anyM[kCoopJ];
+#pragma unroll
+      for (uint32_t j = 0; j < kCoopJ; j++) {
+        mask[j] = __ballot(mine < 16 && mj == j);
+        anyM[j] = memo ? __ballot((pm >> j) & 1) : 0ull;
+      }
+      uint32_t closed = 0;
+#pragma unroll
+      for (uint32_t q = 0; q < 4; q++) {
+        if (!((fOpen >> q) & 1)) continue;
+        const uint64_t sm = 0xffffull << (16 * q);
+        const uint32_t Lq = (uint32_t)(fLs >> (6 * q)) & 63u;
+#pragma unroll
+        for (uint32_t j = 0; j < kCoopJ; j++) {
+          const uint64_t hit = mask[j] & sm;
+          if (hit) {  // first mismatching byte of slot q: piece j, thread f (as in the session below)
+            const uint32_t f = (uint32_t)__builtin_ctzll(hit);
+            const uint32_t mm = (uint32_t)__shfl((int)mine, (int)f);
+            const uint32_t c2 = (uint32_t)__shfl((int)cc, (int)f);
+            const uint32_t rq = (uint32_t)__shfl((int)fRun, (int)f);
+            uint32_t off2 = rq + 16u * 16u * kCoopJ, c2b = 0;
+            if (memo) {
+              const uint32_t m2f = (uint32_t)__shfl((int)mine2, (int)f);
+              const uint32_t c2f = (uint32_t)__shfl((int)cc2, (int)f);
+              if (m2f < 16) {
+                off2 = rq + 16 * ((f - 16 * q) + 16 * j) + m2f;
+                c2b = c2f | 0x10000u;
+              } else {
+                uint32_t j2 = j, f2 = 64;
+                const uint64_t later = anyM[j] & sm & ~((2ull << f) - 1);
+                if (later) {
+                  f2 = (uint32_t)__builtin_ctzll(later);
+                } else {
+#pragma unroll
+                  for (uint32_t jj = 0; jj < kCoopJ; jj++)
+                    if (jj > j && f2 == 64 && (anyM[jj] & sm)) { j2 = jj; f2 = (uint32_t)__builtin_ctzll(anyM[jj] & sm); }
+                }
+                if (f2 == f) {
+                  off2 = rq + 16 * ((f - 16 * q) + 16 * j2);
+                } else if (f2 < 64) {
+                  off2 = rq + 16 * ((f2 - 16 * q) + 16 * j2) + (uint32_t)__shfl((int)mine, (int)f2);
+                  c2b = (uint32_t)__shfl((int)cc, (int)f2) | 0x10000u;
+                }
+              }
+            }
+            if (lane == Lq) {
+              if (memo) {
+                const uint32_t base = i + len;  // text index of this slot's byte 0
+                amAlign = pos - i;
+                amLo = base + rq + 16 * ((f - 16 * q) + 16 * j) + mm + 1;
+                amFront = base + off2;
+                amC = c2b;
+              }
+              len += rq + 16 * ((f - 16 * q) + 16 * j) + mm;
+              smaller = (int8_t)(uint8_t)c2 > (int8_t)(uint8_t)(c2 >> 8);  // FN:55
+              phase = PC_POST;
+            }
+            closed |= 1u << q;
+            fSlotted &= ~(1ull << Lq);
+            break;
+          }
+        }
+      }
+      fOpen &= ~closed;
+      fRun += 16u * 16u * kCoopJ;
+    }
     // PLCP skip (FN:1176-1185): the exit inside the 16-entry window below
     // the match end, if it is there (skS = the skip, or ~0u)
     uint32_t skS = 0xffffffffu;
@@ -1327,24 +1473,56 @@ k_ms_walk2(Walk2Args A) {
     // (4 KiB for a single lane).  A slot ends at its first mismatch.
     // Pending lanes wait (idle, no load) until kCoopMin of them can share the
     // wave's round trips, unless no other lane of the wave is still walking.
+    if (kFused) {  // pending lanes take the free slots; their pieces load in the next memory step
+      uint64_t pend = __ballot(phase == PH_LCE_COOP) & ~fSlotted;
+      uint32_t fresh = 0;
+      while (pend && fOpen != 15u) {
+        const uint32_t q = (uint32_t)__builtin_ctz(~fOpen & 15u);
+        const uint32_t L = (uint32_t)__builtin_ctzll(pend);
+        pend &= pend - 1;
+        fLs = (fLs & ~(63ull << (6 * q))) | ((uint64_t)L << (6 * q));
+        fSlotted |= 1ull << L;
+        fOpen |= 1u << q;
+        fresh |= 1u << q;
+      }
+      if (fresh) {
+        const uint32_t g = lane >> 4;
+        const uint32_t myL = (uint32_t)(fLs >> (6 * g)) & 63u;
+        const uintptr_t nx = ((uintptr_t)__shfl((uint32_t)(ad0 >> 32), (int)myL) << 32) | __shfl((uint32_t)ad0, (int)myL);
+        const uintptr_t nt = ((uintptr_t)__shfl((uint32_t)(ad2 >> 32), (int)myL) << 32) | __shfl((uint32_t)ad2, (int)myL);
+        if ((fresh >> g) & 1) { fXa = nx; fTa = nt; fRun = 0; }
+      }
+      continue;
+    }
     uint64_t coop = __ballot(phase == PH_LCE_COOP);
     const bool drain = coop == __ballot(phase != PH_DONE);
-    if (kCoopRefill && (uint32_t)__popcll(coop) >= 4 && (drain || (uint32_t)__popcll(coop) >= kCoopMin)) {
-      // Four slots of 16 threads, each with its own offset: a slot whose
+    if (kCoopRefill && (uint32_t)__popcll(coop) >= kSlots && (drain || (uint32_t)__popcll(coop) >= kCoopMin)) {
+      // kSlots slots of kSlotW threads, each with its own offset: a slot whose
       // extension ends takes the next pending lane in the same round trip, so
       // the wave's rounds follow the total length of the extensions instead
       // of the longest of each group of four (r04).
-      uint32_t Ls[4];
+      // the slots' lanes, 6 bits each (wave-uniform; packed so that a slot
+      // index that is not a constant does not put an array in scratch)
+      uint64_t LsP0 = 0, LsP1 = 0;
+      auto ls_get = [&](uint32_t q) -> uint32_t {
+        return (uint32_t)(((q < 8 ? LsP0 : LsP1) >> (6 * (q & 7))) & 63u);
+      };
+      auto ls_set = [&](uint32_t q, uint32_t v) {
+        const uint32_t sh = 6 * (q & 7);
+        if (q < 8) LsP0 = (LsP0 & ~(63ull << sh)) | ((uint64_t)v << sh);
+        else LsP1 = (LsP1 & ~(63ull << sh)) | ((uint64_t)v << sh);
+      };
 #pragma unroll
-      for (uint32_t q = 0; q < 4; q++) {
-        Ls[q] = (uint32_t)__builtin_ctzll(coop);
+      for (uint32_t q = 0; q < kSlots; q++) {
+        ls_set(q, (uint32_t)__builtin_ctzll(coop));
         coop &= coop - 1;
       }
-      const uint32_t g = lane >> 4, k = lane & 15;
-      uint32_t myL = g == 0 ? Ls[0] : g == 1 ? Ls[1] : g == 2 ? Ls[2] : Ls[3];
+      const uint32_t g = lane / kSlotW, k = lane % kSlotW;
+      auto slot_lane = [&]() { return ls_get(g); };
+      uint32_t myL = slot_lane();
       uintptr_t xa = ((uintptr_t)__shfl((uint32_t)(ad0 >> 32), (int)myL) << 32) | __shfl((uint32_t)ad0, (int)myL);
       uintptr_t ta = ((uintptr_t)__shfl((uint32_t)(ad2 >> 32), (int)myL) << 32) | __shfl((uint32_t)ad2, (int)myL);
-      uint32_t runT = 0, open = 15u;
+      uint32_t runT = 0, open = (1u << kSlots) - 1u;
       while (open) {
         uint32_t mine = 16, mj = 0, cc = 0;
         uint32_t pm = 0, mine2 = 16, cc2 = 0;  // (memo) pieces with a mismatch; 2nd mismatch of piece mj
@@ -1352,10 +1530,13 @@ k_ms_walk2(Walk2Args A) {
           uint4 xv[kCoopJ], tv[kCoopJ];
 #pragma unroll
           for (uint32_t j = 0; j < kCoopJ; j++) {
-            const uint32_t o = runT + 16 * (k + (j << 4));
+            const uint32_t o = runT + 16 * (k + j * kSlotW);
             xv[j] = ldu16(xa + o);
             tv[j] = CMSBWT_COOP_TEXT_NT ? ldu16_nt(ta + o) : ldu16(ta + o);
           }
+          if (kPieceXor) {
+            first_piece_diff<kCoopJ>(xv, tv, memo, mine, mj, cc, pm, mine2, cc2);
+          } else {
 #pragma unroll
           for (int j = (int)kCoopJ - 1; j >= 0; j--) {
             if (memo) {
@@ -1368,6 +1549,7 @@ k_ms_walk2(Walk2Args A) {
               if (m < 16) { mine = m; mj = (uint32_t)j; cc = (uint32_t)xc | ((uint32_t)tc << 8); }
             }
           }
+          }
         }
         if (STATS && lane == 0) atomicAdd(&sc[31], 1ull);
         uint64_t mask[kCoopJ], anyM[kCoopJ];
@@ -1378,9 +1560,9 @@ k_ms_walk2(Walk2Args A) {
         }
         uint32_t fresh = 0;  // slots given a new lane this round
 #pragma unroll
-        for (uint32_t q = 0; q < 4; q++) {
+        for (uint32_t q = 0; q < kSlots; q++) {
           if (!((open >> q) & 1)) continue;
-          const uint64_t sm = 0xffffull << (q << 4);
+          const uint64_t sm = (~0ull >> (64 - kSlotW)) << (q * kSlotW);
 #pragma unroll
           for (uint32_t j = 0; j < kCoopJ; j++) {
             const uint64_t hit = mask[j] & sm;
@@ -1392,12 +1574,12 @@ k_ms_walk2(Walk2Args A) {
               // memo: the next mismatch after (piece j, thread f) in byte
               // order (the same piece of f, a later thread's piece j, then
               // a later piece), else the round's end, clean
-              uint32_t off2 = rq + 16u * 16u * kCoopJ, c2b = 0;
+              uint32_t off2 = rq + 16u * kSlotW * kCoopJ, c2b = 0;
               if (memo) {
                 const uint32_t m2f = (uint32_t)__shfl((int)mine2, (int)f);
                 const uint32_t c2f = (uint32_t)__shfl((int)cc2, (int)f);
                 if (m2f < 16) {
-                  off2 = rq + 16 * ((f - (q << 4)) + (j << 4)) + m2f;
+                  off2 = rq + 16 * ((f - q * kSlotW) + j * kSlotW) + m2f;
                   c2b = c2f | 0x10000u;
                 } else {
                   uint32_t j2 = j, f2 = 64;
@@ -1410,27 +1592,27 @@ k_ms_walk2(Walk2Args A) {
                       if (jj > j && f2 == 64 && (anyM[jj] & sm)) { j2 = jj; f2 = (uint32_t)__builtin_ctzll(anyM[jj] & sm); }
                   }
                   if (f2 == f) {  // f's own later piece: its first mismatch there is not kept; clean up to it
-                    off2 = rq + 16 * ((f - (q << 4)) + (j2 << 4));
+                    off2 = rq + 16 * ((f - q * kSlotW) + j2 * kSlotW);
                   } else if (f2 < 64) {  // (f2 != f: its first mismatch is in piece j2, an earlier one would precede (j, f))
-                    off2 = rq + 16 * ((f2 - (q << 4)) + (j2 << 4)) + (uint32_t)__shfl((int)mine, (int)f2);
+                    off2 = rq + 16 * ((f2 - q * kSlotW) + j2 * kSlotW) + (uint32_t)__shfl((int)mine, (int)f2);
                     c2b = (uint32_t)__shfl((int)cc, (int)f2) | 0x10000u;
                   }
                 }
               }
-              if (lane == Ls[q]) {
+              if (lane == ls_get(q)) {
                 if (memo) {
                   const uint32_t base = i + len;  // text index of this slot's byte 0
                   amAlign = pos - i;
-                  amLo = base + rq + 16 * ((f - (q << 4)) + (j << 4)) + mm + 1;
+                  amLo = base + rq + 16 * ((f - q * kSlotW) + j * kSlotW) + mm + 1;
                   amFront = base + off2;
                   amC = c2b;
                 }
-                len += rq + 16 * ((f - (q << 4)) + (j << 4)) + mm;
+                len += rq + 16 * ((f - q * kSlotW) + j * kSlotW) + mm;
                 smaller = (int8_t)(uint8_t)c2 > (int8_t)(uint8_t)(c2 >> 8);  // FN:55
                 phase = PC_POST;
               }
               if (coop) {
-                Ls[q] = (uint32_t)__builtin_ctzll(coop);
+                ls_set(q, (uint32_t)__builtin_ctzll(coop));
                 coop &= coop - 1;
                 fresh |= 1u << q;
               } else {
@@ -1440,9 +1622,9 @@ k_ms_walk2(Walk2Args A) {
             }
           }
         }
-        runT = ((fresh >> g) & 1) ? 0u : runT + 16u * 16u * kCoopJ;
+        runT = ((fresh >> g) & 1) ? 0u : runT + 16u * kSlotW * kCoopJ;
         if (fresh) {
-          myL = g == 0 ? Ls[0] : g == 1 ? Ls[1] : g == 2 ? Ls[2] : Ls[3];
+          myL = slot_lane();
           const uintptr_t nx = ((uintptr_t)__shfl((uint32_t)(ad0 >> 32), (int)myL) << 32) |
                                __shfl((uint32_t)ad0, (int)myL);
           const uintptr_t nt = ((uintptr_t)__shfl((uint32_t)(ad2 >> 32), (int)myL) << 32) |
@@ -1484,6 +1666,10 @@ k_ms_walk2(Walk2Args A) {
             const uint32_t o = run + 16 * (k + (j << lgW));
             xv[j] = ldu16(xa + o);
             tv[j] = CMSBWT_COOP_TEXT_NT ? ldu16_nt(ta + o) : ldu16(ta + o);
+          }
+          if (kPieceXor) {
+            first_piece_diff<JR>(xv, tv, memo, mine, mj, cc, pm, mine2, cc2);
+            return;
           }
 #pragma unroll
           for (int j = (int)JR - 1; j >= 0; j--) {
