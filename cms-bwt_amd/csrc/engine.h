@@ -862,12 +862,12 @@ struct Engine {
   // next Start).  Only ASCII references: there the walk's signed (FN:55) and
   // unsigned orders agree.
   // the paired level-K table (DevRef::pfk) of a DNA reference, from pfx's
-  // level K, with CMSBWT_PFX_PAIR=1 (a walk built with -DCMSBWT_PFX_PAIR=1
-  // probes it; ms_walk2.hip has the measurement)
+  // level K, unless CMSBWT_PFX_PAIR=0 (the walk, built with CMSBWT_PFX_PAIR=1
+  // by default, probes it; ms_walk2.hip has the measurement)
   void build_pfx_pair() {
     R.pfk = nullptr;
     dpfk.release();
-    if (!R.pfx || !R.pfxDna || R.kmerB != 2 || R.kmerK < 2 || R.kmerK > 14 || !env_u32("CMSBWT_PFX_PAIR", 0)) return;
+    if (!R.pfx || !R.pfxDna || R.kmerB != 2 || R.kmerK < 2 || R.kmerK > 14 || !env_u32("CMSBWT_PFX_PAIR", 1)) return;
     dpfk.alloc(16ull << (2 * (R.kmerK - 1)));
     launch_ix_pfx_pair(R.pfx + R.pfxOff[R.kmerK], R.kmerK, dpfk.p, st);
     HIPCHK(hipGetLastError());

@@ -421,11 +421,15 @@ constexpr bool kMemoCheck = CMSBWT_MEMO_CHECK != 0;
 // Measured (config 3, one box, bit-exact): L2 -> fabric read requests 286 M
 // -> 250 M per launch, walk kernel 10.73-10.86 -> 10.65-10.82 ms (within the
 // box's spread), with non-temporal probe loads 10.95-11.03 ms: the walk is
-// not bound by its random lines.  Off by default
-// (the table costs 4.3 GB); -DCMSBWT_PFX_PAIR=1 builds it, CMSBWT_PFX_PAIR=1
-// builds the table.
+// not bound by its random lines.  Re-measured on
+// the final configuration (cooperative sessions from 12 lanes, 32-record
+// blocks; one box, two runs each, bit-exact): walk kernel 9.97-10.06 ->
+// 9.83-9.93 ms (the prefetch alone, without the pairs: 10.42-10.54), so it
+// is on: the table costs 4.3 GB of HBM at K = 14.  The environment switch
+// CMSBWT_PFX_PAIR=0 skips the table (the walk then prefetches unpaired);
+// -DCMSBWT_PFX_PAIR=0 builds the walk without either.
 #ifndef CMSBWT_PFX_PAIR
-#define CMSBWT_PFX_PAIR 0
+#define CMSBWT_PFX_PAIR 1
 #endif
 // the paired probes as cached loads (non-temporal loads of one line do not
 // share a fabric request)

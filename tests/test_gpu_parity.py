@@ -220,14 +220,16 @@ def test_run_bucket_bins(engine, oracle, tmp_path, case, geom):
 
 
 @pytest.mark.parametrize("env", [{"CMSBWT_PFX_GENERIC": "1"}, {"CMSBWT_KMER_BITS": "12"}, {"CMSBWT_PFX": "0"},
-                                 {"CMSBWT_PFX_GENERIC": "1", "CMSBWT_CHUNK": "100"}],
-                         ids=["generic_symbol_map", "short_tables", "no_tables", "generic_tiny_chunks"])
+                                 {"CMSBWT_PFX_GENERIC": "1", "CMSBWT_CHUNK": "100"}, {"CMSBWT_PFX_PAIR": "0"}],
+                         ids=["generic_symbol_map", "short_tables", "no_tables", "generic_tiny_chunks",
+                              "unpaired_prefetch"])
 @pytest.mark.parametrize("case", cases.small_cases()[:6] + cases.small_cases()[-3:], ids=lambda c: c[0])
 def test_walk_table_paths(engine, oracle, tmp_path, case, env):
     """The walk's ways to the next character give the same heads: answer
     entries with the ACGT decode or the generic byte map, short tables (more
     heads at depth >= K: child table and binary searches), no tables at all
-    (binary searches and adjustInterval scans only), and many restarts."""
+    (binary searches and adjustInterval scans only), many restarts, and the
+    probe prefetch without the paired level-K table (CMSBWT_PFX_PAIR=0)."""
     _compare(engine, oracle, tmp_path, case, env=env)
 
 

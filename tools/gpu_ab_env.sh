@@ -12,6 +12,6 @@ for rep in 1 2; do
     rc=$?
     if [ $rc = 1 ]; then echo "[$e] FAILED: $(tail -1 gpurun_out/abe_$k.log)"; continue; fi
     [ $rc = 0 ] || { tail -30 gpurun_out/abe_$k.log; exit 1; }
-    echo "[$e] $(tail -1 gpurun_out/abe_$k.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); s=d["stages_ms"]; print("step", d["ms_per_step"], "walk stage", s["ms_walk"], "counter", s["counter_kernel"], "merge", s["merge"], d["parity"]["verdict"])')"
+    echo "[$e] $(tail -1 gpurun_out/abe_$k.log | python -c 'import json,sys; d=json.loads(sys.stdin.read()); s=d["stages_ms"]; print("step", d["ms_per_step"], "walk stage", s["ms_walk"], "walk", s["ms_walk_kernel"], "counter", s["counter_kernel"], "merge", s["merge"], d["parity"]["verdict"])')"
   done
 done
