@@ -393,6 +393,18 @@ constexpr bool kProbeNoSkip = CMSBWT_PROBE_NOSKIP != 0;
 #define CMSBWT_ALIGN_MEMO 1
 #endif
 constexpr bool kAlignMemo = CMSBWT_ALIGN_MEMO != 0;
+// the memo's four words per lane in LDS instead of registers: read when an
+// extension starts, written when a cooperative extension ends; four VGPRs
+// fewer across the step loop.  With the paired probes' prefetch the
+// specialised instance spilled five VGPRs to scratch (writes of the launch
+// 1.85 -> 2.41 GB); without the spills (A/B one box, two runs each,
+// bit-exact): walk kernel 10.01-10.02 -> 9.18-9.22 ms.  LDS per block
+// 33.1 -> 37.2 KB (four blocks per CU still fit).  CMSBWT_MEMO_LDS=0 keeps
+// them in registers
+#ifndef CMSBWT_MEMO_LDS
+#define CMSBWT_MEMO_LDS 1
+#endif
+constexpr bool kMemoLds = CMSBWT_MEMO_LDS != 0;
 // diagnostic builds (CMSBWT_MEMO_CHECK=1): a memo hit only predicts; the LCE
 // runs as without the memo and the result is compared with the prediction
 // (and the predicted match end with the reference and text bounds); the
@@ -479,6 +491,8 @@ k_ms_walk2(Walk2Args A) {
   __shared__ uint32_t lvlL[2 * kMaxLevels];
   __shared__ uint32_t pfxL[17];
   __shared__ uint4 hbuf[kHeadBuf ? kHeadBufN : 1][256];  // 16 B x kHeadBufN per lane (slot-major: no bank conflicts)
+  __shared__ uint4 memoL[kMemoLds ? 256 : 1];  // (CMSBWT_MEMO_LDS) amAlign, amLo, amFront, amC per lane
+  if (kMemoLds) memoL[threadIdx.x] = make_uint4(0u, 0xffffffffu, 0u, 0u);
   if (STATS && threadIdx.x < 32) sc[threadIdx.x] = 0;
   if (A.R.pfx) kmapL[threadIdx.x] = A.R.kmap[threadIdx.x];  // blockDim == 256
   if (threadIdx.x < 17) pfxL[threadIdx.x] = A.R.pfxOff[threadIdx.x];
@@ -753,6 +767,13 @@ k_ms_walk2(Walk2Args A) {
   // FN:52-62 from (pos, len): 16 bytes of x and of the text, unless the
   // alignment memo already knows where this offset's match ends
   auto start_lce = [&]() {
+    if (kMemoLds && memo) {
+      const uint4 m = memoL[threadIdx.x];
+      amAlign = m.x;
+      amLo = m.y;
+      amFront = m.z;
+      amC = m.w;
+    }
     if (memo && pos - i == amAlign && i + len >= amLo && i + len <= amFront) {
       if (kMemoCheck) {  // predict only; the LCE below runs and PC_POST compares
         chkOn = 1;
@@ -880,6 +901,7 @@ k_ms_walk2(Walk2Args A) {
           twAt = 0xffffffffu;
           t32At = 0xfffffff0u;  // (another document's bytes)
           amLo = 0xffffffffu;
+          if (kMemoLds) memoL[threadIdx.x].y = 0xffffffffu;
           pfAt = 0xffffffffu;
           if (hasPfx) {
             phase = PH_PFX_TEXT;
@@ -1140,6 +1162,7 @@ k_ms_walk2(Walk2Args A) {
                 amLo = base + rq + 16 * ((f - 16 * q) + 16 * j) + mm + 1;
                 amFront = base + off2;
                 amC = c2b;
+                if (kMemoLds) memoL[threadIdx.x] = make_uint4(amAlign, amLo, amFront, amC);
               }
               len += rq + 16 * ((f - 16 * q) + 16 * j) + mm;
               smaller = (int8_t)(uint8_t)c2 > (int8_t)(uint8_t)(c2 >> 8);  // FN:55
@@ -1610,6 +1633,7 @@ k_ms_walk2(Walk2Args A) {
                   amLo = base + rq + 16 * ((f - q * kSlotW) + j * kSlotW) + mm + 1;
                   amFront = base + off2;
                   amC = c2b;
+                  if (kMemoLds) memoL[threadIdx.x] = make_uint4(amAlign, amLo, amFront, amC);
                 }
                 len += rq + 16 * ((f - q * kSlotW) + j * kSlotW) + mm;
                 smaller = (int8_t)(uint8_t)c2 > (int8_t)(uint8_t)(c2 >> 8);  // FN:55
@@ -1746,6 +1770,7 @@ k_ms_walk2(Walk2Args A) {
                   amLo = base + run + 16 * ((f - (q << lgW)) + (j << lgW)) + mm + 1;
                   amFront = base + off2;
                   amC = c2b;
+                  if (kMemoLds) memoL[threadIdx.x] = make_uint4(amAlign, amLo, amFront, amC);
                 }
                 len += run + 16 * ((f - (q << lgW)) + (j << lgW)) + mm;
                 smaller = (int8_t)(uint8_t)c2 > (int8_t)(uint8_t)(c2 >> 8);  // FN:55
