@@ -405,6 +405,14 @@ constexpr bool kAlignMemo = CMSBWT_ALIGN_MEMO != 0;
 #define CMSBWT_MEMO_LDS 1
 #endif
 constexpr bool kMemoLds = CMSBWT_MEMO_LDS != 0;
+// the chunk id and pool-block sequence of each lane in LDS (used when a pool
+// block starts and when the chunk ends): two VGPRs fewer (CMSBWT_CHUNK_LDS;
+// A/B one box, bit-exact: walk kernel 9.20-9.25 vs 9.02-9.28 ms, no change
+// once nothing spills, so it stays off)
+#ifndef CMSBWT_CHUNK_LDS
+#define CMSBWT_CHUNK_LDS 0
+#endif
+constexpr bool kChunkLds = CMSBWT_CHUNK_LDS != 0;
 // diagnostic builds (CMSBWT_MEMO_CHECK=1): a memo hit only predicts; the LCE
 // runs as without the memo and the result is compared with the prediction
 // (and the predicted match end with the reference and text bounds); the
@@ -493,6 +501,7 @@ k_ms_walk2(Walk2Args A) {
   __shared__ uint4 hbuf[kHeadBuf ? kHeadBufN : 1][256];  // 16 B x kHeadBufN per lane (slot-major: no bank conflicts)
   __shared__ uint4 memoL[kMemoLds ? 256 : 1];  // (CMSBWT_MEMO_LDS) amAlign, amLo, amFront, amC per lane
   if (kMemoLds) memoL[threadIdx.x] = make_uint4(0u, 0xffffffffu, 0u, 0u);
+  __shared__ uint2 chunkL[kChunkLds ? 256 : 1];  // (CMSBWT_CHUNK_LDS) cid, seq per lane
   if (STATS && threadIdx.x < 32) sc[threadIdx.x] = 0;
   if (A.R.pfx) kmapL[threadIdx.x] = A.R.kmap[threadIdx.x];  // blockDim == 256
   if (threadIdx.x < 17) pfxL[threadIdx.x] = A.R.pfxOff[threadIdx.x];
@@ -888,6 +897,7 @@ k_ms_walk2(Walk2Args A) {
         count = 0;
         fill = kPoolB;
         seq = 0;
+        if (kChunkLds) chunkL[threadIdx.x] = make_uint2(cid, 0u);
         i = a > 0 ? a - 1 : 0;
         if (i >= b) {
           A.chunkCount[cid] = 0;  // empty document: refills next iteration
@@ -976,8 +986,14 @@ k_ms_walk2(Walk2Args A) {
         if (fill == kPoolB) {
           blk++;
           fill = 0;
+          if (kChunkLds) {
+            const uint2 cs = chunkL[threadIdx.x];
+            cid = cs.x;
+            seq = cs.y;
+          }
           if (blk < A.pool.capBlocks) A.pool.blkMeta[blk] = make_uint2(cid, seq);  // (one 8-byte store)
           seq++;
+          if (kChunkLds) chunkL[threadIdx.x].y = seq;
         }
         if (kHeadBuf) {
           constexpr uint32_t M = kHeadBufN - 1;
@@ -1036,6 +1052,7 @@ k_ms_walk2(Walk2Args A) {
       i++;
       prevPos = pos;
       if (i >= b) {
+        if (kChunkLds) cid = chunkL[threadIdx.x].x;
         A.chunkCount[cid] = count;
         phase = PH_NEXT;
         use = 0;
