@@ -14,6 +14,17 @@ constexpr int kMaxLevels = 6;   // block-minima levels over LCP (64^6 > 2^32)
 #define CMSBWT_POOL_B 32
 #endif
 constexpr uint32_t kPoolB = CMSBWT_POOL_B;
+// the walk records each head's BWT character (the text byte before it) in
+// its record when the lane's sliding window just held it (HeadRec.flags bits
+// 8..15, bit 16 = known); k_finalize then reads the text only for the others
+// (CMSBWT_WALK_LCHAR, one setting for every translation unit).  Measured
+// (round 6, A/B one box, bit-exact, 356 parity tests green): walk stage
+// 12.32-12.47 -> 12.64-12.70 ms, the walk's LDS writes cost more than the
+// text lines k_finalize no longer streams; off
+#ifndef CMSBWT_WALK_LCHAR
+#define CMSBWT_WALK_LCHAR 0
+#endif
+constexpr bool kWalkLchar = CMSBWT_WALK_LCHAR != 0;
 // pool blocks a lane of the uniform-step walk reserves per atomic (it keeps
 // unused ones for its next chunk; blocks never started keep blkMeta.x = ~0)
 constexpr uint32_t kPoolBatch = 16;

@@ -37,6 +37,9 @@ __global__ void k_scatter_heads(Pool pool, uint32_t blocksUsed, const uint32_t* 
   h.pos[idx] = r.pos;
   h.len[idx] = r.len;
   h.smaller[idx] = (uint8_t)(r.flags & 1u);
+  // (CMSBWT_WALK_LCHAR) the BWT character when the walk had it: 0x100 | byte,
+  // or 0; parked in tonext, which k_finalize reads before writing it
+  if (kWalkLchar) h.tonext[idx] = r.flags >> 8;
   // (the BWT character before the phrase is read by k_finalize, whose
   // document-ordered threads read the text lines coalesced)
   hdoc[idx] = chunks[cid].doc;
@@ -82,6 +85,7 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
     h.nexthead[i] = 0;
     return;
   }
+  const uint32_t lk = kWalkLchar ? h.tonext[i] : 0u;  // the walk's BWT character (0x100 | byte) or 0
   const uint32_t lo = hdoc[i];  // document of i (written by the scatter)
   const uint32_t de = docEndIdx[lo];
   const uint32_t si = h.start[i];
@@ -116,7 +120,10 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
   // on the host), MatchInSet::operator< is a strict weak order on every
   // position's keys and queries.
   const uint8_t* dt = text + docOff[lo];
-  {
+  // (CMSBWT_WALK_LCHAR) t[ei] lies in head j's match when sj <= ei (ei < sj +
+  // len_j by the search) and then equals x[q] by that match: the text is read
+  // only for the others
+  if (!kWalkLchar || sj > ei || h.len[j] == 0) {
     const uint8_t c = dt[ei];
     const uint8_t xq = isax ? (uint8_t)(ix >> 24) : R.x[q];
     if (!(c == xq || (c == kSep && q == R.n - 1))) atomicOr(errFlags, 8u);
@@ -124,7 +131,7 @@ __global__ void k_finalize(DevRef R, HeadsSoA h, uint32_t H, const uint32_t* __r
   // BWT character of the phrase (FN:1158-1161): the text byte before it, 0x02
   // at a document start.  Read here rather than in k_scatter_heads: heads are
   // in document order, so a wave reads the same text lines as for the check.
-  h.lchar[i] = si == 0 ? (uint8_t)kSep : dt[si - 1];
+  h.lchar[i] = si == 0 ? (uint8_t)kSep : (lk & 0x100u) ? (uint8_t)lk : dt[si - 1];
   h.nexthead[i] = (uint16_t)(j - i);
   if ((uint64_t)h.pos[i] + (s1 - si) > R.n) atomicOr(errFlags, 4u);
 }

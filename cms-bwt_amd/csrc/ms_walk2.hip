@@ -502,6 +502,10 @@ k_ms_walk2(Walk2Args A) {
   __shared__ uint4 memoL[kMemoLds ? 256 : 1];  // (CMSBWT_MEMO_LDS) amAlign, amLo, amFront, amC per lane
   if (kMemoLds) memoL[threadIdx.x] = make_uint4(0u, 0xffffffffu, 0u, 0u);
   __shared__ uint2 chunkL[kChunkLds ? 256 : 1];  // (CMSBWT_CHUNK_LDS) cid, seq per lane
+  // (CMSBWT_WALK_LCHAR) per lane: a text index and its byte, the first byte of
+  // the last window that a window one position further replaced
+  __shared__ uint2 prevL[kWalkLchar ? 256 : 1];
+  if (kWalkLchar) prevL[threadIdx.x] = make_uint2(0xffffffffu, 0u);
   if (STATS && threadIdx.x < 32) sc[threadIdx.x] = 0;
   if (A.R.pfx) kmapL[threadIdx.x] = A.R.kmap[threadIdx.x];  // blockDim == 256
   if (threadIdx.x < 17) pfxL[threadIdx.x] = A.R.pfxOff[threadIdx.x];
@@ -597,6 +601,7 @@ k_ms_walk2(Walk2Args A) {
   };
   // a new text window at `at`: codes of its leading symbols (at most K)
   auto set_window = [&](const uint4 v, uint32_t at) {
+    if (kWalkLchar && twAt != 0xffffffffu && twAt + 1 == at) prevL[threadIdx.x] = make_uint2(twAt, tw.x & 0xffu);
     tw = v;
     twAt = at;
     const uint32_t K = R.kmerK, Bb = R.kmerB;
@@ -910,6 +915,7 @@ k_ms_walk2(Walk2Args A) {
           smaller = false;
           twAt = 0xffffffffu;
           t32At = 0xfffffff0u;  // (another document's bytes)
+          if (kWalkLchar) prevL[threadIdx.x].x = 0xffffffffu;
           amLo = 0xffffffffu;
           if (kMemoLds) memoL[threadIdx.x].y = 0xffffffffu;
           pfAt = 0xffffffffu;
@@ -983,6 +989,12 @@ k_ms_walk2(Walk2Args A) {
         }
       }
       if (head) {
+        // flags: smaller, and the byte before the head when the window gave it
+        uint32_t hflags = smaller ? 1u : 0u;
+        if (kWalkLchar) {
+          const uint2 pv = prevL[threadIdx.x];
+          if (i > 0 && pv.x == i - 1) hflags |= (0x100u | pv.y) << 8;
+        }
         if (fill == kPoolB) {
           blk++;
           fill = 0;
@@ -997,7 +1009,7 @@ k_ms_walk2(Walk2Args A) {
         }
         if (kHeadBuf) {
           constexpr uint32_t M = kHeadBufN - 1;
-          hbuf[fill & M][threadIdx.x] = make_uint4(i, pos, len, smaller ? 1u : 0u);
+          hbuf[fill & M][threadIdx.x] = make_uint4(i, pos, len, hflags);
           if ((fill & M) == M && blk < A.pool.capBlocks) {  // a full piece of the block
             uint4* dst = (uint4*)(A.pool.rec + (uint64_t)blk * kPoolB + (fill - M));
 #pragma unroll
@@ -1008,7 +1020,7 @@ k_ms_walk2(Walk2Args A) {
           r.start = i;
           r.pos = pos;
           r.len = len;
-          r.flags = smaller ? 1u : 0u;
+          r.flags = hflags;
           A.pool.rec[(uint64_t)blk * kPoolB + fill] = r;
         }
         fill++;
