@@ -494,6 +494,12 @@ static_assert(sizeof(HeadRec) == sizeof(uint4), "head records are stored as uint
 template <bool STATS, bool FAST>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(CMSBWT_W2_WAVES, 8)))
 k_ms_walk2(Walk2Args A) {
+  // four blocks of 256 lanes per CU (four waves per SIMD) need <= 40 KB of
+  // LDS per block: the per-lane arrays below must fit beside each other
+  static_assert((kHeadBuf ? kHeadBufN : 1) * 256 * 16 + (kMemoLds ? 256 : 1) * 16 + (kChunkLds ? 256 : 1) * 8 +
+                        (kWalkLchar ? 256 : 1) * 8 + 32 * 8 + 256 + 2 * kMaxLevels * 4 + 17 * 4 <=
+                    160 * 1024 / 4,
+                "walk LDS per block exceeds a quarter of the CU's 160 KB");
   __shared__ unsigned long long sc[STATS ? 32 : 1];
   __shared__ uint8_t kmapL[256];
   __shared__ uint32_t lvlL[2 * kMaxLevels];
